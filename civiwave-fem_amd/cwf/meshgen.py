@@ -1,0 +1,98 @@
+"""Synthetic tet meshes for the benchmark configurations.
+
+Structured hex blocks with lexicographic node numbering (i fastest) where every hex is
+split into 6 conforming Kuhn tetrahedra (local cube corners {0,1,3,7},{0,1,5,7},
+{0,2,3,7},{0,2,6,7},{0,4,5,7},{0,4,6,7}, corner bit pattern (i,j,k)). The reference
+solver accepts tet4 only (src/mesh/preprocess.cpp:326-330), so a "hex8 block" config
+is carried by this expansion. Coordinates are computed as ``h * i`` in float64, the
+same expression the survey's reference drivers used.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+KUHN = np.array([[0, 1, 3, 7], [0, 1, 5, 7], [0, 2, 3, 7], [0, 2, 6, 7], [0, 4, 5, 7], [0, 4, 6, 7]], np.int64)
+
+
+@dataclass
+class TetMesh:
+    coords: np.ndarray  # f64 [N,3]
+    tets: np.ndarray  # u32 [E,4]
+    node_groups: dict = field(default_factory=dict)  # name -> u32 node indices
+    shape: tuple | None = None  # (nx, ny, nz) hexes for structured blocks
+
+    @property
+    def node_count(self) -> int:
+        return self.coords.shape[0]
+
+    @property
+    def element_count(self) -> int:
+        return self.tets.shape[0]
+
+
+def kuhn_block(nx: int, ny: int, nz: int, h: float = 1.0) -> TetMesh:
+    """nx*ny*nz hexes -> 6*nx*ny*nz tets; groups FIXED (x=0 face) and TIP (x=max face)."""
+    A, B, Cn = nx + 1, ny + 1, nz + 1
+    k, j, i = np.meshgrid(np.arange(Cn), np.arange(B), np.arange(A), indexing="ij")
+    if h == 1.0:
+        coords = np.stack([i, j, k], -1).reshape(-1, 3).astype(np.float64)
+    else:
+        coords = np.stack([h * i.astype(np.float64), h * j.astype(np.float64), h * k.astype(np.float64)],
+                          -1).reshape(-1, 3)
+    hk, hj, hi = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    hk, hj, hi = hk.reshape(-1), hj.reshape(-1), hi.reshape(-1)
+    corners = np.empty((hk.size, 8), np.int64)
+    for b in range(8):
+        corners[:, b] = ((hk + ((b >> 2) & 1)) * B + (hj + ((b >> 1) & 1))) * A + (hi + (b & 1))
+    tets = corners[:, KUHN].reshape(-1, 4).astype(np.uint32)
+    kk, jj = np.meshgrid(np.arange(Cn), np.arange(B), indexing="ij")
+    fixed = ((kk * B + jj) * A).reshape(-1).astype(np.uint32)
+    tip = ((kk * B + jj) * A + nx).reshape(-1).astype(np.uint32)
+    return TetMesh(coords, tets, {"FIXED": fixed, "TIP": tip,
+                                  "CORNER": np.array([(nz * B + ny) * A + nx], np.uint32)}, (nx, ny, nz))
+
+
+def jitter_and_permute(mesh: TetMesh, h: float, jitter: float = 0.15, seed_jitter: int = 12345,
+                       seed_perm: int = 42) -> TetMesh:
+    """C4: jitter interior nodes by +-jitter*h and randomly permute node/element order.
+
+    Boundary nodes (on the block faces) are kept on their face so the group definitions
+    stay meaningful. A deterministic numpy PCG64 stream is used.
+    """
+    rng = np.random.Generator(np.random.PCG64(seed_jitter))
+    c = mesh.coords.copy()
+    lo, hi = c.min(0), c.max(0)
+    interior = np.all((c > lo + 1e-9) & (c < hi - 1e-9), axis=1)
+    c[interior] += rng.uniform(-jitter * h, jitter * h, size=(int(interior.sum()), 3))
+    prng = np.random.Generator(np.random.PCG64(seed_perm))
+    node_perm = prng.permutation(mesh.node_count)  # new index -> old index
+    old_to_new = np.empty_like(node_perm)
+    old_to_new[node_perm] = np.arange(node_perm.size)
+    elem_perm = prng.permutation(mesh.element_count)
+    tets = old_to_new[mesh.tets.astype(np.int64)][elem_perm].astype(np.uint32)
+    groups = {k: np.sort(old_to_new[v.astype(np.int64)]).astype(np.uint32) for k, v in mesh.node_groups.items()}
+    return TetMesh(c[node_perm], tets, groups, None)
+
+
+def single_tet() -> TetMesh:
+    """The reference test fixture (tests/pcg_test.cpp:35-74): unit tet, base face fixed."""
+    coords = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], np.float64)
+    tets = np.array([[0, 1, 2, 3]], np.uint32)
+    return TetMesh(coords, tets, {"FIXED": np.array([0, 1, 2], np.uint32), "POINT": np.array([3], np.uint32)})
+
+
+# BASELINE.json configs
+CONFIGS = {
+    "c1": dict(name="cantilever 20x5x10 hex (Kuhn tets)", shape=(20, 5, 10), h=0.1, xi=0.02, w=(5.0, 50.0),
+               tol=2e-4),
+    "c2": dict(name="cube 69^3 hex (Kuhn tets), 1.03M DOF", shape=(69, 69, 69), h=0.1, xi=0.02, w=(5.0, 50.0),
+               tol=3e-4),
+    "c3": dict(name="cube 149^3 hex (Kuhn tets), 10.1M DOF, Rayleigh", shape=(149, 149, 149), h=0.1, xi=0.05,
+               w=(10.0, 100.0), tol=3e-4),
+    "c4": dict(name="jittered/permuted 118^3 hex (Kuhn tets), 5.06M DOF", shape=(118, 118, 118), h=0.1, xi=0.02,
+               w=(5.0, 50.0), tol=3e-4, jitter=True),
+    "c5": dict(name="slab 800x400x50 hex (Kuhn tets), 49.1M DOF", shape=(800, 400, 50), h=0.1, xi=0.02,
+               w=(5.0, 50.0), tol=3e-4),
+}

@@ -1,0 +1,1014 @@
+/*
+ * cwf_oracle.c -- CPU restatement of CiviWave-FEM's matrix-free Newmark/PCG hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline -- never as the product path.
+ *
+ * Every function restates the reference arithmetic in the exact fold order of
+ * /root/reference (cited file:line), so that a build with `-O2 -ffp-contract=off`
+ * reproduces the reference bit for bit:
+ *   - fp32 x fp32 products are exact in fp64;
+ *   - every sum is a left fold in the reference order;
+ *   - structural zeros of the B matrix are skipped: 0*u = +-0 and a running sum that
+ *     starts at +0.0 is never -0.0, so adding +-0 is an exact no-op (finite inputs).
+ *
+ * Pinning: the outputs are checked in tests/test_oracle_pins.py against the reference's
+ * own test fixtures (tests/pcg_test.cpp, physics_test.cpp, preprocess_test.cpp) and the
+ * reference outputs recorded in SURVEY.md section 8c (single tet apply_keff, 1-iteration
+ * PCG, and the n=16 Kuhn block solve: 162 iterations, |r| = 0.14640172515227148,
+ * FNV-1a(x) = f10c27935f2e7a58).
+ */
+#include <math.h>
+#include <stdio.h>
+#include <float.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cwf_oracle.h"
+
+#define UNUSED_SLOT 0xFFFFFFFFu
+
+static char g_msg[256];
+static char g_ctx[256];
+
+const char *orc_last_message(void) { return g_msg; }
+const char *orc_last_context(void) { return g_ctx; }
+
+static int fail(int code, const char *msg, const char *ctx)
+{
+    strncpy(g_msg, msg, sizeof g_msg - 1);
+    g_msg[sizeof g_msg - 1] = 0;
+    strncpy(g_ctx, ctx ? ctx : "", sizeof g_ctx - 1);
+    g_ctx[sizeof g_ctx - 1] = 0;
+    return code;
+}
+
+/* ------------------------------------------------------------------------- */
+/* scalars: materials.hpp:116-155, newmark.cpp:34-81                         */
+/* ------------------------------------------------------------------------- */
+
+void orc_make_stiffness(double E, double nu, double *D36)
+{
+    /* materials.hpp:116-122 compute_lame */
+    const double denom = (1.0 + nu) * (1.0 - 2.0 * nu);
+    const double lambda = (nu * E) / denom;
+    const double mu = E / (2.0 * (1.0 + nu));
+    /* materials.hpp:124-134 make_stiffness_matrix */
+    const double c = lambda + 2.0 * mu;
+    const double D[36] = {c, lambda, lambda, 0, 0, 0, lambda, c, lambda, 0, 0, 0, lambda, lambda, c, 0, 0, 0,
+                          0, 0, 0, mu, 0, 0, 0, 0, 0, 0, mu, 0, 0, 0, 0, 0, 0, mu};
+    memcpy(D36, D, sizeof D);
+}
+
+void orc_rayleigh(double xi, double w1, double w2, double *alpha, double *beta)
+{
+    /* materials.hpp:149-155 compute_rayleigh */
+    const double denom = w1 + w2;
+    *alpha = 2.0 * xi * w1 * w2 / denom;
+    *beta = 2.0 * xi / denom;
+}
+
+void orc_newmark_coefficients(double dt, double beta, double gamma, double *a /*a0..a5*/, double *upd /*2*/)
+{
+    /* newmark.cpp:34-47 make_coefficients */
+    a[0] = 1.0 / (beta * dt * dt);
+    a[1] = gamma / (beta * dt);
+    a[2] = 1.0 / (beta * dt);
+    a[3] = (1.0 / (2.0 * beta)) - 1.0;
+    a[4] = (gamma / beta) - 1.0;
+    a[5] = dt * ((gamma / (2.0 * beta)) - 1.0);
+    /* newmark.cpp:73-81 compute_update_scalars */
+    const double beta_dt = beta * dt;
+    upd[0] = 1.0 / (beta * dt * dt);
+    upd[1] = gamma / beta_dt;
+}
+
+/* ------------------------------------------------------------------------- */
+/* preprocess: preprocess.cpp:268-405 + pack.cpp:41-57,176-200               */
+/* ------------------------------------------------------------------------- */
+
+static void sub3(const double *a, const double *b, double *o)
+{
+    o[0] = a[0] - b[0];
+    o[1] = a[1] - b[1];
+    o[2] = a[2] - b[2];
+}
+
+static void cross3(const double *l, const double *r, double *o)
+{
+    /* math.hpp:124-128 */
+    o[0] = (l[1] * r[2]) - (l[2] * r[1]);
+    o[1] = (l[2] * r[0]) - (l[0] * r[2]);
+    o[2] = (l[0] * r[1]) - (l[1] * r[0]);
+}
+
+static double dot3(const double *l, const double *r)
+{
+    /* math.hpp:89-92 */
+    return (l[0] * r[0]) + (l[1] * r[1]) + (l[2] * r[2]);
+}
+
+static float safe_f32(double v)
+{
+    /* pack.cpp:41-57 safe_cast_double_to_float */
+    if (!isfinite(v))
+        return v > 0 ? INFINITY : (v < 0 ? -INFINITY : NAN);
+    if (v > (double)FLT_MAX)
+        return FLT_MAX;
+    if (v < -(double)FLT_MAX)
+        return -FLT_MAX;
+    return (float)v;
+}
+
+int orc_preprocess_tets(uint64_t node_count, uint64_t element_count, const double *coords, const uint32_t *tets,
+                        const uint32_t *material_index, const double *density, float *grads24, float *volume,
+                        double *mass64, float *mass32, uint32_t *offsets, uint32_t *adj_elem, uint8_t *adj_local,
+                        uint32_t *conn8)
+{
+    /* preprocess.cpp:284-405: only the arithmetic path (group / duplicate checks are host validation) */
+    for (uint64_t n = 0; n < node_count; ++n)
+        mass64[n] = 0.0;
+    uint32_t *counts = (uint32_t *)calloc(node_count ? node_count : 1, sizeof(uint32_t));
+    if (!counts)
+        return fail(ORC_ERR_ALLOC, "allocation failed", "");
+    for (uint64_t e = 0; e < element_count; ++e)
+    {
+        const double *p[4];
+        for (int a = 0; a < 4; ++a)
+        {
+            const uint32_t n = tets[e * 4 + a];
+            if (n >= node_count)
+            {
+                free(counts);
+                return fail(ORC_ERR_NODE_RANGE, "element references node out of range", "");
+            }
+            p[a] = coords + 3 * (uint64_t)n;
+            ++counts[n];
+        }
+        double e0[3], e1[3], e2[3], c12[3];
+        sub3(p[1], p[0], e0);
+        sub3(p[2], p[0], e1);
+        sub3(p[3], p[0], e2);
+        cross3(e1, e2, c12);
+        const double volume6 = dot3(e0, c12);
+        const double vol = fabs(volume6) / 6.0;
+        if (vol <= DBL_EPSILON)
+        {
+            free(counts);
+            return fail(ORC_ERR_VOLUME, "tetrahedron volume non-positive", "");
+        }
+        /* compute_tet_gradients preprocess.cpp:268-280 */
+        const double inv6 = -1.0 / volume6;
+        double a0[3], b0[3], g[4][3];
+        sub3(p[2], p[1], a0);
+        sub3(p[3], p[1], b0);
+        cross3(a0, b0, g[0]);
+        sub3(p[3], p[0], a0);
+        sub3(p[2], p[0], b0);
+        cross3(a0, b0, g[1]);
+        sub3(p[1], p[0], a0);
+        sub3(p[3], p[0], b0);
+        cross3(a0, b0, g[2]);
+        sub3(p[2], p[0], a0);
+        sub3(p[1], p[0], b0);
+        cross3(a0, b0, g[3]);
+        for (int a = 0; a < 8; ++a)
+            for (int k = 0; k < 3; ++k)
+                grads24[e * 24 + a * 3 + k] = a < 4 ? safe_f32(g[a][k] * inv6) : 0.0f;
+        volume[e] = safe_f32(vol);
+        const double lump = density[material_index[e]] * vol / 4.0;
+        for (int a = 0; a < 4; ++a)
+            mass64[tets[e * 4 + a]] += lump;
+        if (conn8)
+            for (int a = 0; a < 8; ++a)
+                conn8[e * 8 + a] = a < 4 ? tets[e * 4 + a] : UNUSED_SLOT;
+    }
+    uint32_t acc = 0;
+    for (uint64_t n = 0; n < node_count; ++n)
+    {
+        offsets[n] = acc;
+        acc += counts[n];
+        mass32[n] = safe_f32(mass64[n]);
+    }
+    offsets[node_count] = acc;
+    for (uint64_t n = 0; n < node_count; ++n)
+        counts[n] = 0;
+    for (uint64_t e = 0; e < element_count; ++e)
+        for (int a = 0; a < 4; ++a)
+        {
+            const uint32_t n = tets[e * 4 + a];
+            const uint32_t w = offsets[n] + counts[n]++;
+            adj_elem[w] = (uint32_t)e;
+            adj_local[w] = (uint8_t)a;
+        }
+    free(counts);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* loads.cpp:63-174                                                          */
+/* ------------------------------------------------------------------------- */
+
+double orc_evaluate_curve(const double *t, const double *v, uint64_t n, double time)
+{
+    /* loads.cpp:63-85 (std::lerp(a,b,w) for w in [0,1]: libstdc++ formula) */
+    if (n == 0)
+        return 1.0;
+    if (time <= t[0])
+        return v[0];
+    for (uint64_t i = 1; i < n; ++i)
+    {
+        if (time <= t[i])
+        {
+            const double span = t[i] - t[i - 1];
+            const double w = span > 0.0 ? (time - t[i - 1]) / span : 0.0;
+            const double a = v[i - 1], b = v[i];
+            /* libstdc++ std::lerp */
+            if ((a <= 0 && b >= 0) || (a >= 0 && b <= 0))
+                return w * b + (1 - w) * a;
+            if (w == 1)
+                return b;
+            const double x = a + w * (b - a);
+            return (w > 1) == (b > a) ? (b < x ? x : b) : (b > x ? x : b);
+        }
+    }
+    return v[n - 1];
+}
+
+void orc_gravity_loads(uint64_t node_count, const double *mass64, const double *gravity, double *loads)
+{
+    /* loads.cpp:91-98 */
+    for (uint64_t n = 0; n < node_count; ++n)
+        for (int k = 0; k < 3; ++k)
+            loads[n * 3 + k] += mass64[n] * gravity[k];
+}
+
+void orc_point_loads(uint64_t count, const uint32_t *nodes, const double *value, double scale, double *loads)
+{
+    /* loads.cpp:152-171 */
+    for (uint64_t i = 0; i < count; ++i)
+        for (int k = 0; k < 3; ++k)
+            loads[(uint64_t)nodes[i] * 3 + k] += scale * value[k];
+}
+
+/* ------------------------------------------------------------------------- */
+/* pcg.cpp                                                                   */
+/* ------------------------------------------------------------------------- */
+
+static int axis_fixed(uint32_t mask, int k) { return (mask >> k) & 1u; }
+
+static void snprintf_iteration(char *buf, size_t n, uint64_t it)
+{
+    snprintf(buf, n, "iteration=%llu", (unsigned long long)it);
+}
+
+static int validate_system(const orc_system *s)
+{
+    /* pcg.cpp:82-139 (size checks are structural in this ABI) */
+    if (s->dof_count != s->node_count * 3)
+        return fail(ORC_ERR_SIZE, "dof count mismatch (expected node_count * 3)", "");
+    if (s->material_count == 0)
+        return fail(ORC_ERR_MATERIALS, "materials table is empty", "");
+    if (s->reduction_block == 0)
+        return fail(ORC_ERR_REDUCTION, "reduction block must be >= 1", "reduction_block=0");
+    if (s->reduction_partials == 0)
+        return fail(ORC_ERR_REDUCTION, "reduction partial count must be >= 1", "reduction_partials=0");
+    return 0;
+}
+
+/* element force for one tet in reference order (pcg.cpp:561-651); f[12] */
+static void element_force(const orc_system *s, uint64_t e, const double *san, double f[12])
+{
+    const float *gr = s->gradients + e * 24;
+    const uint32_t *cn = s->connectivity + e * 8;
+    const double *D = s->stiffness + 36 * (uint64_t)s->material_index[e];
+    double gx[4], gy[4], gz[4], ux[4], uy[4], uz[4];
+    for (int a = 0; a < 4; ++a)
+    {
+        gx[a] = (double)gr[3 * a + 0];
+        gy[a] = (double)gr[3 * a + 1];
+        gz[a] = (double)gr[3 * a + 2];
+        const uint64_t b = 3 * (uint64_t)cn[a];
+        ux[a] = san[b + 0];
+        uy[a] = san[b + 1];
+        uz[a] = san[b + 2];
+    }
+    /* strain = B u, columns ascending (pcg.cpp:622-630) */
+    double eps[6];
+    eps[0] = 0.0, eps[1] = 0.0, eps[2] = 0.0, eps[3] = 0.0, eps[4] = 0.0, eps[5] = 0.0;
+    for (int a = 0; a < 4; ++a)
+    {
+        eps[0] += gx[a] * ux[a];
+        eps[1] += gy[a] * uy[a];
+        eps[2] += gz[a] * uz[a];
+        eps[3] += gy[a] * ux[a];
+        eps[3] += gx[a] * uy[a];
+        eps[4] += gz[a] * uy[a];
+        eps[4] += gy[a] * uz[a];
+        eps[5] += gz[a] * ux[a];
+        eps[5] += gx[a] * uz[a];
+    }
+    /* stress = D strain (pcg.cpp:632-640) */
+    double sig[6];
+    for (int r = 0; r < 6; ++r)
+    {
+        double sum = 0.0;
+        for (int c = 0; c < 6; ++c)
+            sum += D[r * 6 + c] * eps[c];
+        sig[r] = sum;
+    }
+    const double vol = (double)s->volume[e] * s->stiffness_scale; /* pcg.cpp:642 */
+    for (int a = 0; a < 4; ++a)
+    {
+        /* f[col] = (sum_r B[r][col] sigma[r]) * vol, rows ascending (pcg.cpp:643-651) */
+        double fx = 0.0, fy = 0.0, fz = 0.0;
+        fx += gx[a] * sig[0];
+        fx += gy[a] * sig[3];
+        fx += gz[a] * sig[5];
+        fy += gy[a] * sig[1];
+        fy += gx[a] * sig[3];
+        fy += gz[a] * sig[4];
+        fz += gz[a] * sig[2];
+        fz += gy[a] * sig[4];
+        fz += gx[a] * sig[5];
+        f[3 * a + 0] = fx * vol;
+        f[3 * a + 1] = fy * vol;
+        f[3 * a + 2] = fz * vol;
+    }
+}
+
+int orc_apply_keff(const orc_system *s, const float *in, float *out)
+{
+    int st = validate_system(s);
+    if (st)
+        return st;
+    const uint64_t D = s->dof_count;
+    double *san = (double *)malloc(D * sizeof(double) + 1);
+    double *acc = (double *)calloc(D + 1, sizeof(double));
+    if (!san || !acc)
+    {
+        free(san);
+        free(acc);
+        return fail(ORC_ERR_ALLOC, "failed to grow matrix-free workspace buffers", "");
+    }
+    /* pcg.cpp:530-546 sanitize */
+    for (uint64_t d = 0; d < D; ++d)
+        san[d] = (double)in[d];
+    for (uint64_t n = 0; n < s->node_count; ++n)
+        for (int k = 0; k < 3; ++k)
+            if (axis_fixed(s->bc_mask[n], k))
+                san[3 * n + k] = 0.0;
+    /* pcg.cpp:561-662 element loop, ascending element order */
+    for (uint64_t e = 0; e < s->element_count; ++e)
+    {
+        if (s->material_index[e] >= s->material_count)
+        {
+            free(san);
+            free(acc);
+            return fail(ORC_ERR_MATERIAL_RANGE, "element references material out of range", "");
+        }
+        for (int a = 0; a < 4; ++a)
+            if (s->connectivity[e * 8 + a] >= s->node_count)
+            {
+                free(san);
+                free(acc);
+                return fail(ORC_ERR_NODE_RANGE, "element connectivity references node out of range", "");
+            }
+        double f[12];
+        element_force(s, e, san, f);
+        for (int a = 0; a < 4; ++a)
+        {
+            const uint64_t b = 3 * (uint64_t)s->connectivity[e * 8 + a];
+            acc[b + 0] += f[3 * a + 0];
+            acc[b + 1] += f[3 * a + 1];
+            acc[b + 2] += f[3 * a + 2];
+        }
+    }
+    /* pcg.cpp:664-691 mass, Dirichlet identity rows, cast */
+    for (uint64_t n = 0; n < s->node_count; ++n)
+    {
+        const double m = (double)s->lumped_mass[n] * s->mass_factor;
+        for (int k = 0; k < 3; ++k)
+            acc[3 * n + k] += m * san[3 * n + k];
+    }
+    for (uint64_t n = 0; n < s->node_count; ++n)
+        for (int k = 0; k < 3; ++k)
+            if (axis_fixed(s->bc_mask[n], k))
+                acc[3 * n + k] = (double)in[3 * n + k];
+    for (uint64_t d = 0; d < D; ++d)
+        out[d] = (float)acc[d];
+    free(san);
+    free(acc);
+    return 0;
+}
+
+static void invert_spd_3x3(double m[9], double inv[9])
+{
+    /* pcg.cpp:215-268 */
+    const double kDetTol = 1.0e-12;
+#define DET3(M) ((M)[0] * ((M)[4] * (M)[8] - (M)[5] * (M)[7]) - (M)[1] * ((M)[3] * (M)[8] - (M)[5] * (M)[6]) + \
+                 (M)[2] * ((M)[3] * (M)[7] - (M)[4] * (M)[6]))
+    double det = DET3(m);
+    if (fabs(det) < kDetTol)
+    {
+        double md = m[0];
+        if (m[4] > md)
+            md = m[4];
+        if (m[8] > md)
+            md = m[8];
+        double eps = md * 1.0e-6 + 1.0e-12;
+        if (1.0e-6 > eps)
+            eps = 1.0e-6;
+        m[0] += eps;
+        m[4] += eps;
+        m[8] += eps;
+        det = DET3(m);
+    }
+    if (fabs(det) < kDetTol)
+    {
+        for (int i = 0; i < 9; ++i)
+            inv[i] = 0.0;
+        inv[0] = 1.0 / (m[0] > 1.0e-6 ? m[0] : 1.0e-6);
+        inv[4] = 1.0 / (m[4] > 1.0e-6 ? m[4] : 1.0e-6);
+        inv[8] = 1.0 / (m[8] > 1.0e-6 ? m[8] : 1.0e-6);
+        return;
+    }
+#undef DET3
+    const double id = 1.0 / det;
+    inv[0] = (m[4] * m[8] - m[5] * m[7]) * id;
+    inv[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+    inv[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    inv[3] = (m[5] * m[6] - m[3] * m[8]) * id;
+    inv[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+    inv[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    inv[6] = (m[3] * m[7] - m[4] * m[6]) * id;
+    inv[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+    inv[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+int orc_block_jacobi(const orc_system *s, float *inv_out)
+{
+    /* pcg.cpp:270-408 prepare_block_jacobi */
+    int st = validate_system(s);
+    if (st)
+        return st;
+    double *buf = (double *)calloc(s->node_count * 9 + 1, sizeof(double));
+    if (!buf)
+        return fail(ORC_ERR_ALLOC, "failed to grow matrix-free workspace buffers", "");
+    for (uint64_t e = 0; e < s->element_count; ++e)
+    {
+        if (s->material_index[e] >= s->material_count)
+        {
+            free(buf);
+            return fail(ORC_ERR_MATERIAL_RANGE, "element references material out of range", "");
+        }
+        const float *gr = s->gradients + e * 24;
+        const double *Dm = s->stiffness + 36 * (uint64_t)s->material_index[e];
+        double B[6][12];
+        memset(B, 0, sizeof B);
+        for (int a = 0; a < 4; ++a)
+        {
+            const double gx = gr[3 * a], gy = gr[3 * a + 1], gz = gr[3 * a + 2];
+            const int c = 3 * a;
+            B[0][c + 0] = gx;
+            B[1][c + 1] = gy;
+            B[2][c + 2] = gz;
+            B[3][c + 0] = gy;
+            B[3][c + 1] = gx;
+            B[4][c + 1] = gz;
+            B[4][c + 2] = gy;
+            B[5][c + 0] = gz;
+            B[5][c + 2] = gx;
+        }
+        double DB[6][12];
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 12; ++c)
+            {
+                double sum = 0.0;
+                for (int m = 0; m < 6; ++m)
+                    sum += Dm[r * 6 + m] * B[m][c];
+                DB[r][c] = sum;
+            }
+        const double sv = (double)s->volume[e] * s->stiffness_scale;
+        for (int a = 0; a < 4; ++a)
+        {
+            const uint32_t node = s->connectivity[e * 8 + a];
+            if (node >= s->node_count)
+            {
+                free(buf);
+                return fail(ORC_ERR_NODE_RANGE, "element connectivity references node out of range", "");
+            }
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j)
+                {
+                    const int li = 3 * a + i, lj = 3 * a + j;
+                    double sum = 0.0;
+                    for (int r = 0; r < 6; ++r)
+                        sum += B[r][li] * DB[r][lj];
+                    buf[(uint64_t)node * 9 + i * 3 + j] += sum * sv;
+                }
+        }
+    }
+    for (uint64_t n = 0; n < s->node_count; ++n)
+    {
+        const double m = (double)s->lumped_mass[n] * s->mass_factor;
+        for (int k = 0; k < 3; ++k)
+            buf[n * 9 + k * 3 + k] += m;
+    }
+    for (uint64_t n = 0; n < s->node_count; ++n)
+    {
+        double blk[9], inv[9];
+        memcpy(blk, buf + n * 9, sizeof blk);
+        invert_spd_3x3(blk, inv);
+        for (int k = 0; k < 3; ++k)
+            if (axis_fixed(s->bc_mask[n], k))
+                for (int c = 0; c < 3; ++c)
+                    inv[k * 3 + c] = (k == c) ? 1.0 : 0.0;
+        for (int i = 0; i < 9; ++i)
+            inv_out[n * 9 + i] = (float)inv[i];
+    }
+    free(buf);
+    return 0;
+}
+
+static double dot_chunked(const orc_system *s, const float *a, const float *b, double *partials)
+{
+    /* pcg.cpp:170-207 dot_accumulate */
+    const uint64_t blk = s->reduction_block ? s->reduction_block : 1;
+    const uint64_t D = s->dof_count;
+    const uint64_t chunks = (D + blk - 1) / blk;
+    double total = 0.0;
+    for (uint64_t c = 0; c < chunks; ++c)
+    {
+        const uint64_t beg = c * blk, end = beg + blk < D ? beg + blk : D;
+        double acc = 0.0;
+        for (uint64_t i = beg; i < end; ++i)
+            acc += (double)a[i] * (double)b[i];
+        if (partials)
+            partials[c] = acc;
+        total += acc;
+    }
+    if (partials)
+        for (uint64_t c = chunks; c < s->reduction_partials; ++c)
+            partials[c] = 0.0;
+    return total;
+}
+
+double orc_dot(const orc_system *s, const float *a, const float *b, double *partials)
+{
+    return dot_chunked(s, a, b, partials);
+}
+
+static void apply_preconditioner(const orc_system *s, const float *inv, const float *r, float *z)
+{
+    /* pcg.cpp:410-456 */
+    for (uint64_t n = 0; n < s->node_count; ++n)
+    {
+        const double rv[3] = {(double)r[3 * n], (double)r[3 * n + 1], (double)r[3 * n + 2]};
+        for (int k = 0; k < 3; ++k)
+        {
+            double sum = 0.0;
+            for (int c = 0; c < 3; ++c)
+                sum += (double)inv[n * 9 + k * 3 + c] * rv[c];
+            z[3 * n + k] = axis_fixed(s->bc_mask[n], k) ? 0.0f : (float)sum;
+        }
+    }
+}
+
+static void enforce_dirichlet(const orc_system *s, const float *rhs, float *x, float *r)
+{
+    /* pcg.cpp:458-475 */
+    for (uint64_t n = 0; n < s->node_count; ++n)
+        for (int k = 0; k < 3; ++k)
+            if (axis_fixed(s->bc_mask[n], k))
+            {
+                x[3 * n + k] = rhs[3 * n + k];
+                r[3 * n + k] = 0.0f;
+            }
+}
+
+static void mask_vector(const orc_system *s, float *v)
+{
+    for (uint64_t n = 0; n < s->node_count; ++n)
+        for (int k = 0; k < 3; ++k)
+            if (axis_fixed(s->bc_mask[n], k))
+                v[3 * n + k] = 0.0f;
+}
+
+int orc_solve_pcg(const orc_system *s, const float *rhs, uint64_t max_iterations, double relative_tolerance,
+                  int warm_start, float *x, float *r, float *p, float *z, float *Ap, double *partials,
+                  orc_telemetry *tel, double *residual_history)
+{
+    /* pcg.cpp:696-918 */
+    memset(tel, 0, sizeof *tel);
+    int st = validate_system(s);
+    if (st)
+        return st;
+    if (max_iterations == 0)
+        return fail(ORC_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
+    const uint64_t D = s->dof_count;
+    float *inv = (float *)malloc(s->node_count * 9 * sizeof(float) + 4);
+    if (!inv)
+        return fail(ORC_ERR_ALLOC, "failed to grow matrix-free workspace buffers", "");
+    if (!warm_start)
+        for (uint64_t d = 0; d < D; ++d)
+            x[d] = 0.0f;
+    if ((st = orc_block_jacobi(s, inv)) != 0)
+        goto done;
+    if ((st = orc_apply_keff(s, x, Ap)) != 0)
+        goto done;
+    for (uint64_t d = 0; d < D; ++d)
+        r[d] = rhs[d] - Ap[d];
+    enforce_dirichlet(s, rhs, x, r);
+    const double rhs_sq = dot_chunked(s, rhs, rhs, partials);
+    double rhs_norm = sqrt(rhs_sq);
+    if (rhs_norm < 1.0e-12)
+        rhs_norm = 1.0;
+    double res = sqrt(dot_chunked(s, r, r, partials));
+    tel->residual_norm = res;
+    tel->rhs_norm = sqrt(rhs_sq);
+    if (residual_history)
+        residual_history[0] = res;
+    const double tol = relative_tolerance * rhs_norm;
+    if (res <= tol)
+    {
+        tel->converged = 1;
+        tel->iterations = 0;
+        goto done;
+    }
+    apply_preconditioner(s, inv, r, z);
+    double rho = dot_chunked(s, r, z, partials);
+    if (fabs(rho) < 1.0e-18)
+    {
+        st = fail(ORC_ERR_RHO_ZERO, "preconditioner produced near-zero rho", "rho~0");
+        goto done;
+    }
+    memcpy(p, z, D * sizeof(float));
+    mask_vector(s, p);
+    for (uint64_t it = 0; it < max_iterations; ++it)
+    {
+        if ((st = orc_apply_keff(s, p, Ap)) != 0)
+            goto done;
+        const double denom = dot_chunked(s, p, Ap, partials);
+        if (fabs(denom) < 1.0e-18)
+        {
+            static char ctx[64];
+            snprintf_iteration(ctx, sizeof ctx, it);
+            st = fail(ORC_ERR_DENOM_ZERO, "CG denominator approached zero", ctx);
+            goto done;
+        }
+        const double alpha = rho / denom;
+        tel->alpha_last = alpha;
+        for (uint64_t d = 0; d < D; ++d)
+        {
+            x[d] += (float)(alpha * (double)p[d]);
+            r[d] -= (float)(alpha * (double)Ap[d]);
+        }
+        enforce_dirichlet(s, rhs, x, r);
+        res = sqrt(dot_chunked(s, r, r, partials));
+        tel->residual_norm = res;
+        tel->iterations = it + 1;
+        if (residual_history)
+            residual_history[it + 1] = res;
+        if (res <= tol)
+        {
+            tel->converged = 1;
+            break;
+        }
+        apply_preconditioner(s, inv, r, z);
+        const double rho_new = dot_chunked(s, r, z, partials);
+        if (fabs(rho) < 1.0e-18)
+        {
+            static char ctx[64];
+            snprintf_iteration(ctx, sizeof ctx, it);
+            st = fail(ORC_ERR_RHO_ZERO, "CG rho approached zero", ctx);
+            goto done;
+        }
+        const double beta = rho_new / rho;
+        tel->beta_last = beta;
+        rho = rho_new;
+        for (uint64_t d = 0; d < D; ++d)
+            p[d] = (float)((double)z[d] + beta * (double)p[d]);
+        mask_vector(s, p);
+    }
+done:
+    free(inv);
+    return st;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Stepper CPU branch: newmark_stepper.cpp:1094-1379                         */
+/* ------------------------------------------------------------------------- */
+
+int orc_stepper_step(orc_stepper *t, double sim_time, int paused, orc_step_telemetry *out)
+{
+    const orc_system *s0 = t->system;
+    orc_system sys = *s0;
+    const uint64_t N = s0->node_count, D = s0->dof_count;
+    int st = 0;
+    memset(out, 0, sizeof *out);
+    t->accumulated_time = sim_time;
+    /* refresh_coefficients + update_matrix_free_scalars (:1316-1326) */
+    double a[6], upd[2];
+    orc_newmark_coefficients(t->dt, t->beta, t->gamma, a, upd);
+    sys.stiffness_scale = 1.0 + a[1] * t->rayleigh_beta;
+    sys.mass_factor = a[0] + a[1] * t->rayleigh_alpha;
+    /* write_predictor (:1245-1286) */
+    const double dt = t->dt, dt_sq = dt * dt;
+    const double disp_factor = 0.5 - t->beta, vel_factor = 1.0 - t->gamma;
+    for (uint64_t i = 0; i < D; ++i)
+    {
+        const double u = t->u[i], v = t->v[i], ac = t->a[i];
+        t->u_pred[i] = (float)(u + dt * v + disp_factor * dt_sq * ac);
+        t->v_pred[i] = (float)(v + vel_factor * dt * ac);
+    }
+    /* assemble_rhs (:1162-1217) */
+    for (uint64_t n = 0; n < N; ++n)
+    {
+        const double m = (double)s0->lumped_mass[n];
+        for (int k = 0; k < 3; ++k)
+        {
+            const uint64_t i = 3 * n + k;
+            const double u = t->u[i], v = t->v[i], ac = t->a[i];
+            const double mass_term = m * (a[0] * u + a[2] * v + a[3] * ac);
+            const double damping_term = a[1] * u + a[4] * v + a[5] * ac;
+            const double force = (double)t->external_force[i];
+            const double total = force + mass_term + t->rayleigh_alpha * m * damping_term;
+            t->rhs[i] = (float)total;
+            t->damping_rhs[i] = (float)damping_term;
+        }
+    }
+    if (fabs(t->rayleigh_beta) > DBL_EPSILON)
+    {
+        orc_system stiff = *s0;
+        stiff.stiffness_scale = 1.0;
+        stiff.mass_factor = 0.0;
+        if ((st = orc_apply_keff(&stiff, t->damping_rhs, t->damping_out)) != 0)
+            return fail(st, "pcg solve failed", "failed to apply stiffness to damping term");
+        const float bf = (float)t->rayleigh_beta;
+        for (uint64_t i = 0; i < D; ++i)
+            t->rhs[i] += bf * t->damping_out[i];
+    }
+    /* clamp_dirichlet_rhs (:1219-1243) */
+    for (uint64_t n = 0; n < N; ++n)
+        for (int k = 0; k < 3; ++k)
+            if (axis_fixed(s0->bc_mask[n], k))
+                t->rhs[3 * n + k] = t->bc_value[3 * n + k] - t->u[3 * n + k];
+    const double tol = paused ? t->pause_tolerance : t->runtime_tolerance;
+    st = orc_solve_pcg(&sys, t->rhs, t->max_iterations, tol, t->warm_start, t->x, t->r, t->p, t->z, t->Ap,
+                       t->partials, &out->pcg, NULL);
+    if (st)
+        return st;
+    /* apply_state_update (:1288-1314) */
+    const float gob = (float)upd[1], ib = (float)upd[0];
+    for (uint64_t i = 0; i < D; ++i)
+    {
+        const float dx = t->x[i];
+        t->u[i] = t->u_pred[i] + dx;
+        t->a[i] = ib * dx;
+        t->v[i] = t->v_pred[i] + gob * dx;
+    }
+    out->simulation_time = sim_time;
+    out->time_step = t->dt;
+    out->applied_tolerance = tol;
+    out->paused_mode = paused;
+    /* adapt_timestep (:1328-1367) */
+    if (t->adaptive)
+    {
+        const double low = t->low_iteration_ratio * (double)t->max_iterations;
+        if ((double)out->pcg.iterations <= low)
+        {
+            t->dt *= t->increase_factor;
+            out->dt_increased = 1;
+        }
+        else if (!out->pcg.converged)
+        {
+            t->dt *= t->decrease_factor;
+            out->dt_decreased = 1;
+        }
+        if (t->min_dt > 0.0 && t->dt <= t->min_dt)
+        {
+            t->dt = t->min_dt;
+            out->dt_clamped_min = 1;
+        }
+        if (t->max_dt > 0.0 && t->dt >= t->max_dt)
+        {
+            t->dt = t->max_dt;
+            out->dt_clamped_max = 1;
+        }
+    }
+    t->frame_index += 1;
+    t->accumulated_time = sim_time + t->dt;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* dense CPU reference: solver.cpp:37-378 (config-1 oracle, O(D^2) memory)   */
+/* ------------------------------------------------------------------------- */
+
+int orc_dense_assemble(uint64_t node_count, uint64_t element_count, const uint32_t *tets, const double *grads64,
+                       const double *volume64, const uint32_t *material_index, const double *stiffness, double *K)
+{
+    /* solver.cpp:37-88 build_element_stiffness + :267-310 assemble_linear_system */
+    const uint64_t n = node_count * 3;
+    memset(K, 0, n * n * sizeof(double));
+    for (uint64_t e = 0; e < element_count; ++e)
+    {
+        const double *g = grads64 + e * 12;
+        const double *Dm = stiffness + 36 * (uint64_t)material_index[e];
+        double B[6][12], DB[6][12], Ke[12][12];
+        memset(B, 0, sizeof B);
+        for (int a = 0; a < 4; ++a)
+        {
+            const int c = 3 * a;
+            B[0][c + 0] = g[3 * a];
+            B[1][c + 1] = g[3 * a + 1];
+            B[2][c + 2] = g[3 * a + 2];
+            B[3][c + 0] = g[3 * a + 1];
+            B[3][c + 1] = g[3 * a];
+            B[4][c + 1] = g[3 * a + 2];
+            B[4][c + 2] = g[3 * a + 1];
+            B[5][c + 0] = g[3 * a + 2];
+            B[5][c + 2] = g[3 * a];
+        }
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 12; ++c)
+            {
+                double sum = 0.0;
+                for (int m = 0; m < 6; ++m)
+                    sum += Dm[r * 6 + m] * B[m][c];
+                DB[r][c] = sum;
+            }
+        for (int i = 0; i < 12; ++i)
+            for (int j = 0; j < 12; ++j)
+            {
+                double sum = 0.0;
+                for (int r = 0; r < 6; ++r)
+                    sum += B[r][i] * DB[r][j];
+                Ke[i][j] = sum * volume64[e];
+            }
+        for (int a = 0; a < 4; ++a)
+            for (int ka = 0; ka < 3; ++ka)
+            {
+                const uint64_t gi = 3 * (uint64_t)tets[e * 4 + a] + ka;
+                for (int b = 0; b < 4; ++b)
+                    for (int kb = 0; kb < 3; ++kb)
+                    {
+                        const uint64_t gj = 3 * (uint64_t)tets[e * 4 + b] + kb;
+                        K[gi * n + gj] += Ke[3 * a + ka][3 * b + kb];
+                    }
+            }
+    }
+    return 0;
+}
+
+static double ddot(const double *a, const double *b, uint64_t n)
+{
+    double s = 0.0;
+    for (uint64_t i = 0; i < n; ++i)
+        s += a[i] * b[i];
+    return s;
+}
+
+static void dmatvec(const double *M, const double *v, double *o, uint64_t n)
+{
+    for (uint64_t r = 0; r < n; ++r)
+    {
+        double s = 0.0;
+        const double *row = M + r * n;
+        for (uint64_t c = 0; c < n; ++c)
+            s += row[c] * v[c];
+        o[r] = s;
+    }
+}
+
+int orc_dense_newmark_step(uint64_t n, const double *K, const double *mass_diag, const double *load,
+                           const uint8_t *mask, const double *targets, double r_alpha, double r_beta,
+                           const double *coef /* beta gamma dt a0..a5 */, const double *u0, const double *v0,
+                           const double *acc0, double tolerance, uint64_t max_iterations, double *u1, double *v1,
+                           double *acc1, orc_dense_stats *stats)
+{
+    /* solver.cpp:354-378 solve_newmark_step */
+    const double beta = coef[0], gamma = coef[1], dt = coef[2];
+    const double *a = coef + 3;
+    double *rhs = (double *)malloc(n * sizeof(double));
+    double *damp = (double *)malloc(n * sizeof(double));
+    double *tmp = (double *)malloc(n * sizeof(double));
+    double *keff = (double *)malloc(n * n * sizeof(double));
+    double *x = (double *)calloc(n, sizeof(double));
+    double *r = (double *)malloc(n * sizeof(double));
+    double *z = (double *)malloc(n * sizeof(double));
+    double *p = (double *)malloc(n * sizeof(double));
+    double *diag = (double *)malloc(n * sizeof(double));
+    if (!rhs || !damp || !tmp || !keff || !x || !r || !z || !p || !diag)
+        return fail(ORC_ERR_ALLOC, "allocation failed", "");
+    (void)beta;
+    /* newmark.cpp:102-133 build_effective_rhs */
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        const double mass_term = mass_diag[i] * (a[0] * u0[i] + a[2] * v0[i] + a[3] * acc0[i]);
+        const double damping_term = a[1] * u0[i] + a[4] * v0[i] + a[5] * acc0[i];
+        rhs[i] = load[i];
+        rhs[i] += mass_term;
+        rhs[i] += r_alpha * mass_diag[i] * damping_term;
+        damp[i] = damping_term;
+    }
+    if (r_beta != 0.0)
+    {
+        dmatvec(K, damp, tmp, n);
+        for (uint64_t i = 0; i < n; ++i)
+            rhs[i] += r_beta * tmp[i];
+    }
+    /* newmark.cpp:83-100 build_effective_stiffness */
+    const double ss = 1.0 + a[1] * r_beta;
+    for (uint64_t i = 0; i < n * n; ++i)
+        keff[i] = K[i] * ss;
+    const double mf = a[0] + a[1] * r_alpha;
+    for (uint64_t d = 0; d < n; ++d)
+        keff[d * n + d] += mass_diag[d] * mf;
+    /* solver.cpp:242-263 apply_dirichlet */
+    for (uint64_t d = 0; d < n; ++d)
+    {
+        if (!mask[d])
+            continue;
+        for (uint64_t c = 0; c < n; ++c)
+            keff[d * n + c] = 0.0;
+        for (uint64_t row = 0; row < n; ++row)
+            keff[row * n + d] = 0.0;
+        keff[d * n + d] = 1.0;
+        rhs[d] = targets[d] - u0[d];
+    }
+    /* solver.cpp:159-225 conjugate_gradient (scalar Jacobi, absolute tolerance) */
+    memcpy(r, rhs, n * sizeof(double));
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        const double v = keff[i * n + i];
+        diag[i] = fabs(v) > DBL_EPSILON ? v : 1.0;
+    }
+    for (uint64_t i = 0; i < n; ++i)
+        z[i] = r[i] / diag[i];
+    memcpy(p, z, n * sizeof(double));
+    double rho = ddot(r, z, n);
+    double res = sqrt(ddot(r, r, n));
+    memset(stats, 0, sizeof *stats);
+    if (res <= tolerance)
+    {
+        stats->converged = 1;
+        stats->residual_norm = res;
+    }
+    else
+    {
+        uint64_t it;
+        stats->converged = 0;
+        for (it = 0; it < max_iterations; ++it)
+        {
+            dmatvec(keff, p, tmp, n);
+            const double denom = ddot(p, tmp, n);
+            if (fabs(denom) < DBL_EPSILON)
+                break;
+            const double alpha = rho / denom;
+            for (uint64_t i = 0; i < n; ++i)
+            {
+                x[i] += alpha * p[i];
+                r[i] -= alpha * tmp[i];
+            }
+            res = sqrt(ddot(r, r, n));
+            stats->iterations = it + 1;
+            if (res <= tolerance)
+            {
+                stats->converged = 1;
+                break;
+            }
+            for (uint64_t i = 0; i < n; ++i)
+                z[i] = r[i] / diag[i];
+            const double rho_new = ddot(r, z, n);
+            const double b = rho_new / rho;
+            rho = rho_new;
+            for (uint64_t i = 0; i < n; ++i)
+                p[i] = z[i] + b * p[i];
+        }
+        stats->residual_norm = res;
+    }
+    /* newmark.cpp:135-157 update_state + solver.cpp:369-375 */
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        const double du = x[i];
+        u1[i] = u0[i] + du;
+        acc1[i] = a[0] * du - a[2] * v0[i] - a[3] * acc0[i];
+        v1[i] = v0[i] + dt * ((1.0 - gamma) * acc0[i] + gamma * acc1[i]);
+        if (mask[i])
+            u1[i] = targets[i];
+    }
+    free(rhs);
+    free(damp);
+    free(tmp);
+    free(keff);
+    free(x);
+    free(r);
+    free(z);
+    free(p);
+    free(diag);
+    return 0;
+}
