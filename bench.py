@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Benchmark of the matrix-free implicit Newmark/PCG hot path on MI355X.
+
+One "step" = one full Stepper::step (predictor -> RHS -> Dirichlet clamp -> block-Jacobi PCG with
+warm start -> corrector) on the configs[1] workload of BASELINE.json: the 69^3-hex block expanded to
+1,971,054 Kuhn tets (343,000 nodes, 1,029,000 DOF), all inputs resident in HBM before timing.
+
+Prints ONE JSON line (rank 0). value = PCG DOF-iterations per second over the whole job
+(sum over ranks of DOFs x PCG iterations / max-over-ranks wall time of the K timed steps).
+Extra fields: pcg_iterations_per_sec, dof_updates_per_sec (D x steps/s), the live roofline of the
+dominant kernel (K_eff, timed with hipEvents on the handle's stream inside the timed steps) and a
+bounded single-thread CPU baseline (the oracle restatement of the reference's solve_pcg).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): weak scaling, one process per
+GPU, each rank owns one copy of the per-GPU workload ("replicas" until the partitioned solver
+lands).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "civiwave-fem_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", help="BASELINE config key (c1..c5)")
+    ap.add_argument("--mode", default="fast", choices=["fast", "parity"])
+    ap.add_argument("--max-iterations", type=int, default=2000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iterations", type=int, default=40)
+    ap.add_argument("--traffic", default=None, help="PMC summary json (profiles/*.json) for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(case, sK, sM, iters):
+    """Oracle restatement of pcg.cpp solve_pcg, 1 thread, bounded: block-Jacobi setup + `iters` iterations."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import oracle_system  # noqa: E402
+
+    s = oracle_system(case.packing, case.materials, sK, sM)
+    rhs = case.static_rhs()
+    t0 = time.perf_counter()
+    out = s.solve_pcg(rhs, iters, 1e-30)
+    dt = time.perf_counter() - t0
+    it = out["telemetry"].iterations
+    return dict(value=case.packing.dof_count * it / dt, unit="DOF-it/s", cores=1, kind="port",
+                sample=f"{case.name}: oracle solve_pcg (block-Jacobi setup + {it} PCG iterations), "
+                       f"{dt:.2f} s, 1 thread, {os.cpu_count()} host CPUs visible")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # loaded before libcwf_hip.so so both share one HIP runtime
+
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", init_method="env://")
+    import numpy as np
+
+    from cwf import _lib, pcg, scenarios
+    from cwf.stepper import Stepper
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    device = local_rank if world > 1 else 0
+    case = scenarios.config_case(args.config, max_iterations=args.max_iterations)
+    P = case.packing
+    mode = _lib.MODE_FAST if args.mode == "fast" else _lib.MODE_PARITY
+    sK, sM = case.scalars()
+    stepper = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode, device=device)
+    L = _lib.load()
+    h = stepper.system.handle()
+    t_sim = 0.0
+    for w in range(args.warmup):
+        stepper.step(t_sim).value()
+        t_sim += case.cfg.time.initial_dt
+    import ctypes as C
+
+    L.cwf_hip_system_set_timing(h, 1)
+    torch.cuda.synchronize()
+    barrier()
+    total_iters = 0
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        tel = stepper.step(t_sim).value()
+        total_iters += tel.pcg.iterations
+        t_sim += case.cfg.time.initial_dt
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    keff_ms, keff_n = C.c_double(), C.c_uint64()
+    L.cwf_hip_system_timing(h, C.byref(keff_ms), C.byref(keff_n))
+    L.cwf_hip_system_set_timing(h, 0)
+    D = P.dof_count
+    local = np.array([elapsed, D * total_iters, total_iters, D], np.float64)
+    if dist is not None:
+        t = torch.from_numpy(local.copy())
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        dof_iters, iters_sum, dofs_sum = float(t[1]), float(t[2]), float(t[3])
+    else:
+        dof_iters, iters_sum, dofs_sum = local[1], local[2], local[3]
+    avg_keff_ms = keff_ms.value / max(1, keff_n.value)
+    # algorithmic bytes of one K_eff launch: 32 B/node + 72 B/tet (reference layout)
+    alg_bytes = 32.0 * P.node_count + 72.0 * P.element_count
+    achieved = alg_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(case, sK, sM, args.cpu_iterations)
+        result = {
+            "metric": "PCG DOF-iterations/sec per Newmark step (PCG-it/s x DOFs); DOF-updates/s and "
+                      "K_eff HBM GB/s vs roofline reported alongside",
+            "value": dof_iters / elapsed,
+            "unit": "DOF-it/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.mode == "fast" else "f64",
+            "data": "synthetic (structured hex block -> Kuhn tets, gravity + tip load)",
+            "config": {"workload": case.name, "nodes": P.node_count, "tets": P.element_count, "dofs": D,
+                       "mode": args.mode, "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "pcg_iterations": int(iters_sum),
+            "pcg_iterations_per_sec": iters_sum / world / elapsed,
+            "dof_updates_per_sec": dofs_sum * args.steps / elapsed,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "kernel": "k_keff_" + args.mode, "avg_launch_ms": avg_keff_ms,
+                         "launches": int(keff_n.value), "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    stepper.close()
+    stepper.system.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

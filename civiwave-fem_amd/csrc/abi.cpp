@@ -1,0 +1,908 @@
+// abi.cpp -- C-ABI (include/cwf_hip.h) over the gfx950 kernels: handle lifetime, HBM upload,
+// apply_keff / block-Jacobi / dot / solve_pcg / Stepper orchestration. One HIP stream per
+// handle; the PCG loop is enqueued in batches and only the 104-B control block is read back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "cwf_internal.hpp"
+
+namespace cwf
+{
+
+static thread_local std::string g_err, g_ctx;
+
+int set_error(cwf_hip_system *h, int code, const std::string &msg, const std::string &ctx)
+{
+    if (h)
+    {
+        h->err = msg;
+        h->ctx = ctx;
+    }
+    g_err = msg;
+    g_ctx = ctx;
+    return code;
+}
+
+int hip_fail(cwf_hip_system *h, hipError_t e, const char *what)
+{
+    return set_error(h, CWF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e), hipGetErrorName(e));
+}
+
+}  // namespace cwf
+
+using namespace cwf;
+
+#define HIPTRY(h, expr)                                                                                        \
+    do                                                                                                         \
+    {                                                                                                          \
+        hipError_t e__ = (expr);                                                                               \
+        if (e__ != hipSuccess)                                                                                 \
+            return hip_fail((h), e__, #expr);                                                                  \
+    } while (0)
+
+namespace
+{
+
+template <class T> int dalloc(cwf_hip_system *h, T **p, size_t count)
+{
+    void *q = nullptr;
+    const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess)
+        return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer",
+                         "bytes=" + std::to_string(bytes));
+    h->owned.push_back(q);
+    h->bytes += bytes;
+    *p = static_cast<T *>(q);
+    return 0;
+}
+
+template <class T> int upload(cwf_hip_system *h, T **dst, const T *src, size_t count)
+{
+    if (int st = dalloc(h, dst, count))
+        return st;
+    if (count)
+        HIPTRY(h, hipMemcpy(*dst, src, count * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+}
+
+bool iso_pattern(const double *D)
+{
+    for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 6; ++c)
+        {
+            const bool nz = (r < 3 && c < 3) || (r == c);
+            if (!nz && D[6 * r + c] != 0.0)
+                return false;
+        }
+    return true;
+}
+
+int check_ready(cwf_hip_system *h)
+{
+    if (!h)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess)
+        return hip_fail(h, e, "hipSetDevice");
+    return 0;
+}
+
+// stage a DOF vector: host -> device scratch, or use the device pointer directly
+int stage_in(cwf_hip_system *h, const float *src, float *scratch, uint64_t n, int kind, const float **out)
+{
+    if (kind == CWF_PTR_DEVICE)
+    {
+        *out = src;
+        return 0;
+    }
+    HIPTRY(h, hipMemcpyAsync(scratch, src, n * sizeof(float), hipMemcpyHostToDevice, h->stream));
+    *out = scratch;
+    return 0;
+}
+
+std::string pcg_error_message(int code, int iter, std::string *ctx)
+{
+    if (code == CWF_ERR_DENOM_ZERO)
+    {
+        *ctx = "iteration=" + std::to_string(iter);
+        return "CG denominator approached zero";  // pcg.cpp:846-849
+    }
+    if (code == CWF_ERR_RHO_ZERO && iter < 0)
+    {
+        *ctx = "rho~0";
+        return "preconditioner produced near-zero rho";  // pcg.cpp:810-813
+    }
+    *ctx = "iteration=" + std::to_string(iter);
+    return "CG rho approached zero";  // pcg.cpp:889-892
+}
+
+// run solve_pcg on device buffers h->rhs (or rhs_dev) and h->x. x must already hold the warm start.
+int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
+{
+    if (set.max_iterations == 0)
+        return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
+    if (h->hist_cap < set.max_iterations + 1)
+    {
+        if (h->hist)
+            (void)hipFree(h->hist);
+        h->hist = nullptr;
+        const uint64_t cap = std::max<uint64_t>(set.max_iterations + 1, 1024);
+        if (hipMalloc(reinterpret_cast<void **>(&h->hist), cap * sizeof(double)) != hipSuccess)
+            return set_error(h, CWF_ERR_ALLOC, "failed to grow matrix-free workspace buffers",
+                             "history=" + std::to_string(cap));
+        h->hist_cap = cap;
+    }
+    hipStream_t st = h->stream;
+    if (!set.warm_start)
+        HIPTRY(h, hipMemsetAsync(h->x, 0, h->ds.D * sizeof(float), st));
+    const bool fast = h->mode == CWF_MODE_FAST;
+    if (fast)
+        fast_pcg_init(h, rhs_dev, set.relative_tolerance, st);
+    else
+        parity_pcg_init(h, rhs_dev, set.relative_tolerance, st);
+    HIPTRY(h, hipGetLastError());
+    uint64_t enq = 0;
+    constexpr uint64_t kMaxBatch = 64;
+    uint64_t batch = set.check_interval > 0 ? std::min<uint64_t>((uint64_t)set.check_interval, kMaxBatch) : 4;
+    if (h->timing && h->ev.empty())
+    {
+        h->ev.resize(2 * kMaxBatch);
+        for (auto &e : h->ev)
+            HIPTRY(h, hipEventCreate(&e));
+    }
+    uint64_t prev_enq = 0, prev_nb = 0;
+    for (;;)
+    {
+        HIPTRY(h, hipMemcpyAsync(h->ctl_host, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+        HIPTRY(h, hipStreamSynchronize(st));
+        if (h->timing && prev_nb)
+        {
+            // only launches that did work: iteration index < completed iterations
+            for (uint64_t i = 0; i < prev_nb; ++i)
+            {
+                if (prev_enq + i >= h->ctl_host->iterations)
+                    break;
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]) == hipSuccess)
+                {
+                    h->keff_ms += ms;
+                    ++h->keff_count;
+                }
+            }
+            prev_nb = 0;
+        }
+        if (!h->ctl_host->active || enq >= set.max_iterations)
+            break;
+        const uint64_t nb = std::min<uint64_t>(batch, set.max_iterations - enq);
+        for (uint64_t i = 0; i < nb; ++i)
+        {
+            hipEvent_t e0 = h->timing ? h->ev[2 * i] : nullptr, e1 = h->timing ? h->ev[2 * i + 1] : nullptr;
+            if (fast)
+                fast_pcg_iteration(h, rhs_dev, st, e0, e1);
+            else
+                parity_pcg_iteration(h, rhs_dev, st, e0, e1);
+        }
+        HIPTRY(h, hipGetLastError());
+        prev_enq = enq;
+        prev_nb = nb;
+        enq += nb;
+        if (set.check_interval <= 0)
+            batch = std::min<uint64_t>(batch * 2, kMaxBatch);
+    }
+    const Ctl &c = *h->ctl_host;
+    h->hist_count = c.iterations + 1;
+    if (tel)
+    {
+        tel->iterations = c.iterations;
+        tel->residual_norm = c.res;
+        tel->rhs_norm = c.rhs_norm_raw;
+        tel->alpha_last = c.alpha_last;
+        tel->beta_last = c.beta_last;
+        tel->converged = c.converged;
+        tel->reserved = 0;
+    }
+    if (c.error)
+    {
+        std::string ctx;
+        std::string msg = pcg_error_message(c.error, c.error_iter, &ctx);
+        return set_error(h, c.error, msg, ctx);
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cwf_hip_abi_version(void) { return CWF_HIP_ABI_VERSION; }
+
+int cwf_hip_device_count(int *count)
+{
+    if (!count)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess)
+    {
+        *count = 0;
+        return hip_fail(nullptr, e, "hipGetDeviceCount");
+    }
+    return 0;
+}
+
+const char *cwf_hip_last_error(const cwf_hip_system *h) { return h ? h->err.c_str() : g_err.c_str(); }
+const char *cwf_hip_last_context(const cwf_hip_system *h) { return h ? h->ctx.c_str() : g_ctx.c_str(); }
+
+void cwf_hip_system_destroy(cwf_hip_system *h)
+{
+    if (!h)
+        return;
+    (void)hipSetDevice(h->device);
+    if (h->stream)
+        (void)hipStreamSynchronize(h->stream);
+    for (void *p : h->owned)
+        (void)hipFree(p);
+    if (h->hist)
+        (void)hipFree(h->hist);
+    if (h->ctl_host)
+        (void)hipHostFree(h->ctl_host);
+    for (hipEvent_t e : h->ev)
+        (void)hipEventDestroy(e);
+    if (h->stream)
+        (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system **out)
+{
+    if (!d || !out)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    *out = nullptr;
+    const uint64_t N = d->node_count, E = d->element_count;
+    // validate_system (pcg.cpp:82-139)
+    if (d->dof_count != N * 3)
+        return set_error(nullptr, CWF_ERR_SIZE, "dof count mismatch (expected node_count * 3)",
+                         "node_count=" + std::to_string(N) + " dof_count=" + std::to_string(d->dof_count));
+    if (d->material_count == 0 || !d->material_stiffness)
+        return set_error(nullptr, CWF_ERR_MATERIALS, "materials table is empty");
+    if (d->reduction_block == 0)
+        return set_error(nullptr, CWF_ERR_REDUCTION, "reduction block must be >= 1", "reduction_block=0");
+    if (d->reduction_partials == 0)
+        return set_error(nullptr, CWF_ERR_REDUCTION, "reduction partial count must be >= 1", "reduction_partials=0");
+    if ((E && (!d->element_connectivity || !d->element_gradients || !d->element_volume ||
+               !d->element_material_index)) ||
+        (N && (!d->lumped_mass || !d->bc_mask)))
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null system array");
+    if (N * 3 >= (1ull << 32) || E >= (1ull << 30))
+        return set_error(nullptr, CWF_ERR_UNSUPPORTED, "mesh too large for one handle (shard it)",
+                         "nodes=" + std::to_string(N) + " elements=" + std::to_string(E));
+    for (uint64_t e = 0; e < E; ++e)
+    {
+        if (d->element_material_index[e] >= d->material_count)
+            return set_error(nullptr, CWF_ERR_MATERIAL_RANGE, "element references material out of range",
+                             "element=" + std::to_string(e) +
+                                 " material_index=" + std::to_string(d->element_material_index[e]));
+        for (int a = 0; a < 4; ++a)
+            if (d->element_connectivity[e * 8 + a] >= N)
+                return set_error(nullptr, CWF_ERR_NODE_RANGE, "element connectivity references node out of range",
+                                 "element=" + std::to_string(e) +
+                                     " node=" + std::to_string(d->element_connectivity[e * 8 + a]));
+    }
+    hipError_t he = hipSetDevice(device);
+    if (he != hipSuccess)
+        return hip_fail(nullptr, he, "hipSetDevice");
+
+    cwf_hip_system *h = new (std::nothrow) cwf_hip_system();
+    if (!h)
+        return set_error(nullptr, CWF_ERR_ALLOC, "host allocation failed");
+    auto bail = [&](int st) {
+        std::string m = h->err, c = h->ctx;
+        cwf_hip_system_destroy(h);
+        set_error(nullptr, st, m, c);
+        return st;
+    };
+    h->device = device;
+    h->mode = d->mode == CWF_MODE_FAST ? CWF_MODE_FAST : CWF_MODE_PARITY;
+    h->reduction_block = d->reduction_block;
+    h->reduction_partials = d->reduction_partials;
+    if ((he = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail(hip_fail(h, he, "hipStreamCreate"));
+    if ((he = hipHostMalloc(reinterpret_cast<void **>(&h->ctl_host), sizeof(Ctl), hipHostMallocDefault)) !=
+        hipSuccess)
+        return bail(hip_fail(h, he, "hipHostMalloc"));
+
+    DevSys &s = h->ds;
+    s.N = (uint32_t)N;
+    s.E = (uint32_t)E;
+    s.D = (uint32_t)(3 * N);
+    s.M = (uint32_t)d->material_count;
+    s.sK = d->stiffness_scale;
+    s.sM = d->mass_factor;
+    s.iso = 1;
+    for (uint64_t m = 0; m < d->material_count; ++m)
+        s.iso &= iso_pattern(d->material_stiffness + 36 * m) ? 1 : 0;
+
+    // element records (64 B/tet)
+    {
+        std::vector<uint32_t> rec;
+        try
+        {
+            rec.resize(E * 16);
+        }
+        catch (const std::bad_alloc &)
+        {
+            return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
+        }
+        for (uint64_t e = 0; e < E; ++e)
+        {
+            uint32_t *r = rec.data() + e * 16;
+            for (int a = 0; a < 4; ++a)
+                r[a] = d->element_connectivity[e * 8 + a];
+            std::memcpy(r + 4, d->element_gradients + e * 24, 12 * sizeof(float));
+        }
+        uint4 *erec = nullptr;
+        if (int st = upload(h, &erec, reinterpret_cast<const uint4 *>(rec.data()), E * 4))
+            return bail(st);
+        s.erec = erec;
+    }
+    {
+        float *vol;
+        uint32_t *mat;
+        double *dm;
+        float *mass;
+        uint32_t *mask;
+        if (int st = upload(h, &vol, d->element_volume, E))
+            return bail(st);
+        if (int st = upload(h, &mat, d->element_material_index, E))
+            return bail(st);
+        if (int st = upload(h, &dm, d->material_stiffness, 36 * d->material_count))
+            return bail(st);
+        if (int st = upload(h, &mass, d->lumped_mass, N))
+            return bail(st);
+        if (int st = upload(h, &mask, d->bc_mask, N))
+            return bail(st);
+        s.vol = vol;
+        s.mat = mat;
+        s.dmat = dm;
+        s.mass = mass;
+        s.mask = mask;
+    }
+    // node -> element CSR, ascending element per node (preprocess.cpp:380-403)
+    {
+        std::vector<uint32_t> off(N + 1, 0), inc;
+        try
+        {
+            inc.resize(E * 4);
+        }
+        catch (const std::bad_alloc &)
+        {
+            return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
+        }
+        if (d->adjacency_offsets && d->adjacency_elements && d->adjacency_local)
+        {
+            std::memcpy(off.data(), d->adjacency_offsets, (N + 1) * sizeof(uint32_t));
+            if (off[N] != E * 4)
+                return bail(set_error(h, CWF_ERR_SIZE, "adjacency size mismatch",
+                                      "expected=" + std::to_string(E * 4) + " actual=" + std::to_string(off[N])));
+            for (uint64_t j = 0; j < E * 4; ++j)
+                inc[j] = (d->adjacency_elements[j] << 2) | (d->adjacency_local[j] & 3u);
+        }
+        else
+        {
+            std::vector<uint32_t> cnt(N, 0);
+            for (uint64_t e = 0; e < E; ++e)
+                for (int a = 0; a < 4; ++a)
+                    ++cnt[d->element_connectivity[e * 8 + a]];
+            uint32_t acc = 0;
+            for (uint64_t n = 0; n < N; ++n)
+            {
+                off[n] = acc;
+                acc += cnt[n];
+                cnt[n] = 0;
+            }
+            off[N] = acc;
+            for (uint64_t e = 0; e < E; ++e)
+                for (int a = 0; a < 4; ++a)
+                {
+                    const uint32_t n = d->element_connectivity[e * 8 + a];
+                    inc[off[n] + cnt[n]++] = ((uint32_t)e << 2) | (uint32_t)a;
+                }
+        }
+        uint32_t *doff, *dinc;
+        if (int st = upload(h, &doff, off.data(), N + 1))
+            return bail(st);
+        if (int st = upload(h, &dinc, inc.data(), E * 4))
+            return bail(st);
+        s.off = doff;
+        s.inc = dinc;
+    }
+    // solver scratch
+    const uint64_t D = 3 * N;
+    for (float **v : {&h->x, &h->r, &h->p, &h->z, &h->Ap, &h->rhs, &h->tmp})
+        if (int st = dalloc(h, v, D))
+            return bail(st);
+    if (int st = dalloc(h, &h->inv, 9 * N))
+        return bail(st);
+    const uint64_t chunks = (D + d->reduction_block - 1) / d->reduction_block;
+    h->part_cap = std::max<uint64_t>({chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), 1});
+    if (int st = dalloc(h, &h->part0, h->part_cap))
+        return bail(st);
+    if (int st = dalloc(h, &h->part1, h->part_cap))
+        return bail(st);
+    if (int st = dalloc(h, &h->ctl, 1))
+        return bail(st);
+    if (int st = dalloc(h, &h->scal, 8))
+        return bail(st);
+    HIPTRY(h, hipMemset(h->x, 0, D * sizeof(float)));
+    HIPTRY(h, hipMemset(h->ctl, 0, sizeof(Ctl)));
+    HIPTRY(h, hipDeviceSynchronize());
+    *out = h;
+    return 0;
+}
+
+int cwf_hip_system_set_scalars(cwf_hip_system *h, double stiffness_scale, double mass_factor)
+{
+    if (int st = check_ready(h))
+        return st;
+    h->ds.sK = stiffness_scale;
+    h->ds.sM = mass_factor;
+    return 0;
+}
+
+int cwf_hip_system_set_mode(cwf_hip_system *h, int mode)
+{
+    if (int st = check_ready(h))
+        return st;
+    h->mode = mode == CWF_MODE_FAST ? CWF_MODE_FAST : CWF_MODE_PARITY;
+    return 0;
+}
+
+int cwf_hip_system_set_timing(cwf_hip_system *h, int enabled)
+{
+    if (int st = check_ready(h))
+        return st;
+    h->timing = enabled ? 1 : 0;
+    h->keff_ms = 0.0;
+    h->keff_count = 0;
+    return 0;
+}
+
+int cwf_hip_system_timing(cwf_hip_system *h, double *keff_ms, uint64_t *keff_launches)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (keff_ms)
+        *keff_ms = h->keff_ms;
+    if (keff_launches)
+        *keff_launches = h->keff_count;
+    h->keff_ms = 0.0;
+    h->keff_count = 0;
+    return 0;
+}
+
+int cwf_hip_keff_timed(cwf_hip_system *h, const float *x, float *y, int reps, double *avg_ms)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (!x || !y || !avg_ms || reps <= 0)
+        return set_error(h, CWF_ERR_ARGUMENT, "bad argument");
+    hipEvent_t a, b;
+    HIPTRY(h, hipEventCreate(&a));
+    HIPTRY(h, hipEventCreate(&b));
+    HIPTRY(h, hipEventRecord(a, h->stream));
+    for (int i = 0; i < reps; ++i)
+    {
+        if (h->mode == CWF_MODE_FAST)
+            fast_keff(h, x, y, false, nullptr, h->part0, h->stream);
+        else
+            parity_keff(h, x, y, false, nullptr, h->stream);
+    }
+    HIPTRY(h, hipEventRecord(b, h->stream));
+    HIPTRY(h, hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPTRY(h, hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *avg_ms = (double)ms / reps;
+    return 0;
+}
+
+int cwf_hip_system_memory(const cwf_hip_system *h, uint64_t *bytes)
+{
+    if (!h || !bytes)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    *bytes = h->bytes;
+    return 0;
+}
+
+int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, int kind)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "input/output span size mismatch",
+                         "input=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+    const float *xin = nullptr;
+    if (int st = stage_in(h, x, h->tmp, n, kind, &xin))
+        return st;
+    float *yout = kind == CWF_PTR_DEVICE ? y : h->Ap;
+    if (h->mode == CWF_MODE_FAST)
+        fast_keff(h, xin, yout, true, nullptr, nullptr, h->stream);
+    else
+        parity_keff(h, xin, yout, true, nullptr, h->stream);
+    HIPTRY(h, hipGetLastError());
+    if (kind != CWF_PTR_DEVICE)
+        HIPTRY(h, hipMemcpyAsync(y, yout, n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int kind)
+{
+    if (int st = check_ready(h))
+        return st;
+    const uint64_t req = 9ull * h->ds.N;
+    if (n < req)
+        return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
+                         "required=" + std::to_string(req) + " available=" + std::to_string(n));
+    float *dst = kind == CWF_PTR_DEVICE ? inv_out : h->inv;
+    parity_block_jacobi(h, dst, h->stream);
+    HIPTRY(h, hipGetLastError());
+    if (kind != CWF_PTR_DEVICE)
+        HIPTRY(h, hipMemcpyAsync(inv_out, dst, req * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_dot(cwf_hip_system *h, const float *a, const float *b, uint64_t n, int kind, double *out,
+                double *partials)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (!out)
+        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "dot product span size mismatch",
+                         "lhs=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+    const float *da = nullptr, *db = nullptr;
+    if (int st = stage_in(h, a, h->tmp, n, kind, &da))
+        return st;
+    if (int st = stage_in(h, b, h->Ap, n, kind, &db))
+        return st;
+    double *res = h->scal;
+    uint32_t count;
+    if (h->mode == CWF_MODE_FAST)
+    {
+        count = fast_dot_blocks(h->ds.D);
+        fast_dot(da, db, nullptr, h->ds.D, h->part0, nullptr, h->stream);
+        fast_fold(h->part0, count, res, h->stream);
+    }
+    else
+    {
+        count = parity_chunk_count(h);
+        parity_dot_partials(h, da, db, nullptr, h->part0, nullptr, nullptr, h->stream);
+        parity_fold(h->part0, count, res, h->stream);
+    }
+    HIPTRY(h, hipGetLastError());
+    HIPTRY(h, hipMemcpyAsync(out, res, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (partials)
+    {
+        const uint64_t total = h->reduction_partials;
+        const uint64_t ncopy = std::min<uint64_t>(count, total);
+        if (kind == CWF_PTR_DEVICE)
+        {
+            HIPTRY(h, hipMemcpyAsync(partials, h->part0, ncopy * sizeof(double), hipMemcpyDeviceToDevice,
+                                     h->stream));
+            if (total > ncopy)
+                HIPTRY(h, hipMemsetAsync(partials + ncopy, 0, (total - ncopy) * sizeof(double), h->stream));
+        }
+        else
+        {
+            HIPTRY(h, hipMemcpyAsync(partials, h->part0, ncopy * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+            HIPTRY(h, hipStreamSynchronize(h->stream));
+            for (uint64_t c = ncopy; c < total; ++c)
+                partials[c] = 0.0;
+        }
+    }
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_settings *settings, float *x_inout,
+                      float *residual_out, uint64_t n, int kind, cwf_pcg_telemetry *telemetry)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (!rhs || !settings || !x_inout)
+        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
+    if (telemetry)
+        std::memset(telemetry, 0, sizeof *telemetry);
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "rhs span size mismatch",
+                         "rhs=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+    if (settings->max_iterations == 0)
+        return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
+    const float *drhs = nullptr;
+    if (int st = stage_in(h, rhs, h->rhs, n, kind, &drhs))
+        return st;
+    if (settings->warm_start)
+        HIPTRY(h, hipMemcpyAsync(h->x, x_inout, n * sizeof(float),
+                                 kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 h->stream));
+    int st = run_pcg(h, drhs, *settings, telemetry);
+    const hipMemcpyKind back = kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIPTRY(h, hipMemcpyAsync(x_inout, h->x, n * sizeof(float), back, h->stream));
+    if (residual_out)
+        HIPTRY(h, hipMemcpyAsync(residual_out, h->r, n * sizeof(float), back, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return st;
+}
+
+int cwf_hip_residual_history(cwf_hip_system *h, double *out, uint64_t capacity, uint64_t *count)
+{
+    if (int st = check_ready(h))
+        return st;
+    const uint64_t c = std::min(capacity, h->hist_count);
+    if (c && out)
+        HIPTRY(h, hipMemcpy(out, h->hist, c * sizeof(double), hipMemcpyDeviceToHost));
+    if (count)
+        *count = c;
+    return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Stepper (newmark_stepper.cpp:1005-1379)
+// ------------------------------------------------------------------------------------------
+
+struct cwf_hip_stepper
+{
+    cwf_hip_system *sys = nullptr;
+    cwf_stepper_desc d{};
+    double dt = 1e-3, accumulated_time = 0.0, beta = 0.25, gamma = 0.5;
+    uint64_t frame_index = 0;
+    int warm_start = 1;
+    float *u = nullptr, *v = nullptr, *a = nullptr, *up = nullptr, *vp = nullptr, *f = nullptr, *bcv = nullptr,
+          *damp = nullptr, *kd = nullptr, *srhs = nullptr;
+    std::vector<void *> owned;
+};
+
+namespace
+{
+int st_alloc(cwf_hip_stepper *t, float **p, uint64_t n)
+{
+    void *q = nullptr;
+    if (hipMalloc(&q, std::max<uint64_t>(n, 4) * sizeof(float)) != hipSuccess)
+        return set_error(t->sys, CWF_ERR_ALLOC, "failed to allocate stepper buffers");
+    t->owned.push_back(q);
+    *p = static_cast<float *>(q);
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+void cwf_hip_stepper_destroy(cwf_hip_stepper *t)
+{
+    if (!t)
+        return;
+    (void)hipSetDevice(t->sys->device);
+    (void)hipStreamSynchronize(t->sys->stream);
+    for (void *p : t->owned)
+        (void)hipFree(p);
+    delete t;
+}
+
+int cwf_hip_stepper_create(cwf_hip_system *h, const cwf_stepper_desc *desc, cwf_hip_stepper **out)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (!desc || !out)
+        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
+    *out = nullptr;
+    auto *t = new (std::nothrow) cwf_hip_stepper();
+    if (!t)
+        return set_error(h, CWF_ERR_ALLOC, "host allocation failed");
+    t->sys = h;
+    t->d = *desc;
+    t->d.external_force = nullptr;
+    t->d.bc_value = nullptr;
+    t->dt = desc->initial_dt > 0.0 ? desc->initial_dt : 1.0e-3;  // :1020
+    t->warm_start = desc->warm_start;
+    const uint64_t D = h->ds.D;
+    for (float **p : {&t->u, &t->v, &t->a, &t->up, &t->vp, &t->f, &t->bcv, &t->damp, &t->kd, &t->srhs})
+        if (int st = st_alloc(t, p, D))
+        {
+            cwf_hip_stepper_destroy(t);
+            return st;
+        }
+    hipStream_t s = h->stream;
+    for (float *p : {t->u, t->v, t->a, t->up, t->vp, t->f, t->bcv})
+        (void)hipMemsetAsync(p, 0, D * sizeof(float), s);
+    if (desc->external_force)
+        (void)hipMemcpyAsync(t->f, desc->external_force, D * sizeof(float), hipMemcpyHostToDevice, s);
+    if (desc->bc_value)
+        (void)hipMemcpyAsync(t->bcv, desc->bc_value, D * sizeof(float), hipMemcpyHostToDevice, s);
+    (void)hipMemsetAsync(h->x, 0, D * sizeof(float), s);  // solver.x starts at 0 (pack.cpp:214)
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess)
+    {
+        cwf_hip_stepper_destroy(t);
+        return hip_fail(h, e, "stepper create");
+    }
+    *out = t;
+    return 0;
+}
+
+int cwf_hip_stepper_step(cwf_hip_stepper *t, double sim_time, int paused, cwf_step_telemetry *tel)
+{
+    if (!t)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
+    cwf_hip_system *h = t->sys;
+    if (int st = check_ready(h))
+        return st;
+    hipStream_t s = h->stream;
+    const uint32_t N = h->ds.N, D = h->ds.D;
+    t->accumulated_time = sim_time;
+    // refresh_coefficients + update_matrix_free_scalars (:1316-1326)
+    const double b = t->beta, g = t->gamma, dt = t->dt;
+    double c6[6];
+    c6[0] = 1.0 / (b * dt * dt);
+    c6[1] = g / (b * dt);
+    c6[2] = 1.0 / (b * dt);
+    c6[3] = (1.0 / (2.0 * b)) - 1.0;
+    c6[4] = (g / b) - 1.0;
+    c6[5] = dt * ((g / (2.0 * b)) - 1.0);
+    const double inv_beta_dt2 = 1.0 / (b * dt * dt);
+    const double gamma_over_beta_dt = g / (b * dt);
+    const cwf::DevSys saved = h->ds;
+    h->ds.sK = 1.0 + c6[1] * t->d.rayleigh_beta;
+    h->ds.sM = c6[0] + c6[1] * t->d.rayleigh_alpha;
+    stepper_predictor(D, t->u, t->v, t->a, t->up, t->vp, dt, b, g, s);
+    stepper_assemble_rhs(N, h->ds.mass, t->u, t->v, t->a, t->f, t->srhs, t->damp, c6, t->d.rayleigh_alpha, s);
+    if (std::fabs(t->d.rayleigh_beta) > DBL_EPSILON)
+    {
+        cwf::DevSys stiff = h->ds;  // stiffness_only_system_ (:1051-1053)
+        stiff.sK = 1.0;
+        stiff.sM = 0.0;
+        if (h->mode == CWF_MODE_FAST)
+            fast_keff_ds(stiff, t->damp, t->kd, true, nullptr, nullptr, s);
+        else
+            parity_keff_ds(stiff, t->damp, t->kd, true, nullptr, s);
+        stepper_rhs_damping(D, t->srhs, t->kd, (float)t->d.rayleigh_beta, s);
+    }
+    stepper_clamp(N, h->ds.mask, t->bcv, t->u, t->srhs, s);
+    const double tol = paused ? t->d.pause_tolerance : t->d.runtime_tolerance;
+    cwf_pcg_settings ps{t->d.max_iterations, tol, t->warm_start, 0};
+    cwf_pcg_telemetry pt{};
+    int st = run_pcg(h, t->srhs, ps, &pt);
+    h->ds.sK = saved.sK;
+    h->ds.sM = saved.sM;
+    if (st)
+    {
+        std::string inner = h->err;
+        return set_error(h, st, "pcg solve failed", inner);  // :1130-1133
+    }
+    stepper_update(D, h->x, t->up, t->vp, t->u, t->v, t->a, (float)inv_beta_dt2, (float)gamma_over_beta_dt, s);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(s);
+    if (e != hipSuccess)
+        return hip_fail(h, e, "stepper update");
+    cwf_step_telemetry T{};
+    T.simulation_time = sim_time;
+    T.time_step = t->dt;
+    T.applied_tolerance = tol;
+    T.paused_mode = paused ? 1 : 0;
+    T.pcg = pt;
+    // adapt_timestep (:1328-1367)
+    if (t->d.adaptive)
+    {
+        const double low = t->d.low_iteration_ratio * (double)t->d.max_iterations;
+        if ((double)pt.iterations <= low)
+        {
+            t->dt *= t->d.increase_factor;
+            T.dt_increased = 1;
+        }
+        else if (!pt.converged)
+        {
+            t->dt *= t->d.decrease_factor;
+            T.dt_decreased = 1;
+        }
+        if (t->d.min_dt > 0.0 && t->dt <= t->d.min_dt)
+        {
+            t->dt = t->d.min_dt;
+            T.dt_clamped_min = 1;
+        }
+        if (t->d.max_dt > 0.0 && t->dt >= t->d.max_dt)
+        {
+            t->dt = t->d.max_dt;
+            T.dt_clamped_max = 1;
+        }
+    }
+    ++t->frame_index;
+    t->accumulated_time = sim_time + t->dt;
+    if (tel)
+        *tel = T;
+    return 0;
+}
+
+int cwf_hip_stepper_get_state(cwf_hip_stepper *t, int which, float *out, uint64_t n, int kind)
+{
+    if (!t || !out)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    cwf_hip_system *h = t->sys;
+    if (int st = check_ready(h))
+        return st;
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "state span size mismatch");
+    const float *src = which == 0 ? t->u : which == 1 ? t->v : which == 2 ? t->a : which == 3 ? h->x : nullptr;
+    if (!src)
+        return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
+    HIPTRY(h, hipMemcpyAsync(out, src, n * sizeof(float),
+                             kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_stepper_set_state(cwf_hip_stepper *t, int which, const float *in, uint64_t n, int kind)
+{
+    if (!t || !in)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    cwf_hip_system *h = t->sys;
+    if (int st = check_ready(h))
+        return st;
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "state span size mismatch");
+    float *dst = which == 0 ? t->u : which == 1 ? t->v : which == 2 ? t->a : which == 3 ? h->x : nullptr;
+    if (!dst)
+        return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
+    HIPTRY(h, hipMemcpyAsync(dst, in, n * sizeof(float),
+                             kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_stepper_set_external_force(cwf_hip_stepper *t, const float *f, uint64_t n, int kind)
+{
+    if (!t || !f)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    cwf_hip_system *h = t->sys;
+    if (int st = check_ready(h))
+        return st;
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "external force span size mismatch");
+    HIPTRY(h, hipMemcpyAsync(t->f, f, n * sizeof(float),
+                             kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_stepper_set_warm_start(cwf_hip_stepper *t, int enabled)
+{
+    if (!t)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
+    t->warm_start = enabled ? 1 : 0;
+    return 0;
+}
+
+int cwf_hip_stepper_time(const cwf_hip_stepper *t, double *current_time, double *time_step)
+{
+    if (!t)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
+    if (current_time)
+        *current_time = t->accumulated_time;
+    if (time_step)
+        *time_step = t->dt;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+// cwf_internal.hpp -- device data layout and host handle of the MI355X hot path.
+//
+// HBM layout (one handle):
+//   erec     uint4[E*4]  64-B element record: {conn0..3} {gx0 gy0 gz0 gx1} {gy1 gz1 gx2 gy2} {gz2 gx3 gy3 gz3}
+//                        (f32 gradient bits; one 64-B line per tet, read with 4 x dwordx4)
+//   vol      f32[E], mat u32[E]
+//   mass     f32[N], mask u32[N] (bit k = axis k constrained)
+//   off      u32[N+1], inc u32[4E] = (element << 2) | local_slot, ascending element per node
+//   dmat     f64[M*36] (+ isotropic flag: only the 12 structurally nonzero entries are used)
+//   vectors  f32[3N] node-interleaved (dof = 3n + k), the reference's DOF order
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/cwf_hip.h"
+
+namespace cwf
+{
+
+struct DevSys
+{
+    uint32_t N = 0;  // nodes
+    uint32_t E = 0;  // tets
+    uint32_t D = 0;  // dofs
+    uint32_t M = 0;  // materials
+    const uint4 *erec = nullptr;
+    const float *vol = nullptr;
+    const uint32_t *mat = nullptr;
+    const double *dmat = nullptr;
+    const float *mass = nullptr;
+    const uint32_t *mask = nullptr;
+    const uint32_t *off = nullptr;
+    const uint32_t *inc = nullptr;
+    double sK = 1.0;  // stiffness_scale
+    double sM = 0.0;  // mass_factor
+    int iso = 0;      // every material has the isotropic Voigt zero pattern
+};
+
+// Device-resident PCG control block: scalars of pcg.cpp:696-918 live here so that the
+// iteration loop never waits on the host (the host polls `active` every few iterations).
+struct Ctl
+{
+    double rho, alpha, beta, tol, res, rhs_norm, rhs_norm_raw, alpha_last, beta_last, denom, rr, rz;
+    unsigned long long iterations;  // completed iterations
+    int active;                     // 1 while the loop should keep running
+    int converged;
+    int error;       // cwf_status (0 = none)
+    int error_iter;  // iteration index for the error context
+};
+
+struct DevBuf
+{
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace cwf
+
+struct cwf_hip_system
+{
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int mode = CWF_MODE_PARITY;
+    cwf::DevSys ds{};
+    uint64_t reduction_block = 256;
+    uint64_t reduction_partials = 1;
+    // owned HBM
+    std::vector<void *> owned;
+    uint64_t bytes = 0;
+    // solver scratch (f32 dofs) and partials
+    float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
+    float *inv = nullptr;  // block Jacobi [9N]
+    double *part0 = nullptr, *part1 = nullptr;  // chunk / block partials
+    uint64_t part_cap = 0;
+    cwf::Ctl *ctl = nullptr;       // device
+    cwf::Ctl *ctl_host = nullptr;  // pinned
+    double *scal = nullptr;        // device scalar scratch
+    double *hist = nullptr;        // device residual history
+    uint64_t hist_cap = 0;
+    uint64_t hist_count = 0;
+    std::string err, ctx;
+    // live K_eff timing (cwf_hip_system_set_timing)
+    int timing = 0;
+    std::vector<hipEvent_t> ev;  // 2 per enqueued iteration of one batch
+    double keff_ms = 0.0;
+    uint64_t keff_count = 0;
+};
+
+namespace cwf
+{
+// set the handle's (or global) error and return the code
+int set_error(cwf_hip_system *h, int code, const std::string &msg, const std::string &ctx = "");
+int hip_fail(cwf_hip_system *h, hipError_t e, const char *what);
+
+// ---- kernels_parity.hip ----
+uint32_t parity_chunk_count(const cwf_hip_system *h);
+void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st);
+void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st);
+void parity_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st);
+void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b, const float *c, double *pab,
+                         double *pac, const Ctl *ctl, hipStream_t st);
+void parity_fold(const double *part, uint32_t count, double *out, hipStream_t st);
+void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
+void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, hipEvent_t e0 = nullptr,
+                          hipEvent_t e1 = nullptr);
+void launch_init_residual(const cwf_hip_system *h, const float *rhs, hipStream_t st);
+void launch_precond(const cwf_hip_system *h, const Ctl *ctl, hipStream_t st);
+void launch_p_init(const cwf_hip_system *h, hipStream_t st);
+
+// ---- kernels_fast.hip ----
+uint32_t fast_block_count(const cwf_hip_system *h);
+uint32_t fast_dot_blocks(uint32_t D);
+void fast_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, double *part,
+               hipStream_t st);
+void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, double *part,
+                  hipStream_t st);
+void fast_dot(const float *a, const float *b, const float *c, uint32_t D, double *pab, double *pac, hipStream_t st);
+void fast_fold(const double *part, uint32_t count, double *out, hipStream_t st);
+void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
+void fast_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, hipEvent_t e0 = nullptr,
+                        hipEvent_t e1 = nullptr);
+
+// ---- stepper.hip ----
+void stepper_predictor(uint32_t D, const float *u, const float *v, const float *a, float *up, float *vp, double dt,
+                       double beta, double gamma, hipStream_t st);
+void stepper_assemble_rhs(uint32_t N, const float *mass, const float *u, const float *v, const float *a,
+                          const float *f, float *rhs, float *damp, const double *c6, double ralpha, hipStream_t st);
+void stepper_rhs_damping(uint32_t D, float *rhs, const float *kd, float bf, hipStream_t st);
+void stepper_clamp(uint32_t N, const uint32_t *mask, const float *bcv, const float *u, float *rhs, hipStream_t st);
+void stepper_update(uint32_t D, const float *x, const float *up, const float *vp, float *u, float *v, float *a,
+                    float ib, float gob, hipStream_t st);
+
+}  // namespace cwf

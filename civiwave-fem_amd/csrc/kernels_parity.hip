@@ -1,0 +1,788 @@
+// kernels_parity.hip -- reference-order (bit-exact) kernels for gfx950.
+//
+// Every fold reproduces /root/reference/src/gpu/pcg.cpp in order:
+//  * node-centric gather over the ascending node->element CSR reproduces the scatter-add of
+//    pcg.cpp:653-661 (an fp64 accumulator per DOF that receives element contributions in
+//    ascending element order, starting at +0.0);
+//  * element math is fp64 on fp32 inputs with the reference operand order; structural zeros
+//    of B (and of an isotropic D) are skipped, which is exact: every fold starts at +0.0, a
+//    round-to-nearest sum that starts at +0.0 is never -0.0, so adding a +-0 term is a no-op;
+//  * this TU is compiled with -ffp-contract=off (no FMA contraction), IEEE fp64 div/sqrt.
+#include "cwf_internal.hpp"
+
+#include <algorithm>
+
+namespace cwf
+{
+namespace
+{
+
+constexpr int kBlock = 256;
+constexpr int kMaxLdsMaterials = 16;
+
+struct Grad
+{
+    float g[12];  // g[3a+k]
+    uint32_t c[4];
+};
+
+__device__ __forceinline__ void load_erec(const uint4 *__restrict__ erec, uint32_t e, Grad &r)
+{
+    const uint4 q0 = erec[4u * e + 0u];
+    const uint4 q1 = erec[4u * e + 1u];
+    const uint4 q2 = erec[4u * e + 2u];
+    const uint4 q3 = erec[4u * e + 3u];
+    r.c[0] = q0.x;
+    r.c[1] = q0.y;
+    r.c[2] = q0.z;
+    r.c[3] = q0.w;
+    r.g[0] = __uint_as_float(q1.x);
+    r.g[1] = __uint_as_float(q1.y);
+    r.g[2] = __uint_as_float(q1.z);
+    r.g[3] = __uint_as_float(q1.w);
+    r.g[4] = __uint_as_float(q2.x);
+    r.g[5] = __uint_as_float(q2.y);
+    r.g[6] = __uint_as_float(q2.z);
+    r.g[7] = __uint_as_float(q2.w);
+    r.g[8] = __uint_as_float(q3.x);
+    r.g[9] = __uint_as_float(q3.y);
+    r.g[10] = __uint_as_float(q3.z);
+    r.g[11] = __uint_as_float(q3.w);
+}
+
+// stress = D strain (pcg.cpp:632-640). ISO: 12-entry table [D00 D01 D02 D10 D11 D12 D20 D21 D22 D33 D44 D55].
+template <bool ISO>
+__device__ __forceinline__ void stress_fp64(const double *Dm, const double e[6], double s[6])
+{
+    if constexpr (ISO)
+    {
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+        {
+            double sum = 0.0;
+            sum += Dm[3 * r + 0] * e[0];
+            sum += Dm[3 * r + 1] * e[1];
+            sum += Dm[3 * r + 2] * e[2];
+            s[r] = sum;
+        }
+#pragma unroll
+        for (int r = 3; r < 6; ++r)
+        {
+            double sum = 0.0;
+            sum += Dm[6 + r] * e[r];
+            s[r] = sum;
+        }
+    }
+    else
+    {
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+        {
+            double sum = 0.0;
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                sum += Dm[6 * r + c] * e[c];
+            s[r] = sum;
+        }
+    }
+}
+
+// K_eff x, one thread per node, fp64 element math recomputed per incidence (pcg.cpp:505-694).
+template <bool ISO, bool SANITIZE>
+__global__ __launch_bounds__(kBlock) void k_keff_parity(DevSys s, const float *__restrict__ x,
+                                                        float *__restrict__ y, const Ctl *__restrict__ ctl)
+{
+    constexpr int kTab = ISO ? 12 : 36;
+    __shared__ double dtab[kMaxLdsMaterials * 36];
+    if (ctl && !ctl->active)
+        return;
+    const uint32_t nm = s.M < kMaxLdsMaterials ? s.M : kMaxLdsMaterials;
+    for (uint32_t i = threadIdx.x; i < nm * kTab; i += kBlock)
+    {
+        const uint32_t m = i / kTab, t = i % kTab;
+        uint32_t src;
+        if constexpr (ISO)
+            src = t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7;  // (3,3) (4,4) (5,5)
+        else
+            src = t;
+        dtab[i] = s.dmat[36u * m + src];
+    }
+    __syncthreads();
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+    const uint32_t jb = s.off[n], je = s.off[n + 1];
+    for (uint32_t j = jb; j < je; ++j)
+    {
+        const uint32_t inc = s.inc[j];
+        const uint32_t e = inc >> 2, a = inc & 3u;
+        Grad G;
+        load_erec(s.erec, e, G);
+        double u[12];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            const uint32_t m = G.c[q];
+            const float *xp = x + 3u * m;
+            double u0 = (double)xp[0], u1 = (double)xp[1], u2 = (double)xp[2];
+            if constexpr (SANITIZE)
+            {
+                const uint32_t mk = s.mask[m];
+                if (mk & 1u)
+                    u0 = 0.0;
+                if (mk & 2u)
+                    u1 = 0.0;
+                if (mk & 4u)
+                    u2 = 0.0;
+            }
+            u[3 * q + 0] = u0;
+            u[3 * q + 1] = u1;
+            u[3 * q + 2] = u2;
+        }
+        double gx[4], gy[4], gz[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            gx[q] = (double)G.g[3 * q + 0];
+            gy[q] = (double)G.g[3 * q + 1];
+            gz[q] = (double)G.g[3 * q + 2];
+        }
+        // strain = B u, columns ascending (pcg.cpp:622-630)
+        double eps[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            eps[0] += gx[q] * u[3 * q + 0];
+            eps[1] += gy[q] * u[3 * q + 1];
+            eps[2] += gz[q] * u[3 * q + 2];
+            eps[3] += gy[q] * u[3 * q + 0];
+            eps[3] += gx[q] * u[3 * q + 1];
+            eps[4] += gz[q] * u[3 * q + 1];
+            eps[4] += gy[q] * u[3 * q + 2];
+            eps[5] += gz[q] * u[3 * q + 0];
+            eps[5] += gx[q] * u[3 * q + 2];
+        }
+        const uint32_t mi = s.mat[e];
+        const double *Dm = mi < (uint32_t)kMaxLdsMaterials ? dtab + kTab * mi : nullptr;
+        double sig[6];
+        if (Dm)
+            stress_fp64<ISO>(Dm, eps, sig);
+        else
+        {
+            double tab[36];
+            for (int t = 0; t < kTab; ++t)
+            {
+                uint32_t src;
+                if constexpr (ISO)
+                    src = t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7;
+                else
+                    src = t;
+                tab[t] = s.dmat[36u * mi + src];
+            }
+            stress_fp64<ISO>(tab, eps, sig);
+        }
+        const double vol = (double)s.vol[e] * s.sK;  // pcg.cpp:642
+        const double ax = a == 0 ? gx[0] : a == 1 ? gx[1] : a == 2 ? gx[2] : gx[3];
+        const double ay = a == 0 ? gy[0] : a == 1 ? gy[1] : a == 2 ? gy[2] : gy[3];
+        const double az = a == 0 ? gz[0] : a == 1 ? gz[1] : a == 2 ? gz[2] : gz[3];
+        // f[col] = (sum_r B[r][col] sigma_r) * vol (pcg.cpp:643-651)
+        double fx = 0.0, fy = 0.0, fz = 0.0;
+        fx += ax * sig[0];
+        fx += ay * sig[3];
+        fx += az * sig[5];
+        fy += ay * sig[1];
+        fy += ax * sig[3];
+        fy += az * sig[4];
+        fz += az * sig[2];
+        fz += ay * sig[4];
+        fz += ax * sig[5];
+        acc0 += fx * vol;
+        acc1 += fy * vol;
+        acc2 += fz * vol;
+    }
+    // mass term (pcg.cpp:664-672), Dirichlet identity rows (674-686), cast (688-691)
+    const uint32_t mk = s.mask[n];
+    const double m = (double)s.mass[n] * s.sM;
+    const float x0 = x[3u * n + 0], x1 = x[3u * n + 1], x2 = x[3u * n + 2];
+    const double s0 = (SANITIZE && (mk & 1u)) ? 0.0 : (double)x0;
+    const double s1 = (SANITIZE && (mk & 2u)) ? 0.0 : (double)x1;
+    const double s2 = (SANITIZE && (mk & 4u)) ? 0.0 : (double)x2;
+    acc0 += m * s0;
+    acc1 += m * s1;
+    acc2 += m * s2;
+    if (mk & 1u)
+        acc0 = (double)x0;
+    if (mk & 2u)
+        acc1 = (double)x1;
+    if (mk & 4u)
+        acc2 = (double)x2;
+    y[3u * n + 0] = (float)acc0;
+    y[3u * n + 1] = (float)acc1;
+    y[3u * n + 2] = (float)acc2;
+}
+
+__device__ void invert_spd_3x3(double m[9], double inv[9])
+{
+    // pcg.cpp:215-268
+    const double kDetTol = 1.0e-12;
+    auto det3 = [&]() {
+        return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+               m[2] * (m[3] * m[7] - m[4] * m[6]);
+    };
+    double det = det3();
+    if (fabs(det) < kDetTol)
+    {
+        const double md = fmax(fmax(m[0], m[4]), m[8]);
+        const double eps = fmax(1.0e-6, md * 1.0e-6 + 1.0e-12);
+        m[0] += eps;
+        m[4] += eps;
+        m[8] += eps;
+        det = det3();
+    }
+    if (fabs(det) < kDetTol)
+    {
+        for (int i = 0; i < 9; ++i)
+            inv[i] = 0.0;
+        inv[0] = 1.0 / fmax(m[0], 1.0e-6);
+        inv[4] = 1.0 / fmax(m[4], 1.0e-6);
+        inv[8] = 1.0 / fmax(m[8], 1.0e-6);
+        return;
+    }
+    const double id = 1.0 / det;
+    inv[0] = (m[4] * m[8] - m[5] * m[7]) * id;
+    inv[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+    inv[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    inv[3] = (m[5] * m[6] - m[3] * m[8]) * id;
+    inv[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+    inv[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    inv[6] = (m[3] * m[7] - m[4] * m[6]) * id;
+    inv[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+    inv[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+// Block-Jacobi inverse, one thread per node (pcg.cpp:270-408): the node's diagonal 3x3 block of
+// every incident K_e in ascending element order, + m*s_M, fp64 inverse, constrained rows -> identity.
+__global__ __launch_bounds__(kBlock) void k_block_jacobi_parity(DevSys s, float *__restrict__ inv_out)
+{
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    double blk[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t j = s.off[n]; j < s.off[n + 1]; ++j)
+    {
+        const uint32_t inc = s.inc[j];
+        const uint32_t e = inc >> 2, a = inc & 3u;
+        const uint4 *rec = s.erec + 4u * e;
+        const float *gf = reinterpret_cast<const float *>(rec + 1);
+        const double gx = (double)gf[3 * a + 0], gy = (double)gf[3 * a + 1], gz = (double)gf[3 * a + 2];
+        const double *Dm = s.dmat + 36u * s.mat[e];
+        // nonzero rows of B column 3a+k, ascending: k=0 {0:gx,3:gy,5:gz} k=1 {1:gy,3:gx,4:gz} k=2 {2:gz,4:gy,5:gx}
+        const int rows[3][3] = {{0, 3, 5}, {1, 3, 4}, {2, 4, 5}};
+        const double vals[3][3] = {{gx, gy, gz}, {gy, gx, gz}, {gz, gy, gx}};
+        double DB[6][3];
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+            {
+                double sum = 0.0;
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+                    sum += Dm[6 * r + rows[k][t]] * vals[k][t];
+                DB[r][k] = sum;
+            }
+        const double sv = (double)s.vol[e] * s.sK;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+            {
+                double sum = 0.0;
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+                    sum += vals[i][t] * DB[rows[i][t]][k];
+                blk[3 * i + k] += sum * sv;
+            }
+    }
+    const double m = (double)s.mass[n] * s.sM;
+    blk[0] += m;
+    blk[4] += m;
+    blk[8] += m;
+    double iv[9];
+    invert_spd_3x3(blk, iv);
+    const uint32_t mk = s.mask[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (mk & (1u << k))
+            for (int c = 0; c < 3; ++c)
+                iv[3 * k + c] = (k == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        inv_out[9u * n + i] = (float)iv[i];
+}
+
+// ---- reductions (pcg.cpp:170-207): sequential fp64 fold inside each reduction_block chunk ----
+
+// generic chunk size: one thread per chunk, sequential loads
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_dot_chunks_generic(const float *__restrict__ a,
+                                                               const float *__restrict__ b,
+                                                               const float *__restrict__ c, uint32_t D,
+                                                               uint32_t B, uint32_t chunks, double *__restrict__ pab,
+                                                               double *__restrict__ pac, const Ctl *__restrict__ ctl)
+{
+    if (ctl && !ctl->active)
+        return;
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= chunks)
+        return;
+    const uint32_t beg = k * B, end = min(beg + B, D);
+    double s0 = 0.0, s1 = 0.0;
+    for (uint32_t i = beg; i < end; ++i)
+    {
+        const double av = (double)a[i];
+        s0 += av * (double)b[i];
+        if constexpr (NV == 2)
+            s1 += av * (double)c[i];
+    }
+    pab[k] = s0;
+    if constexpr (NV == 2)
+        pac[k] = s1;
+}
+
+// chunk = 256 DOFs: one wave per 64 chunks, 32-DOF slabs staged through LDS so that the
+// global loads are coalesced 128-B runs while each lane keeps its chunk's sequential fold.
+template <int NV>
+__global__ __launch_bounds__(64) void k_dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
+                                                      const float *__restrict__ c, uint32_t D, uint32_t chunks,
+                                                      double *__restrict__ pab, double *__restrict__ pac,
+                                                      const Ctl *__restrict__ ctl)
+{
+    __shared__ float sa[64][33];
+    __shared__ float sb[64][33];
+    __shared__ float sc[NV == 2 ? 64 : 1][33];
+    if (ctl && !ctl->active)
+        return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t c0 = blockIdx.x * 64u;
+    double s0 = 0.0, s1 = 0.0;
+    for (uint32_t step = 0; step < 8; ++step)
+    {
+#pragma unroll 8
+        for (uint32_t q = 0; q < 32; ++q)
+        {
+            const uint32_t chunk = q * 2u + (lane >> 5), o = lane & 31u;
+            const uint64_t gi = (uint64_t)(c0 + chunk) * 256u + step * 32u + o;
+            const bool ok = gi < D;
+            sa[chunk][o] = ok ? a[gi] : 0.0f;
+            sb[chunk][o] = ok ? b[gi] : 0.0f;
+            if constexpr (NV == 2)
+                sc[chunk][o] = ok ? c[gi] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (uint32_t i = 0; i < 32; ++i)
+        {
+            const double av = (double)sa[lane][i];
+            s0 += av * (double)sb[lane][i];
+            if constexpr (NV == 2)
+                s1 += av * (double)sc[lane][i];
+        }
+        __syncthreads();
+    }
+    const uint32_t k = c0 + lane;
+    if (k < chunks)
+    {
+        pab[k] = s0;
+        if constexpr (NV == 2)
+            pac[k] = s1;
+    }
+}
+
+// ordered sequential fold over chunk partials: total += partial[c] (pcg.cpp:200)
+template <int NC>
+__device__ void fold_seq(const double *__restrict__ p0, const double *__restrict__ p1, uint32_t count, double &t0,
+                         double &t1)
+{
+    double a0 = 0.0, a1 = 0.0;
+    uint32_t c = 0;
+    for (; c + 8 <= count; c += 8)
+    {
+        double v0[8], v1[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+        {
+            v0[q] = p0[c + q];
+            if constexpr (NC == 2)
+                v1[q] = p1[c + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+        {
+            a0 += v0[q];
+            if constexpr (NC == 2)
+                a1 += v1[q];
+        }
+    }
+    for (; c < count; ++c)
+    {
+        a0 += p0[c];
+        if constexpr (NC == 2)
+            a1 += p1[c];
+    }
+    t0 = a0;
+    t1 = a1;
+}
+
+__global__ void k_fold1(const double *__restrict__ p, uint32_t count, double *__restrict__ out)
+{
+    double t0, t1;
+    fold_seq<1>(p, nullptr, count, t0, t1);
+    out[0] = t0;
+}
+
+// ---- PCG scalar phases (single thread), pcg.cpp:768-895 ----
+
+__global__ void k_pcg_init_scalars(Ctl *ctl, const double *__restrict__ p_rhs, const double *__restrict__ p_rr,
+                                   uint32_t count, double rel_tol, double *__restrict__ hist)
+{
+    double rhs_sq, rr;
+    fold_seq<2>(p_rhs, p_rr, count, rhs_sq, rr);
+    double rhs_norm = sqrt(rhs_sq);
+    if (rhs_norm < 1.0e-12)
+        rhs_norm = 1.0;
+    const double res = sqrt(rr);
+    Ctl c{};
+    c.res = res;
+    c.rhs_norm = rhs_norm;
+    c.rhs_norm_raw = sqrt(rhs_sq);
+    c.tol = rel_tol * rhs_norm;
+    c.iterations = 0;
+    c.converged = res <= c.tol ? 1 : 0;
+    c.active = c.converged ? 0 : 1;
+    c.error = 0;
+    c.error_iter = 0;
+    hist[0] = res;
+    *ctl = c;
+}
+
+__global__ void k_pcg_init_rho(Ctl *ctl, const double *__restrict__ p_rz, uint32_t count)
+{
+    if (!ctl->active)
+        return;
+    double rho, unused;
+    fold_seq<1>(p_rz, nullptr, count, rho, unused);
+    ctl->rho = rho;
+    if (fabs(rho) < 1.0e-18)
+    {
+        ctl->error = CWF_ERR_RHO_ZERO;
+        ctl->error_iter = -1;
+        ctl->active = 0;
+    }
+}
+
+__global__ void k_pcg_alpha(Ctl *ctl, const double *__restrict__ p_pAp, uint32_t count)
+{
+    if (!ctl->active)
+        return;
+    double denom, unused;
+    fold_seq<1>(p_pAp, nullptr, count, denom, unused);
+    ctl->denom = denom;
+    if (fabs(denom) < 1.0e-18)
+    {
+        ctl->error = CWF_ERR_DENOM_ZERO;
+        ctl->error_iter = (int)ctl->iterations;
+        ctl->active = 0;
+        return;
+    }
+    const double alpha = ctl->rho / denom;
+    ctl->alpha = alpha;
+    ctl->alpha_last = alpha;
+}
+
+__global__ void k_pcg_beta(Ctl *ctl, const double *__restrict__ p_rr, const double *__restrict__ p_rz,
+                           uint32_t count, double *__restrict__ hist)
+{
+    if (!ctl->active)
+        return;
+    double rr, rz;
+    fold_seq<2>(p_rr, p_rz, count, rr, rz);
+    const double res = sqrt(rr);
+    const unsigned long long it = ctl->iterations;
+    ctl->res = res;
+    ctl->iterations = it + 1;
+    hist[it + 1] = res;
+    if (res <= ctl->tol)
+    {
+        ctl->converged = 1;
+        ctl->active = 0;
+        return;
+    }
+    if (fabs(ctl->rho) < 1.0e-18)
+    {
+        ctl->error = CWF_ERR_RHO_ZERO;
+        ctl->error_iter = (int)it;
+        ctl->active = 0;
+        return;
+    }
+    const double beta = rz / ctl->rho;
+    ctl->beta = beta;
+    ctl->beta_last = beta;
+    ctl->rho = rz;
+}
+
+// ---- node-wise vector phases ----
+
+// r = rhs - Ap (f32), then enforce_dirichlet_solution (pcg.cpp:761-766, 458-475)
+__global__ __launch_bounds__(kBlock) void k_init_residual(DevSys s, const float *__restrict__ rhs,
+                                                          const float *__restrict__ Ap, float *__restrict__ x,
+                                                          float *__restrict__ r)
+{
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    const uint32_t mk = s.mask[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        const uint32_t d = 3u * n + k;
+        float rv = rhs[d] - Ap[d];
+        if (mk & (1u << k))
+        {
+            x[d] = rhs[d];
+            rv = 0.0f;
+        }
+        r[d] = rv;
+    }
+}
+
+__device__ __forceinline__ void precond_node(const float *__restrict__ inv, uint32_t n, uint32_t mk, const float rv[3],
+                                             float z[3])
+{
+    // pcg.cpp:426-453
+    const double r0 = (double)rv[0], r1 = (double)rv[1], r2 = (double)rv[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        double sum = 0.0;
+        sum += (double)inv[9u * n + 3 * k + 0] * r0;
+        sum += (double)inv[9u * n + 3 * k + 1] * r1;
+        sum += (double)inv[9u * n + 3 * k + 2] * r2;
+        z[k] = (mk & (1u << k)) ? 0.0f : (float)sum;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_precond(DevSys s, const float *__restrict__ inv,
+                                                    const float *__restrict__ r, float *__restrict__ z,
+                                                    const Ctl *__restrict__ ctl)
+{
+    if (ctl && !ctl->active)
+        return;
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    const float rv[3] = {r[3u * n], r[3u * n + 1], r[3u * n + 2]};
+    float zv[3];
+    precond_node(inv, n, s.mask[n], rv, zv);
+    z[3u * n] = zv[0];
+    z[3u * n + 1] = zv[1];
+    z[3u * n + 2] = zv[2];
+}
+
+// p = z, constrained -> 0 (pcg.cpp:815-828)
+__global__ __launch_bounds__(kBlock) void k_p_init(DevSys s, const float *__restrict__ z, float *__restrict__ p,
+                                                   const Ctl *__restrict__ ctl)
+{
+    if (!ctl->active)
+        return;
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    const uint32_t mk = s.mask[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        p[3u * n + k] = (mk & (1u << k)) ? 0.0f : z[3u * n + k];
+}
+
+// x += f32(alpha p); r -= f32(alpha Ap); enforce; z = M^-1 r  (pcg.cpp:854-860, 877)
+__global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__restrict__ rhs,
+                                                   const float *__restrict__ inv, const float *__restrict__ p,
+                                                   const float *__restrict__ Ap, float *__restrict__ x,
+                                                   float *__restrict__ r, float *__restrict__ z,
+                                                   const Ctl *__restrict__ ctl)
+{
+    if (!ctl->active)
+        return;
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    const double alpha = ctl->alpha;
+    const uint32_t mk = s.mask[n];
+    float rv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        const uint32_t d = 3u * n + k;
+        float xv = x[d] + (float)(alpha * (double)p[d]);
+        float rr = r[d] - (float)(alpha * (double)Ap[d]);
+        if (mk & (1u << k))
+        {
+            xv = rhs[d];
+            rr = 0.0f;
+        }
+        x[d] = xv;
+        r[d] = rr;
+        rv[k] = rr;
+    }
+    float zv[3];
+    precond_node(inv, n, mk, rv, zv);
+    z[3u * n] = zv[0];
+    z[3u * n + 1] = zv[1];
+    z[3u * n + 2] = zv[2];
+}
+
+// p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
+__global__ __launch_bounds__(kBlock) void k_p_update(DevSys s, const float *__restrict__ z, float *__restrict__ p,
+                                                     const Ctl *__restrict__ ctl)
+{
+    if (!ctl->active)
+        return;
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    const double beta = ctl->beta;
+    const uint32_t mk = s.mask[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        const uint32_t d = 3u * n + k;
+        const float pv = (float)((double)z[d] + beta * (double)p[d]);
+        p[d] = (mk & (1u << k)) ? 0.0f : pv;
+    }
+}
+
+inline unsigned grid_for(uint32_t n, uint32_t b) { return (n + b - 1) / b; }
+
+}  // namespace
+
+uint32_t parity_chunk_count(const cwf_hip_system *h)
+{
+    const uint64_t B = h->reduction_block ? h->reduction_block : 1;
+    return (uint32_t)((h->ds.D + B - 1) / B);
+}
+
+void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
+{
+    if (s.N == 0)
+        return;
+    const dim3 g(grid_for(s.N, kBlock)), b(kBlock);
+    if (s.iso)
+    {
+        if (sanitize)
+            k_keff_parity<true, true><<<g, b, 0, st>>>(s, x, y, ctl);
+        else
+            k_keff_parity<true, false><<<g, b, 0, st>>>(s, x, y, ctl);
+    }
+    else
+    {
+        if (sanitize)
+            k_keff_parity<false, true><<<g, b, 0, st>>>(s, x, y, ctl);
+        else
+            k_keff_parity<false, false><<<g, b, 0, st>>>(s, x, y, ctl);
+    }
+}
+
+void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
+{
+    parity_keff_ds(h->ds, x, y, sanitize, ctl, st);
+}
+
+void parity_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st)
+{
+    if (h->ds.N == 0)
+        return;
+    k_block_jacobi_parity<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, inv);
+}
+
+void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b, const float *c, double *pab,
+                         double *pac, const Ctl *ctl, hipStream_t st)
+{
+    const uint32_t D = h->ds.D, B = (uint32_t)(h->reduction_block ? h->reduction_block : 1);
+    const uint32_t chunks = parity_chunk_count(h);
+    if (chunks == 0)
+        return;
+    if (B == 256)
+    {
+        if (c)
+            k_dot_chunks256<2><<<grid_for(chunks, 64), 64, 0, st>>>(a, b, c, D, chunks, pab, pac, ctl);
+        else
+            k_dot_chunks256<1><<<grid_for(chunks, 64), 64, 0, st>>>(a, b, c, D, chunks, pab, pac, ctl);
+    }
+    else
+    {
+        if (c)
+            k_dot_chunks_generic<2><<<grid_for(chunks, kBlock), kBlock, 0, st>>>(a, b, c, D, B, chunks, pab, pac,
+                                                                                ctl);
+        else
+            k_dot_chunks_generic<1><<<grid_for(chunks, kBlock), kBlock, 0, st>>>(a, b, c, D, B, chunks, pab, pac,
+                                                                                ctl);
+    }
+}
+
+void parity_fold(const double *part, uint32_t count, double *out, hipStream_t st)
+{
+    k_fold1<<<1, 1, 0, st>>>(part, count, out);
+}
+
+void launch_init_residual(const cwf_hip_system *h, const float *rhs, hipStream_t st)
+{
+    k_init_residual<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, rhs, h->Ap, h->x, h->r);
+}
+
+void launch_precond(const cwf_hip_system *h, const Ctl *ctl, hipStream_t st)
+{
+    k_precond<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, h->inv, h->r, h->z, ctl);
+}
+
+void launch_p_init(const cwf_hip_system *h, hipStream_t st)
+{
+    k_p_init<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, h->z, h->p, h->ctl);
+}
+
+// solve_pcg prologue (pcg.cpp:744-828). Requires x (warm start or zeroed) on device.
+void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st)
+{
+    const DevSys &s = h->ds;
+    const uint32_t chunks = parity_chunk_count(h);
+    parity_block_jacobi(h, h->inv, st);
+    parity_keff(h, h->x, h->Ap, true, nullptr, st);
+    k_init_residual<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->Ap, h->x, h->r);
+    parity_dot_partials(h, rhs, rhs, nullptr, h->part0, nullptr, nullptr, st);
+    parity_dot_partials(h, h->r, h->r, nullptr, h->part1, nullptr, nullptr, st);
+    k_pcg_init_scalars<<<1, 1, 0, st>>>(h->ctl, h->part0, h->part1, chunks, rel_tol, h->hist);
+    k_precond<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->inv, h->r, h->z, h->ctl);
+    parity_dot_partials(h, h->r, h->z, nullptr, h->part0, nullptr, h->ctl, st);
+    k_pcg_init_rho<<<1, 1, 0, st>>>(h->ctl, h->part0, chunks);
+    k_p_init<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
+}
+
+// one PCG iteration (pcg.cpp:830-915); no-op once ctl->active == 0
+void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
+{
+    const DevSys &s = h->ds;
+    const uint32_t chunks = parity_chunk_count(h);
+    if (e0)
+        (void)hipEventRecord(e0, st);
+    parity_keff(h, h->p, h->Ap, false, h->ctl, st);
+    if (e1)
+        (void)hipEventRecord(e1, st);
+    parity_dot_partials(h, h->p, h->Ap, nullptr, h->part0, nullptr, h->ctl, st);
+    k_pcg_alpha<<<1, 1, 0, st>>>(h->ctl, h->part0, chunks);
+    k_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl);
+    parity_dot_partials(h, h->r, h->r, h->z, h->part0, h->part1, h->ctl, st);
+    k_pcg_beta<<<1, 1, 0, st>>>(h->ctl, h->part0, h->part1, chunks, h->hist);
+    k_p_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
+}
+
+}  // namespace cwf

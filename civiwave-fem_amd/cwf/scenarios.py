@@ -1,0 +1,65 @@
+"""Synthetic scenarios of BASELINE.json's configs: structured Kuhn-tet
+blocks, x=0 face fixed, gravity + a -500 N point load per node of the x=max face, steel-like
+material (E=30 GPa, nu=0.2, rho=2500), Newmark dt=0.01."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import meshgen, pack
+from .physics import (Assignment, Config, Damping, DirichletFix, Loads, Material, PointLoad, SolverSettings,
+                      TimeSettings, compute_rayleigh, effective_scalars, make_coefficients, make_properties)
+
+
+@dataclass
+class Case:
+    name: str
+    mesh: pack.Mesh
+    cfg: Config
+    packing: pack.PackingResult
+
+    @property
+    def materials(self):
+        return [make_properties(m) for m in self.cfg.materials]
+
+    @property
+    def rayleigh(self):
+        return compute_rayleigh(self.cfg.damping)
+
+    def scalars(self, dt: float | None = None):
+        c = make_coefficients(dt if dt is not None else self.cfg.time.initial_dt)
+        return effective_scalars(c, self.rayleigh)
+
+    def static_rhs(self) -> np.ndarray:
+        """external force with the constrained rows zeroed (the survey drivers' solve_pcg RHS)."""
+        rhs = self.packing.external_force.copy()
+        mask = np.repeat(self.packing.bc_mask, 3) & np.tile(np.array([1, 2, 4], np.uint32), self.packing.node_count)
+        rhs[mask != 0] = 0.0
+        return rhs
+
+
+def make_config(xi=0.02, w=(5.0, 50.0), tol=3e-4, max_iterations=2000, dt=0.01, gravity=(0.0, 0.0, -9.81),
+                point=(0.0, 0.0, -500.0), point_group="TIP") -> Config:
+    return Config(materials=[Material("steel", 30.0e9, 0.2, 2500.0)], assignments=[Assignment("SOLID", "steel")],
+                  damping=Damping(xi, w[0], w[1]), time=TimeSettings(dt, False, 0.0, 0.0),
+                  solver=SolverSettings("pcg", "block_jacobi", tol, 1.0e-5, max_iterations),
+                  loads=Loads(tuple(gravity), [], [PointLoad(point_group, tuple(point))]),
+                  dirichlet=[DirichletFix("FIXED", (True, True, True), (0.0, 0.0, 0.0))])
+
+
+def block_case(nx, ny, nz, h=0.1, jitter=False, **cfg_kw) -> Case:
+    tm = meshgen.kuhn_block(nx, ny, nz, h)
+    if jitter:
+        tm = meshgen.jitter_and_permute(tm, h)
+    mesh = pack.from_tetmesh(tm)
+    cfg = make_config(**cfg_kw)
+    return Case(f"kuhn{nx}x{ny}x{nz}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
+
+
+def config_case(key: str, max_iterations: int = 2000) -> Case:
+    c = meshgen.CONFIGS[key]
+    case = block_case(*c["shape"], h=c["h"], jitter=c.get("jitter", False), xi=c["xi"], w=c["w"], tol=c["tol"],
+                      max_iterations=max_iterations)
+    case.name = f"{key}: {c['name']}"
+    return case

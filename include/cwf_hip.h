@@ -1,0 +1,219 @@
+/*
+ * cwf_hip.h -- C-ABI of the MI355X (gfx950) matrix-free Newmark/PCG hot path.
+ *
+ * Drop-in boundary for CiviWave-FEM's L4 solver core. Every entry point below replaces a
+ * reference C++ interface (cited as /root/reference file:line); plain pointers and sizes
+ * only, no torch or C++ types, no exceptions. Return value: 0 on success, a negative
+ * cwf_status on failure; cwf_hip_last_error()/cwf_hip_last_context() then hold the
+ * reference's message text and breadcrumb (e.g. "CG denominator approached zero",
+ * "iteration=12").
+ *
+ * Threading: one handle = one device + one HIP stream, externally synchronised
+ * (the reference Stepper is single-threaded, newmark_stepper.hpp:92). Distinct handles may
+ * run concurrently on distinct threads.
+ *
+ * Pointer kinds: every vector argument is host memory when `ptr_kind == CWF_PTR_HOST`
+ * (copied in/out, call is synchronous) or device memory (HBM) when CWF_PTR_DEVICE
+ * (used in place, the call still returns after the work completes on the handle's stream).
+ */
+#ifndef CWF_HIP_H
+#define CWF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CWF_HIP_ABI_VERSION 1
+
+typedef enum cwf_status
+{
+    CWF_OK = 0,
+    CWF_ERR_SIZE = -1,           /* pcg.cpp:82-125 "... size mismatch" */
+    CWF_ERR_NODE_RANGE = -2,     /* pcg.cpp:609-613 "element connectivity references node out of range" */
+    CWF_ERR_MATERIAL_RANGE = -3, /* pcg.cpp:566-570 "element references material out of range" */
+    CWF_ERR_MATERIALS = -4,      /* pcg.cpp:126-129 "materials table is empty" */
+    CWF_ERR_REDUCTION = -5,      /* pcg.cpp:130-137 reduction_block / reduction_partials == 0 */
+    CWF_ERR_MAX_ITERATIONS = -6, /* pcg.cpp:739-742 "max_iterations must be >= 1" */
+    CWF_ERR_RHO_ZERO = -7,       /* pcg.cpp:810-813, 889-892 */
+    CWF_ERR_DENOM_ZERO = -8,     /* pcg.cpp:846-849 "CG denominator approached zero" */
+    CWF_ERR_ALLOC = -9,          /* pcg.cpp:65-68 workspace allocation failure */
+    CWF_ERR_HIP = -10,           /* HIP runtime error (message holds hipGetErrorString) */
+    CWF_ERR_ARGUMENT = -11,      /* NULL handle / pointer */
+    CWF_ERR_COMM = -12,          /* RCCL / communicator failure */
+    CWF_ERR_UNSUPPORTED = -13
+} cwf_status;
+
+typedef enum cwf_ptr_kind
+{
+    CWF_PTR_HOST = 0,
+    CWF_PTR_DEVICE = 1
+} cwf_ptr_kind;
+
+/* Arithmetic mode. PARITY reproduces the reference fold order bit for bit (fp64 element math,
+ * 256-DOF chunked sequential fp64 dots). FAST: fp32 element math, fp64 tree reductions,
+ * tolerance-checked against the oracle. Both consume the same inputs. */
+typedef enum cwf_mode
+{
+    CWF_MODE_PARITY = 0,
+    CWF_MODE_FAST = 1
+} cwf_mode;
+
+/* Mirrors cwf::gpu::pcg::MatrixFreeSystem (include/cwf/gpu/pcg.hpp:67-86) plus the packed
+ * adjacency of cwf::mesh::pack::AdjacencyBuffers (include/cwf/mesh/pack.hpp:120-125).
+ * All pointers are host memory; the handle copies them to HBM at create time. */
+typedef struct cwf_system_desc
+{
+    uint64_t node_count;
+    uint64_t element_count;
+    uint64_t dof_count;                 /* must equal 3 * node_count */
+    const uint32_t *element_connectivity; /* [element_count * 8], tets use slots 0..3 */
+    const float *element_gradients;     /* [element_count * 24], grad N_a xyz, a = 0..7 */
+    const float *element_volume;        /* [element_count] */
+    const uint32_t *element_material_index; /* [element_count] */
+    const double *material_stiffness;   /* [material_count * 36], ElasticProperties::stiffness */
+    uint64_t material_count;
+    const float *lumped_mass;           /* [node_count] */
+    const uint32_t *bc_mask;            /* [node_count], bit0/1/2 = x/y/z constrained */
+    const uint32_t *adjacency_offsets;  /* [node_count + 1] or NULL (built from connectivity) */
+    const uint32_t *adjacency_elements; /* [offsets[N]] ascending element index per node, or NULL */
+    const uint8_t *adjacency_local;     /* [offsets[N]] local slot 0..3, or NULL */
+    double stiffness_scale;             /* 1 + a1 * beta_R */
+    double mass_factor;                 /* a0 + a1 * alpha_R */
+    uint64_t reduction_block;           /* 256 in the reference (pack.hpp:183) */
+    uint64_t reduction_partials;        /* >= ceil(dof_count / reduction_block) */
+    int32_t mode;                       /* cwf_mode */
+    int32_t reserved;
+} cwf_system_desc;
+
+/* PcgSettings (pcg.hpp:115-120) */
+typedef struct cwf_pcg_settings
+{
+    uint64_t max_iterations;
+    double relative_tolerance;
+    int32_t warm_start;
+    int32_t check_interval; /* iterations enqueued between host convergence checks; 0 = auto */
+} cwf_pcg_settings;
+
+/* PcgTelemetry (pcg.hpp:125-133) */
+typedef struct cwf_pcg_telemetry
+{
+    uint64_t iterations;
+    double residual_norm;
+    double rhs_norm;
+    double alpha_last;
+    double beta_last;
+    int32_t converged;
+    int32_t reserved;
+} cwf_pcg_telemetry;
+
+typedef struct cwf_hip_system cwf_hip_system;
+
+/* Library / device info. */
+int cwf_hip_abi_version(void);
+int cwf_hip_device_count(int *count);
+const char *cwf_hip_last_error(const cwf_hip_system *h);   /* h may be NULL: last create error */
+const char *cwf_hip_last_context(const cwf_hip_system *h);
+
+/* Create / destroy: replaces building a MatrixFreeSystem over packed buffers
+ * (newmark_stepper.cpp:1034-1049) and DeviceBufferArena::create (device_buffers.cpp:132). */
+int cwf_hip_system_create(const cwf_system_desc *desc, int device, cwf_hip_system **out);
+void cwf_hip_system_destroy(cwf_hip_system *h);
+/* update stiffness_scale / mass_factor (newmark_stepper.cpp:1322-1326) */
+int cwf_hip_system_set_scalars(cwf_hip_system *h, double stiffness_scale, double mass_factor);
+int cwf_hip_system_set_mode(cwf_hip_system *h, int mode);
+/* bytes of HBM held by the handle */
+int cwf_hip_system_memory(const cwf_hip_system *h, uint64_t *bytes);
+
+/* Live kernel timing (measurement support, not a reference interface): when enabled, every
+ * K_eff launch inside solve_pcg / stepper_step is bracketed by hipEvents on the handle's stream;
+ * cwf_hip_system_timing returns the summed device time (ms) and launch count of the launches that
+ * did work, and resets the accumulators. */
+int cwf_hip_system_set_timing(cwf_hip_system *h, int enabled);
+int cwf_hip_system_timing(cwf_hip_system *h, double *keff_ms, uint64_t *keff_launches);
+/* Standalone timed K_eff: `reps` launches of the PCG-loop SpMV (no sanitize) on device x -> y,
+ * bracketed by one hipEvent pair; *avg_ms = elapsed / reps. */
+int cwf_hip_keff_timed(cwf_hip_system *h, const float *x_dev, float *y_dev, int reps, double *avg_ms);
+
+/* cwf::gpu::pcg::apply_keff (pcg.hpp:161-163, pcg.cpp:505-694): y = K_eff x with
+ * Dirichlet identity rows. n = dof_count. */
+int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, int ptr_kind);
+
+/* cwf::gpu::pcg::build_block_jacobi_inverse (pcg.hpp:226-227, pcg.cpp:479-503):
+ * inv_out[node*9 + 3*i + j], row-major f32. n = node_count * 9. */
+int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int ptr_kind);
+
+/* dot_accumulate (pcg.cpp:170-207): chunked fp64 dot of two f32 DOF vectors. partials may be
+ * NULL; otherwise [reduction_partials] chunk partials are written (host or device by ptr_kind). */
+int cwf_hip_dot(cwf_hip_system *h, const float *a, const float *b, uint64_t n, int ptr_kind, double *out,
+                double *partials);
+
+/* cwf::gpu::pcg::solve_pcg (pcg.hpp:210-212, pcg.cpp:696-918). x_inout is the warm start
+ * (settings->warm_start) and receives the solution; residual_out (nullable) receives r. */
+int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_settings *settings, float *x_inout,
+                      float *residual_out, uint64_t n, int ptr_kind, cwf_pcg_telemetry *telemetry);
+
+/* Residual history of the last solve_pcg (|r| after each iteration, entry 0 = initial),
+ * up to `capacity` entries. Returns the number written via *count. */
+int cwf_hip_residual_history(cwf_hip_system *h, double *out, uint64_t capacity, uint64_t *count);
+
+/* ---------------------------------------------------------------------------------------
+ * Newmark stepper: cwf::gpu::newmark::Stepper (newmark_stepper.hpp:92-190). Device-resident
+ * node state (u, v, a, predictor, external force, bc values); one step = predictor -> RHS
+ * (+ beta_R * K * d when beta_R != 0) -> Dirichlet clamp -> PCG -> corrector -> adaptive dt.
+ * ------------------------------------------------------------------------------------- */
+
+/* AdaptivePolicy (newmark_stepper.hpp:58-63) + config::SolverSettings / TimeSettings */
+typedef struct cwf_stepper_desc
+{
+    double rayleigh_alpha, rayleigh_beta; /* RayleighCoefficients */
+    double runtime_tolerance, pause_tolerance;
+    uint64_t max_iterations;
+    double initial_dt;
+    int32_t adaptive;
+    int32_t warm_start; /* Stepper::warm_start_enabled_ default true */
+    double min_dt, max_dt;
+    double low_iteration_ratio, increase_factor, decrease_factor; /* 0.3, 1.1, 0.5 */
+    const float *external_force; /* [3N] interleaved dof = 3n+k (NodeBuffers::external_force) */
+    const float *bc_value;       /* [3N] (NodeBuffers::bc_value) */
+} cwf_stepper_desc;
+
+/* StepTelemetry (newmark_stepper.hpp:68-79) */
+typedef struct cwf_step_telemetry
+{
+    double simulation_time, time_step, applied_tolerance;
+    int32_t paused_mode, dt_increased, dt_decreased, dt_clamped_min, dt_clamped_max, reserved;
+    cwf_pcg_telemetry pcg;
+} cwf_step_telemetry;
+
+typedef struct cwf_hip_stepper cwf_hip_stepper;
+
+int cwf_hip_stepper_create(cwf_hip_system *system, const cwf_stepper_desc *desc, cwf_hip_stepper **out);
+void cwf_hip_stepper_destroy(cwf_hip_stepper *st);
+/* Stepper::step(simulation_time_seconds, paused_mode) */
+int cwf_hip_stepper_step(cwf_hip_stepper *st, double simulation_time, int paused, cwf_step_telemetry *tel);
+/* which: 0 = displacement, 1 = velocity, 2 = acceleration; out [3N] */
+int cwf_hip_stepper_get_state(cwf_hip_stepper *st, int which, float *out, uint64_t n, int ptr_kind);
+int cwf_hip_stepper_set_state(cwf_hip_stepper *st, int which, const float *in, uint64_t n, int ptr_kind);
+/* rewrite nodes.external_force between steps (viewer.cpp:262-266) */
+int cwf_hip_stepper_set_external_force(cwf_hip_stepper *st, const float *f, uint64_t n, int ptr_kind);
+int cwf_hip_stepper_set_warm_start(cwf_hip_stepper *st, int enabled);
+int cwf_hip_stepper_time(const cwf_hip_stepper *st, double *current_time, double *time_step);
+
+/* ---------------------------------------------------------------------------------------
+ * Host-side preprocessing (no GPU needed): tet gradients/volume/lumped mass/CSR exactly as
+ * mesh::pre::run + pack::build_packed_buffers (preprocess.cpp:268-405, pack.cpp:41-200).
+ * Outputs are caller-allocated: grads[E*24], volume[E], mass[N] (f64) and mass32[N],
+ * offsets[N+1], adj_elem[4E], adj_local[4E], conn8[8E].
+ * ------------------------------------------------------------------------------------- */
+int cwf_preprocess_tets(uint64_t node_count, uint64_t element_count, const double *coords, const uint32_t *tets,
+                        const uint32_t *material_index, const double *density, uint64_t material_count,
+                        float *grads24, float *volume, double *mass64, float *mass32, uint32_t *offsets,
+                        uint32_t *adj_elem, uint8_t *adj_local, uint32_t *conn8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CWF_HIP_H */

@@ -1,0 +1,39 @@
+"""Shared test helpers: build oracle systems from the product's packed buffers."""
+import hashlib
+
+import numpy as np
+
+import oracle as O
+from cwf import meshgen, pack, scenarios
+from cwf.physics import make_coefficients, compute_rayleigh, effective_scalars
+
+
+def oracle_system(P, materials, sK, sM, reduction_block=256):
+    packed = O.Packed(P.node_count, P.element_count, P.connectivity, P.gradients, P.volume, P.material_index,
+                      P.lumped_mass64, P.lumped_mass, P.offsets, P.element_indices, P.local_indices)
+    stiff = np.concatenate([np.asarray(m.stiffness if hasattr(m, "stiffness") else m, np.float64).reshape(-1)
+                            for m in materials])
+    return O.System(packed, stiff, P.bc_mask, sK, sM, reduction_block)
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+
+
+def assert_bitwise(a, b, what=""):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    diff = np.nonzero(bits(a) != bits(b))[0]
+    assert diff.size == 0, f"{what}: {diff.size} words differ, first at {diff[:5]}: {a[diff[:5]]} vs {b[diff[:5]]}"
+
+
+def kuhn16_reference_case():
+    """The survey's reference driver setup: n=16 Kuhn block, h=1, x=0 face
+    fixed, -500 N z point load at node (n,n,n), no gravity, dt=0.01, xi=0.02, w=5..50."""
+    case = scenarios.block_case(16, 16, 16, h=1.0, gravity=(0.0, 0.0, 0.0), point_group="CORNER")
+    ez = case.packing.external_force.reshape(-1, 3)[:, 2]
+    D = case.packing.dof_count
+    i = np.arange(D)
+    rhs = (ez[i // 3] * (i % 3 == 2).astype(np.float32)).astype(np.float32)  # float * bool (keeps -0.0)
+    return case, rhs

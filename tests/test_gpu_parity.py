@@ -1,0 +1,227 @@
+"""Parity of the HIP path (libcwf_hip.so on cuda:0) with the pinned oracle and the committed
+golden fixtures. PARITY mode: bit-exact (integer/fp32 words compared as bits, fp64 telemetry
+compared with ==). FAST mode: tolerance stated per test."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from cwf import _lib, pack, pcg, physics, scenarios
+from cwf.stepper import Stepper
+from helpers import assert_bitwise, kuhn16_reference_case, oracle_system
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gpu_system(case, mode=_lib.MODE_PARITY, sK=None, sM=None):
+    s0, m0 = case.scalars()
+    return pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, s0 if sK is None else sK,
+                                             m0 if sM is None else sM, mode=mode)
+
+
+CASES = {
+    "c1_small": lambda: scenarios.block_case(8, 3, 4, h=0.1, tol=1e-6, max_iterations=600),
+    "jitter": lambda: scenarios.block_case(7, 6, 5, h=0.1, jitter=True, tol=1e-6, max_iterations=600),
+    "rayleigh": lambda: scenarios.block_case(6, 4, 3, h=0.1, xi=0.05, w=(10.0, 100.0), tol=1e-6,
+                                             max_iterations=600),
+}
+
+
+@pytest.fixture(scope="module", params=sorted(CASES))
+def case(request):
+    return CASES[request.param]()
+
+
+def test_device_fp64_div_sqrt_correctly_rounded(case):
+    # the PCG scalars (alpha = rho/denom, |r| = sqrt) must round like the host: check via a solve
+    s = gpu_system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(5, 1e-12), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, 5, 1e-12)["telemetry"]
+    assert (t.alpha_last, t.beta_last, t.residual_norm) == (ref.alpha_last, ref.beta_last, ref.residual_norm)
+
+
+def test_apply_keff_bitwise(case):
+    s = gpu_system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rng = np.random.Generator(np.random.PCG64(3))
+    x = rng.uniform(-1, 1, case.packing.dof_count).astype(np.float32)
+    y = np.zeros_like(x)
+    assert pcg.apply_keff(s, x, y).has_value()
+    assert_bitwise(y, o.apply_keff(x), "apply_keff")
+
+
+def test_apply_keff_input_size_mismatch_error(case):
+    s = gpu_system(case)
+    r = pcg.apply_keff(s, np.zeros(5, np.float32), np.zeros(5, np.float32))
+    assert not r.has_value() and r.error().message == "input/output span size mismatch"
+
+
+def test_block_jacobi_bitwise(case):
+    s = gpu_system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    inv = np.zeros(case.packing.node_count * 9, np.float32)
+    assert pcg.build_block_jacobi_inverse(s, None, inv).has_value()
+    assert_bitwise(inv, o.block_jacobi(), "block_jacobi")
+
+
+def test_dot_and_partials_bitwise(case):
+    s = gpu_system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rng = np.random.Generator(np.random.PCG64(5))
+    a = rng.standard_normal(case.packing.dof_count).astype(np.float32)
+    b = rng.standard_normal(case.packing.dof_count).astype(np.float32)
+    parts = np.zeros(case.packing.reduction_partials, np.float64)
+    r = pcg.dot(s, a, b, parts)
+    ref, ref_parts = o.dot(a, b)
+    assert r.value() == ref
+    assert_bitwise(parts, ref_parts, "partials")
+
+
+def test_solve_pcg_bitwise_with_history(case):
+    s = gpu_system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x, r = np.zeros_like(rhs), np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(600, 1e-6), pcg.PcgVectors(x, r)).value()
+    ref = o.solve_pcg(rhs, 600, 1e-6, history=True)
+    rt = ref["telemetry"]
+    assert (t.iterations, t.converged) == (rt.iterations, bool(rt.converged))
+    assert (t.residual_norm, t.rhs_norm, t.alpha_last, t.beta_last) == (rt.residual_norm, rt.rhs_norm,
+                                                                          rt.alpha_last, rt.beta_last)
+    assert_bitwise(x, ref["x"], "x")
+    assert_bitwise(r, ref["r"], "r")
+    h = pcg.residual_history(s)
+    assert np.array_equal(h, ref["history"])  # fp64 residual norms bit-comparable
+
+
+def test_solve_pcg_warm_start_bitwise(case):
+    s = gpu_system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x0 = (np.arange(rhs.size) % 7 * 1e-7).astype(np.float32)
+    x = x0.copy()
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(50, 1e-5, True), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, 50, 1e-5, warm_start=True, x=x0)
+    assert t.iterations == ref["telemetry"].iterations
+    assert_bitwise(x, ref["x"], "x warm")
+
+
+def test_stepper_three_steps_bitwise(case):
+    P = case.packing
+    st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time)
+    sK, sM = case.scalars()
+    o = oracle_system(P, case.materials, sK, sM)
+    r = case.rayleigh
+    ost = O.Stepper(o, P.external_force, P.bc_value, (r.alpha, r.beta), case.cfg.solver.runtime_tolerance,
+                    case.cfg.solver.pause_tolerance, case.cfg.solver.max_iterations, case.cfg.time.initial_dt)
+    for k in range(3):
+        t = st.step(k * 0.01).value()
+        rt = ost.step(k * 0.01)
+        assert t.pcg.iterations == rt.pcg.iterations and t.pcg.residual_norm == rt.pcg.residual_norm
+    for which, ref in ((Stepper.DISPLACEMENT, ost.u), (Stepper.VELOCITY, ost.v), (Stepper.ACCELERATION, ost.a)):
+        assert_bitwise(st.get_state(which), ref, f"state {which}")
+    assert st.current_time() == ost.current_time and st.time_step() == ost.time_step
+
+
+@pytest.mark.parametrize("name", ["single_tet", "kuhn4x3x2", "jitter6"])
+def test_golden_fixtures_bitwise(name):
+    g = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+    mesh = pack.Mesh(g["coords"], g["tets"], None, {"SOLID": 1}, {}, [])
+    sK, sM, ra, rb, dt, tol, ptol, maxit = g["scalars"]
+    pre = pack.preprocess(mesh, physics.Config(materials=[physics.Material("steel", 30e9, 0.2, 2500.0)],
+                                               assignments=[physics.Assignment("SOLID", "steel")]))
+    mats = [physics.make_properties(physics.Material("steel", 30e9, 0.2, 2500.0))]
+    N = mesh.node_count
+    s = pcg.MatrixFreeSystem(pre["conn8"], pre["grads"], pre["volume"], pre["material_index"], mats, pre["mass32"],
+                             g["bc_mask"], N, mesh.element_count, 3 * N, sK, sM)
+    y = np.zeros(3 * N, np.float32)
+    assert pcg.apply_keff(s, g["keff_in"], y).has_value()
+    assert_bitwise(y, g["keff_out"], "keff")
+    inv = np.zeros(9 * N, np.float32)
+    pcg.build_block_jacobi_inverse(s, None, inv).value()
+    assert_bitwise(inv, g["bj_inv"], "bj")
+    x, r = np.zeros(3 * N, np.float32), np.zeros(3 * N, np.float32)
+    t = pcg.solve_pcg(s, g["pcg_rhs"], pcg.PcgSettings(400, 1e-6),
+                      pcg.PcgVectors(x, r)).value()
+    assert t.iterations == int(g["pcg_tel"][0])
+    assert t.residual_norm == g["pcg_tel"][1]
+    assert_bitwise(x, g["pcg_x"], "pcg x")
+    assert np.array_equal(pcg.residual_history(s), g["pcg_hist"])
+
+
+def test_kuhn16_reference_solve_on_gpu():
+    """The survey's recorded reference run, reproduced on the GPU: 162 iterations,
+    |r| = 0.14640172515227148, FNV-1a(x) = f10c27935f2e7a58."""
+    case, rhs = kuhn16_reference_case()
+    s = gpu_system(case)
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(500, 3e-4), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    assert t.iterations == 162
+    assert t.residual_norm == 0.14640172515227148
+    assert O.fnv1a64_words(x) == "f10c27935f2e7a58"
+
+
+def test_stagnation_error_path_matches_reference_text():
+    case = scenarios.block_case(8, 8, 8, h=1.0, gravity=(0.0, 0.0, 0.0), point_group="CORNER")
+    ez = case.packing.external_force.reshape(-1, 3)[:, 2]
+    i = np.arange(case.packing.dof_count)
+    rhs = (ez[i // 3] * (i % 3 == 2).astype(np.float32)).astype(np.float32)
+    s = gpu_system(case)
+    x = np.zeros_like(rhs)
+    r = pcg.solve_pcg(s, rhs, pcg.PcgSettings(500, 1e-8), pcg.PcgVectors(x, np.zeros_like(rhs)))
+    assert not r.has_value()
+    assert r.error().message == "CG denominator approached zero"
+    assert r.error().context == ["iteration=133"]
+
+
+def test_max_iterations_zero_error():
+    case = CASES["c1_small"]()
+    s = gpu_system(case)
+    rhs = case.static_rhs()
+    r = pcg.solve_pcg(s, rhs, pcg.PcgSettings(0, 1e-6), pcg.PcgVectors(np.zeros_like(rhs), None))
+    assert r.error().message == "max_iterations must be >= 1" and r.error().context == ["max_iterations=0"]
+
+
+def test_pause_mode_and_adaptive_dt():
+    # tests/newmark_stepper_test.cpp:241-269
+    case = scenarios.block_case(3, 2, 2, h=0.1, tol=3e-4, max_iterations=64)
+    st = Stepper(case.packing, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time)
+    t = st.step(0.0, True).value()
+    assert t.paused_mode and abs(t.applied_tolerance - case.cfg.solver.pause_tolerance) < 1e-12
+    ts = physics.TimeSettings(0.01, True, 0.0, 0.02)
+    from cwf.stepper import AdaptivePolicy
+
+    st2 = Stepper(case.packing, case.materials, case.rayleigh, case.cfg.solver, ts, AdaptivePolicy(1.0, 2.0, 0.5))
+    t2 = st2.step(0.0).value()
+    assert t2.dt_increased and t2.dt_clamped_max and abs(st2.time_step() - 0.02) < 1e-12
+
+
+# ---------------------------------------------------------------- fast mode (tolerance) ----
+def test_fast_mode_apply_keff_close(case):
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rng = np.random.Generator(np.random.PCG64(3))
+    x = rng.uniform(-1, 1, case.packing.dof_count).astype(np.float32)
+    y = np.zeros_like(x)
+    pcg.apply_keff(s, x, y).value()
+    ref = o.apply_keff(x).astype(np.float64)
+    # fp32 element math vs fp64: relative to the operator scale (max |row|)
+    assert np.max(np.abs(y - ref)) <= 2e-5 * np.max(np.abs(ref))
+
+
+def test_fast_mode_solve_close(case):
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(600, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, 600, 1e-6)
+    assert t.converged
+    # tolerance: the solve itself only guarantees |r| <= 1e-6 |rhs|; solutions agree to 1e-4 relative
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
