@@ -186,10 +186,12 @@ int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set
         {
             hipEvent_t e0 = h->timing ? h->ev[2 * i] : nullptr, e1 = h->timing ? h->ev[2 * i + 1] : nullptr;
             if (fast)
-                fast_pcg_iteration(h, rhs_dev, st, e0, e1);
+                fast_pcg_iteration(h, rhs_dev, (unsigned)(enq + i), st, e0, e1);
             else
                 parity_pcg_iteration(h, rhs_dev, st, e0, e1);
         }
+        if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
+            fast_check_pcg(h, (unsigned)(enq + nb), st);
         HIPTRY(h, hipGetLastError());
         prev_enq = enq;
         prev_nb = nb;
@@ -423,6 +425,64 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         s.off = doff;
         s.inc = dinc;
     }
+    // FAST-mode element tiles (tiles.cpp)
+    if (E)
+    {
+        HostTiles ht;
+        try
+        {
+            build_tiles(d, ht);
+        }
+        catch (const std::bad_alloc &)
+        {
+            return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
+        }
+        DevTiles &t = s.t;
+        uint4 *planes;
+        if (int st = dalloc(h, &planes, 3 * E))
+            return bail(st);
+        for (int q = 0; q < 3; ++q)
+            HIPTRY(h, hipMemcpy(planes + q * E, ht.planes[q].data(), E * sizeof(uint4), hipMemcpyHostToDevice));
+        if (!ht.mat.empty())
+        {
+            uint32_t *tm;
+            if (int st = upload(h, &tm, ht.mat.data(), E))
+                return bail(st);
+            t.mat = tm;
+        }
+        uint32_t *teo, *tno, *tn, *co, *npo, *nps;
+        uint16_t *ce;
+        float *part;
+        if (int st = upload(h, &teo, ht.tile_elem_off.data(), ht.tile_elem_off.size()))
+            return bail(st);
+        if (int st = upload(h, &tno, ht.tile_node_off.data(), ht.tile_node_off.size()))
+            return bail(st);
+        if (int st = upload(h, &tn, ht.tile_nodes.data(), ht.tile_nodes.size()))
+            return bail(st);
+        if (int st = upload(h, &co, ht.csr_off.data(), ht.csr_off.size()))
+            return bail(st);
+        if (int st = upload(h, &ce, ht.csr_ent.data(), ht.csr_ent.size()))
+            return bail(st);
+        if (int st = upload(h, &npo, ht.node_part_off.data(), ht.node_part_off.size()))
+            return bail(st);
+        if (int st = upload(h, &nps, ht.node_part_slot.data(), ht.node_part_slot.size()))
+            return bail(st);
+        if (int st = dalloc(h, &part, 3 * ht.tile_nodes.size()))
+            return bail(st);
+        t.ntiles = ht.ntiles;
+        t.max_tile_nodes = ht.max_tile_nodes;
+        t.total_tile_nodes = (uint32_t)ht.tile_nodes.size();
+        t.E = (uint32_t)E;
+        t.planes = planes;
+        t.tile_elem_off = teo;
+        t.tile_node_off = tno;
+        t.tile_nodes = tn;
+        t.csr_off = co;
+        t.csr_ent = ce;
+        t.node_part_off = npo;
+        t.node_part_slot = nps;
+        t.part = part;
+    }
     // solver scratch
     const uint64_t D = 3 * N;
     for (float **v : {&h->x, &h->r, &h->p, &h->z, &h->Ap, &h->rhs, &h->tmp})
@@ -431,10 +491,13 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     if (int st = dalloc(h, &h->inv, 9 * N))
         return bail(st);
     const uint64_t chunks = (D + d->reduction_block - 1) / d->reduction_block;
-    h->part_cap = std::max<uint64_t>({chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), 1});
+    h->part_cap = std::max<uint64_t>(
+        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), (uint64_t)s.t.ntiles, 1});
     if (int st = dalloc(h, &h->part0, h->part_cap))
         return bail(st);
     if (int st = dalloc(h, &h->part1, h->part_cap))
+        return bail(st);
+    if (int st = dalloc(h, &h->part2, h->part_cap))
         return bail(st);
     if (int st = dalloc(h, &h->ctl, 1))
         return bail(st);

@@ -21,6 +21,41 @@
 namespace cwf
 {
 
+// FAST-mode element tiles (tiles.cpp): element-centric K_eff with deterministic LDS folds
+constexpr int kTileElems = 512;      // elements per tile (= per 256-thread workgroup)
+constexpr int kMaxTileNodes = 2048;  // distinct nodes per tile (u16 local corner ids, LDS bound)
+
+struct DevTiles
+{
+    uint32_t ntiles = 0;
+    uint32_t max_tile_nodes = 0;
+    uint32_t total_tile_nodes = 0;
+    uint32_t E = 0;
+    // [3][E] 48-B records: {idx01, idx23, g0x, g0y} {g0z, g1x, g1y, g1z} {g2x, g2y, g2z, vol};
+    // g3 = -(g0 + g1 + g2) (partition of unity of the linear tet)
+    const uint4 *planes = nullptr;
+    const uint32_t *mat = nullptr;            // [E] material per element (tile order), NULL when M == 1
+    const uint32_t *tile_elem_off = nullptr;  // [ntiles+1]
+    const uint32_t *tile_node_off = nullptr;  // [ntiles+1]
+    const uint32_t *tile_nodes = nullptr;     // [total] global node ids; bit 31 = owner slot of the node
+    const uint32_t *csr_off = nullptr;        // [total+1]
+    const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
+    const uint32_t *node_part_off = nullptr;  // [N+1]
+    const uint32_t *node_part_slot = nullptr; // [total]
+    float *part = nullptr;                    // [3*total] tile-node partial sums (scratch)
+};
+
+struct HostTiles
+{
+    uint32_t ntiles = 0, max_tile_nodes = 0;
+    std::vector<uint4> planes[3];
+    std::vector<uint32_t> mat;
+    std::vector<uint32_t> tile_elem_off, tile_node_off, tile_nodes, csr_off, node_part_off, node_part_slot;
+    std::vector<uint16_t> csr_ent;
+};
+
+int build_tiles(const cwf_system_desc *d, HostTiles &out);
+
 struct DevSys
 {
     uint32_t N = 0;  // nodes
@@ -38,6 +73,7 @@ struct DevSys
     double sK = 1.0;  // stiffness_scale
     double sM = 0.0;  // mass_factor
     int iso = 0;      // every material has the isotropic Voigt zero pattern
+    DevTiles t{};     // FAST-mode tiles (empty in a PARITY-only handle)
 };
 
 // Device-resident PCG control block: scalars of pcg.cpp:696-918 live here so that the
@@ -50,6 +86,7 @@ struct Ctl
     int converged;
     int error;       // cwf_status (0 = none)
     int error_iter;  // iteration index for the error context
+    double rho2[2];  // FAST: rho by iteration parity (written by one kernel, read by the next)
 };
 
 struct DevBuf
@@ -74,7 +111,7 @@ struct cwf_hip_system
     // solver scratch (f32 dofs) and partials
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
     float *inv = nullptr;  // block Jacobi [9N]
-    double *part0 = nullptr, *part1 = nullptr;  // chunk / block partials
+    double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
     uint64_t part_cap = 0;
     cwf::Ctl *ctl = nullptr;       // device
     cwf::Ctl *ctl_host = nullptr;  // pinned
@@ -121,7 +158,12 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
 void fast_dot(const float *a, const float *b, const float *c, uint32_t D, double *pab, double *pac, hipStream_t st);
 void fast_fold(const double *part, uint32_t count, double *out, hipStream_t st);
 void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
-void fast_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, hipEvent_t e0 = nullptr,
+void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
+void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st);
+void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
+unsigned fast_tile_blocks(const DevSys &s);
+unsigned fast_update_blocks(const DevSys &s);
+void fast_pcg_iteration(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr);
 
 // ---- stepper.hip ----

@@ -1,0 +1,182 @@
+// tiles.cpp -- host-side build of the FAST-mode element tiles.
+//
+// The fast K_eff is element-centric: one workgroup per tile of <= kTileElems consecutive
+// elements (Morton order of the element centroids when node coordinates are given, so a tile is
+// a compact 3-D block). Per tile the host precomputes
+//   * the tile's distinct nodes (sorted global ids) -> the workgroup gathers their p into LDS,
+//   * every element's 4 corners as u16 indices into that node list,
+//   * a local CSR  tile-node -> (element_local * 4 + corner), ascending element, so the LDS fold of
+//     the element forces into tile-node partial sums is deterministic (no atomics),
+//   * the node -> (tile, slot) list, ascending tile, used by the finalize pass that adds a node's
+//     2..8 tile partials in a fixed order.
+// Element records are stored as 4 SoA planes of uint4 so every dwordx4 load of a wave is one
+// contiguous 1 KiB run:  plane0 = {idx01, idx23, vol_bits, material}, planes1..3 = the 12 gradients.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "cwf_internal.hpp"
+
+namespace cwf
+{
+namespace
+{
+inline uint64_t spread21(uint64_t v)
+{
+    v &= 0x1fffff;
+    v = (v | v << 32) & 0x1f00000000ffffull;
+    v = (v | v << 16) & 0x1f0000ff0000ffull;
+    v = (v | v << 8) & 0x100f00f00f00f00full;
+    v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+    v = (v | v << 2) & 0x1249249249249249ull;
+    return v;
+}
+}  // namespace
+
+int build_tiles(const cwf_system_desc *d, HostTiles &out)
+{
+    const uint64_t N = d->node_count, E = d->element_count;
+    std::vector<uint32_t> order(E);
+    std::iota(order.begin(), order.end(), 0u);
+    if (d->node_coords && E)
+    {
+        double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+        for (uint64_t n = 0; n < N; ++n)
+            for (int k = 0; k < 3; ++k)
+            {
+                lo[k] = std::min(lo[k], d->node_coords[3 * n + k]);
+                hi[k] = std::max(hi[k], d->node_coords[3 * n + k]);
+            }
+        double ext = 0.0;
+        for (int k = 0; k < 3; ++k)
+            ext = std::max(ext, hi[k] - lo[k]);
+        const double scale = ext > 0 ? (double)((1u << 21) - 1) / ext : 0.0;
+        std::vector<uint64_t> key(E);
+        for (uint64_t e = 0; e < E; ++e)
+        {
+            double c[3] = {0, 0, 0};
+            for (int a = 0; a < 4; ++a)
+                for (int k = 0; k < 3; ++k)
+                    c[k] += d->node_coords[3 * (uint64_t)d->element_connectivity[e * 8 + a] + k];
+            uint64_t q[3];
+            for (int k = 0; k < 3; ++k)
+                q[k] = (uint64_t)std::llround((c[k] * 0.25 - lo[k]) * scale);
+            key[e] = spread21(q[0]) | spread21(q[1]) << 1 | spread21(q[2]) << 2;
+        }
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    }
+
+    out = HostTiles{};
+    out.tile_elem_off.push_back(0);
+    out.tile_node_off.push_back(0);
+    out.csr_off.push_back(0);
+    for (int q = 0; q < 3; ++q)
+        out.planes[q].resize(E);
+    if (d->material_count > 1)
+        out.mat.resize(E);
+    out.csr_ent.reserve(E * 4);
+    std::vector<uint32_t> stamp(N, 0xFFFFFFFFu), local(N, 0);
+    std::vector<uint32_t> nodes;
+    std::vector<uint32_t> cnt;
+    uint64_t e = 0;
+    uint32_t tile = 0;
+    while (e < E)
+    {
+        // greedy: up to kTileElems elements while the tile's node list fits kMaxTileNodes
+        nodes.clear();
+        const uint64_t e0 = e;
+        while (e < E && e - e0 < (uint64_t)kTileElems)
+        {
+            const uint32_t src = order[e];
+            uint32_t add = 0;
+            for (int a = 0; a < 4; ++a)
+                add += stamp[d->element_connectivity[(uint64_t)src * 8 + a]] != tile ? 1u : 0u;
+            if (nodes.size() + add > (size_t)kMaxTileNodes)
+                break;
+            for (int a = 0; a < 4; ++a)
+            {
+                const uint32_t g = d->element_connectivity[(uint64_t)src * 8 + a];
+                if (stamp[g] != tile)
+                {
+                    stamp[g] = tile;
+                    nodes.push_back(g);
+                }
+            }
+            ++e;
+        }
+        std::sort(nodes.begin(), nodes.end());
+        for (uint32_t i = 0; i < nodes.size(); ++i)
+            local[nodes[i]] = i;
+        const uint32_t ne = (uint32_t)(e - e0), nn = (uint32_t)nodes.size();
+        // element records + local CSR
+        cnt.assign(nn + 1, 0);
+        for (uint32_t j = 0; j < ne; ++j)
+        {
+            const uint32_t src = order[e0 + j];
+            uint32_t li[4];
+            for (int a = 0; a < 4; ++a)
+            {
+                li[a] = local[d->element_connectivity[(uint64_t)src * 8 + a]];
+                ++cnt[li[a] + 1];
+            }
+            const float *g = d->element_gradients + (uint64_t)src * 24;
+            uint4 q0, q1, q2;
+            q0.x = li[0] | (li[1] << 16);
+            q0.y = li[2] | (li[3] << 16);
+            std::memcpy(&q0.z, g + 0, 8);   // g0x g0y
+            std::memcpy(&q1, g + 2, 16);    // g0z g1x g1y g1z
+            std::memcpy(&q2, g + 6, 12);    // g2x g2y g2z
+            std::memcpy(&q2.w, &d->element_volume[src], 4);
+            out.planes[0][e0 + j] = q0;
+            out.planes[1][e0 + j] = q1;
+            out.planes[2][e0 + j] = q2;
+            if (!out.mat.empty())
+                out.mat[e0 + j] = d->element_material_index[src];
+        }
+        for (uint32_t i = 0; i < nn; ++i)
+            cnt[i + 1] += cnt[i];
+        const uint64_t base = out.csr_ent.size();
+        out.csr_ent.resize(base + 4ull * ne);
+        std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
+        for (uint32_t j = 0; j < ne; ++j)
+        {
+            const uint32_t src = order[e0 + j];
+            for (int a = 0; a < 4; ++a)
+            {
+                const uint32_t l = local[d->element_connectivity[(uint64_t)src * 8 + a]];
+                out.csr_ent[base + cur[l]++] = (uint16_t)(j * 4 + a);
+            }
+        }
+        for (uint32_t i = 0; i < nn; ++i)
+        {
+            out.tile_nodes.push_back(nodes[i]);
+            out.csr_off.push_back((uint32_t)(base + cnt[i + 1]));
+        }
+        out.max_tile_nodes = std::max(out.max_tile_nodes, nn);
+        out.tile_elem_off.push_back((uint32_t)e);
+        out.tile_node_off.push_back((uint32_t)out.tile_nodes.size());
+        ++tile;
+    }
+    out.ntiles = tile;
+    // node -> slots (ascending tile)
+    const uint64_t total = out.tile_nodes.size();
+    out.node_part_off.assign(N + 1, 0);
+    for (uint64_t s = 0; s < total; ++s)
+        ++out.node_part_off[out.tile_nodes[s] + 1];
+    for (uint64_t n = 0; n < N; ++n)
+        out.node_part_off[n + 1] += out.node_part_off[n];
+    out.node_part_slot.resize(total);
+    std::vector<uint32_t> cur(out.node_part_off.begin(), out.node_part_off.end() - 1);
+    for (uint64_t s = 0; s < total; ++s)
+        out.node_part_slot[cur[out.tile_nodes[s]]++] = (uint32_t)s;
+    // owner slot = the node's first (lowest-tile) slot: bit 31 of tile_nodes
+    for (uint64_t n = 0; n < N; ++n)
+        if (out.node_part_off[n + 1] > out.node_part_off[n])
+            out.tile_nodes[out.node_part_slot[out.node_part_off[n]]] |= 0x80000000u;
+    return 0;
+}
+
+}  // namespace cwf

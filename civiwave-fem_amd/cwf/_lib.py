@@ -34,7 +34,7 @@ class SystemDesc(C.Structure):
         ("lumped_mass", C.c_void_p), ("bc_mask", C.c_void_p), ("adjacency_offsets", C.c_void_p),
         ("adjacency_elements", C.c_void_p), ("adjacency_local", C.c_void_p), ("stiffness_scale", C.c_double),
         ("mass_factor", C.c_double), ("reduction_block", C.c_uint64), ("reduction_partials", C.c_uint64),
-        ("mode", C.c_int32), ("reserved", C.c_int32),
+        ("mode", C.c_int32), ("reserved", C.c_int32), ("node_coords", C.c_void_p),
     ]
 
 

@@ -92,7 +92,10 @@ class MatrixFreeSystem:
     def __init__(self, element_connectivity, element_gradients, element_volume, element_material_index, materials,
                  lumped_mass, bc_mask, node_count, element_count, dof_count, stiffness_scale=1.0, mass_factor=0.0,
                  reduction_block=256, reduction_partials=None, adjacency=None, mode: int = _lib.MODE_PARITY,
-                 device: int = 0):
+                 device: int = 0, node_coords=None):
+        # node_coords (optional, [N,3]) only orders the FAST-mode element tiles (Morton order)
+        self.node_coords = (None if node_coords is None else
+                            np.ascontiguousarray(np.asarray(node_coords, np.float64).reshape(-1)))
         self.element_connectivity = np.ascontiguousarray(element_connectivity, np.uint32)
         self.element_gradients = np.ascontiguousarray(element_gradients, np.float32)
         self.element_volume = np.ascontiguousarray(element_volume, np.float32)
@@ -119,7 +122,7 @@ class MatrixFreeSystem:
                    packing.lumped_mass, packing.bc_mask, packing.node_count, packing.element_count,
                    packing.dof_count, stiffness_scale, mass_factor, packing.reduction_block,
                    packing.reduction_partials, (packing.offsets, packing.element_indices, packing.local_indices),
-                   mode, device)
+                   mode, device, packing.position0)
 
     # -- handle management --------------------------------------------------------------
     def handle(self):
@@ -138,7 +141,8 @@ class MatrixFreeSystem:
                 p(adj[0]) if adj is not None else None,
                 p(adj[1]) if adj is not None else None,
                 p(adj[2]) if adj is not None else None,
-                self.stiffness_scale, self.mass_factor, self.reduction_block, self.reduction_partials, self.mode, 0)
+                self.stiffness_scale, self.mass_factor, self.reduction_block, self.reduction_partials, self.mode, 0,
+                p(self.node_coords) if self.node_coords is not None else None)
             h = C.c_void_p()
             st = L.cwf_hip_system_create(C.byref(desc), self.device, C.byref(h))
             if st:

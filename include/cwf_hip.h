@@ -86,6 +86,7 @@ typedef struct cwf_system_desc
     uint64_t reduction_partials;        /* >= ceil(dof_count / reduction_block) */
     int32_t mode;                       /* cwf_mode */
     int32_t reserved;
+    const double *node_coords;          /* [node_count * 3] or NULL: only used to order FAST-mode tiles */
 } cwf_system_desc;
 
 /* PcgSettings (pcg.hpp:115-120) */

@@ -1,0 +1,381 @@
+// cwf_hip.hpp -- C++20 host mirror of CiviWave's L4 solver-core interface over the C-ABI.
+//
+// Same names, argument meaning and error behaviour as the reference headers:
+//   cwf::hip::pcg::{MatrixFreeSystem, MatrixFreeWorkspace, PcgVectors, PcgSettings, PcgTelemetry,
+//                   PcgError, apply_keff, solve_pcg, build_block_jacobi_inverse}
+//       <- include/cwf/gpu/pcg.hpp:47-227
+//   cwf::hip::newmark::{Stepper, StepTelemetry, StepError, AdaptivePolicy}
+//       <- include/cwf/gpu/newmark_stepper.hpp:49-190
+// Results are cwf::hip::expected<T, E> (std::expected is C++23; this header targets C++20 so it
+// builds with the image's g++ 11). Header-only; link libcwf_hip.so.
+//
+// Device state: the first call with a workspace uploads the system's spans to HBM and keeps the
+// handle in the workspace (the reference reuses one workspace per system, pcg.hpp:91-97), so
+// a workspace must not be shared between different meshes. stiffness_scale / mass_factor are
+// pushed on every call.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <span>
+#include <string>
+#include <utility>
+#include <variant>
+#include <vector>
+
+#include "cwf_hip.h"
+
+namespace cwf::hip
+{
+
+template <class E> struct unexpected
+{
+    E error;
+};
+
+template <class T, class E> class expected
+{
+public:
+    expected(T v) : v_(std::in_place_index<0>, std::move(v)) {}
+    expected(unexpected<E> u) : v_(std::in_place_index<1>, std::move(u.error)) {}
+    bool has_value() const noexcept { return v_.index() == 0; }
+    explicit operator bool() const noexcept { return has_value(); }
+    T &value() { return std::get<0>(v_); }
+    const T &value() const { return std::get<0>(v_); }
+    T &operator*() { return value(); }
+    T *operator->() { return &value(); }
+    const E &error() const { return std::get<1>(v_); }
+
+private:
+    std::variant<T, E> v_;
+};
+
+template <class E> class expected<void, E>
+{
+public:
+    expected() = default;
+    expected(unexpected<E> u) : err_(std::move(u.error)), ok_(false) {}
+    bool has_value() const noexcept { return ok_; }
+    explicit operator bool() const noexcept { return ok_; }
+    const E &error() const { return err_; }
+
+private:
+    E err_{};
+    bool ok_ = true;
+};
+
+namespace pcg
+{
+
+struct PcgError
+{
+    std::string message;
+    std::vector<std::string> context;
+};
+
+// materials[m] = ElasticProperties::stiffness (6x6 Voigt, row-major)
+struct MatrixFreeSystem
+{
+    std::span<const std::uint32_t> element_connectivity;
+    std::span<const float> element_gradients;
+    std::span<const float> element_volume;
+    std::span<const std::uint32_t> element_material_index;
+    std::span<const std::array<double, 36>> materials;
+    std::span<const float> lumped_mass;
+    std::span<const std::uint32_t> bc_mask;
+    std::size_t node_count{};
+    std::size_t element_count{};
+    std::size_t dof_count{};
+    double stiffness_scale{};
+    double mass_factor{};
+    std::size_t reduction_block{};
+    std::size_t reduction_partials{};
+    int mode = CWF_MODE_PARITY;  // build extension: PARITY (bit-exact) or FAST
+    int device = 0;              // build extension: HIP device ordinal
+};
+
+struct MatrixFreeWorkspace
+{
+    cwf_hip_system *handle = nullptr;
+    MatrixFreeWorkspace() = default;
+    MatrixFreeWorkspace(const MatrixFreeWorkspace &) = delete;
+    MatrixFreeWorkspace &operator=(const MatrixFreeWorkspace &) = delete;
+    MatrixFreeWorkspace(MatrixFreeWorkspace &&o) noexcept : handle(std::exchange(o.handle, nullptr)) {}
+    ~MatrixFreeWorkspace() { cwf_hip_system_destroy(handle); }
+};
+
+struct PcgVectors
+{
+    std::span<float> solution;
+    std::span<float> residual;
+    std::span<float> search_direction;  // scratch lives in HBM; kept for signature parity
+    std::span<float> preconditioned;
+    std::span<float> matvec;
+    std::span<double> partials;
+};
+
+struct PcgSettings
+{
+    std::size_t max_iterations{128U};
+    double relative_tolerance{3.0e-4};
+    bool warm_start{false};
+};
+
+struct PcgTelemetry
+{
+    std::size_t iterations{};
+    double residual_norm{};
+    double rhs_norm{};
+    double alpha_last{};
+    double beta_last{};
+    bool converged{};
+};
+
+namespace detail
+{
+inline PcgError last(const cwf_hip_system *h)
+{
+    PcgError e{cwf_hip_last_error(h), {}};
+    const std::string ctx = cwf_hip_last_context(h);
+    if (!ctx.empty())
+        e.context.push_back(ctx);
+    return e;
+}
+
+inline expected<cwf_hip_system *, PcgError> bind(const MatrixFreeSystem &s, MatrixFreeWorkspace &ws)
+{
+    if (!ws.handle)
+    {
+        std::vector<double> mats;
+        for (const auto &m : s.materials)
+            mats.insert(mats.end(), m.begin(), m.end());
+        cwf_system_desc d{};
+        d.node_count = s.node_count;
+        d.element_count = s.element_count;
+        d.dof_count = s.dof_count;
+        d.element_connectivity = s.element_connectivity.data();
+        d.element_gradients = s.element_gradients.data();
+        d.element_volume = s.element_volume.data();
+        d.element_material_index = s.element_material_index.data();
+        d.material_stiffness = mats.empty() ? nullptr : mats.data();
+        d.material_count = s.materials.size();
+        d.lumped_mass = s.lumped_mass.data();
+        d.bc_mask = s.bc_mask.data();
+        d.stiffness_scale = s.stiffness_scale;
+        d.mass_factor = s.mass_factor;
+        d.reduction_block = s.reduction_block;
+        d.reduction_partials = s.reduction_partials;
+        d.mode = s.mode;
+        if (s.element_connectivity.size() != s.element_count * 8U)
+            return unexpected<PcgError>{{"connectivity size mismatch",
+                                         {"expected=" + std::to_string(s.element_count * 8U),
+                                          "actual=" + std::to_string(s.element_connectivity.size())}}};
+        if (s.element_gradients.size() != s.element_count * 24U)
+            return unexpected<PcgError>{{"gradient table size mismatch",
+                                         {"expected=" + std::to_string(s.element_count * 24U),
+                                          "actual=" + std::to_string(s.element_gradients.size())}}};
+        if (s.element_volume.size() != s.element_count || s.element_material_index.size() != s.element_count ||
+            s.bc_mask.size() != s.node_count || s.lumped_mass.size() != s.node_count)
+            return unexpected<PcgError>{{"system table size mismatch", {}}};
+        if (cwf_hip_system_create(&d, s.device, &ws.handle) != 0)
+            return unexpected<PcgError>{last(nullptr)};
+    }
+    cwf_hip_system_set_scalars(ws.handle, s.stiffness_scale, s.mass_factor);
+    cwf_hip_system_set_mode(ws.handle, s.mode);
+    return ws.handle;
+}
+}  // namespace detail
+
+// pcg.hpp:161-163
+[[nodiscard]] inline auto apply_keff(const MatrixFreeSystem &system, std::span<const float> input,
+                                     std::span<float> output, MatrixFreeWorkspace &workspace)
+    -> expected<void, PcgError>
+{
+    if (input.size() != system.dof_count || output.size() != system.dof_count)
+        return unexpected<PcgError>{{"input/output span size mismatch",
+                                     {"input=" + std::to_string(input.size()),
+                                      "output=" + std::to_string(output.size()),
+                                      "dofs=" + std::to_string(system.dof_count)}}};
+    auto h = detail::bind(system, workspace);
+    if (!h)
+        return unexpected<PcgError>{h.error()};
+    if (cwf_hip_apply_keff(*h, input.data(), output.data(), input.size(), CWF_PTR_HOST) != 0)
+        return unexpected<PcgError>{detail::last(*h)};
+    return {};
+}
+
+// pcg.hpp:210-212
+[[nodiscard]] inline auto solve_pcg(const MatrixFreeSystem &system, std::span<const float> rhs,
+                                    const PcgSettings &settings, PcgVectors vectors, MatrixFreeWorkspace &workspace)
+    -> expected<PcgTelemetry, PcgError>
+{
+    if (rhs.size() != system.dof_count)
+        return unexpected<PcgError>{{"rhs span size mismatch", {"rhs=" + std::to_string(rhs.size()),
+                                                                 "dofs=" + std::to_string(system.dof_count)}}};
+    if (vectors.solution.size() != system.dof_count)
+        return unexpected<PcgError>{{"solver vector span size mismatch", {}}};
+    auto h = detail::bind(system, workspace);
+    if (!h)
+        return unexpected<PcgError>{h.error()};
+    cwf_pcg_settings cs{settings.max_iterations, settings.relative_tolerance, settings.warm_start ? 1 : 0, 0};
+    cwf_pcg_telemetry t{};
+    float *res = vectors.residual.size() == system.dof_count ? vectors.residual.data() : nullptr;
+    if (cwf_hip_solve_pcg(*h, rhs.data(), &cs, vectors.solution.data(), res, rhs.size(), CWF_PTR_HOST, &t) != 0)
+        return unexpected<PcgError>{detail::last(*h)};
+    return PcgTelemetry{t.iterations, t.residual_norm, t.rhs_norm, t.alpha_last, t.beta_last, t.converged != 0};
+}
+
+// pcg.hpp:226-227
+[[nodiscard]] inline auto build_block_jacobi_inverse(const MatrixFreeSystem &system, MatrixFreeWorkspace &workspace,
+                                                     std::span<float> out_inverse) -> expected<void, PcgError>
+{
+    const auto required = system.node_count * 9U;
+    if (out_inverse.size() < required)
+        return unexpected<PcgError>{{"block inverse span too small", {"required=" + std::to_string(required),
+                                                                      "available=" +
+                                                                          std::to_string(out_inverse.size())}}};
+    auto h = detail::bind(system, workspace);
+    if (!h)
+        return unexpected<PcgError>{h.error()};
+    if (cwf_hip_build_block_jacobi_inverse(*h, out_inverse.data(), out_inverse.size(), CWF_PTR_HOST) != 0)
+        return unexpected<PcgError>{detail::last(*h)};
+    return {};
+}
+
+}  // namespace pcg
+
+namespace newmark
+{
+
+struct StepError
+{
+    std::string message;
+    std::vector<std::string> context;
+};
+
+struct AdaptivePolicy
+{
+    double low_iteration_ratio{0.3};
+    double increase_factor{1.1};
+    double decrease_factor{0.5};
+};
+
+struct StepTelemetry
+{
+    double simulation_time{};
+    double time_step{};
+    double applied_tolerance{};
+    bool paused_mode{};
+    bool dt_increased{};
+    bool dt_decreased{};
+    bool dt_clamped_min{};
+    bool dt_clamped_max{};
+    pcg::PcgTelemetry pcg{};
+};
+
+struct SolverSettings  // config::SolverSettings subset (config.hpp:100-107)
+{
+    double runtime_tolerance{3.0e-4};
+    double pause_tolerance{1.0e-5};
+    std::uint32_t max_iterations{128};
+};
+
+struct TimeSettings  // config::TimeSettings (config.hpp:88-94)
+{
+    double initial_dt{0.01};
+    bool adaptive{false};
+    double min_dt{0.0};
+    double max_dt{0.0};
+};
+
+struct Rayleigh
+{
+    double alpha{};
+    double beta{};
+};
+
+// Stepper(packing, materials, rayleigh, solver_settings, time_settings, policy): the packing is
+// the MatrixFreeSystem spans plus the node external force / Dirichlet values (dof = 3n+k).
+class Stepper
+{
+public:
+    Stepper(const pcg::MatrixFreeSystem &system, std::span<const float> external_force,
+            std::span<const float> bc_value, Rayleigh rayleigh, const SolverSettings &solver,
+            const TimeSettings &time, AdaptivePolicy policy = {})
+    {
+        auto h = pcg::detail::bind(system, ws_);
+        if (!h)
+        {
+            init_error_ = StepError{h.error().message, h.error().context};
+            return;
+        }
+        cwf_stepper_desc d{};
+        d.rayleigh_alpha = rayleigh.alpha;
+        d.rayleigh_beta = rayleigh.beta;
+        d.runtime_tolerance = solver.runtime_tolerance;
+        d.pause_tolerance = solver.pause_tolerance;
+        d.max_iterations = solver.max_iterations;
+        d.initial_dt = time.initial_dt;
+        d.adaptive = time.adaptive ? 1 : 0;
+        d.warm_start = 1;
+        d.min_dt = time.min_dt;
+        d.max_dt = time.max_dt;
+        d.low_iteration_ratio = policy.low_iteration_ratio;
+        d.increase_factor = policy.increase_factor;
+        d.decrease_factor = policy.decrease_factor;
+        d.external_force = external_force.data();
+        d.bc_value = bc_value.data();
+        if (cwf_hip_stepper_create(*h, &d, &st_) != 0)
+            init_error_ = StepError{cwf_hip_last_error(*h), {cwf_hip_last_context(*h)}};
+        dofs_ = system.dof_count;
+    }
+    ~Stepper() { cwf_hip_stepper_destroy(st_); }
+    Stepper(const Stepper &) = delete;
+    Stepper &operator=(const Stepper &) = delete;
+
+    [[nodiscard]] auto step(double simulation_time_seconds, bool paused_mode = false)
+        -> expected<StepTelemetry, StepError>
+    {
+        if (!st_)
+            return unexpected<StepError>{init_error_};
+        cwf_step_telemetry t{};
+        if (cwf_hip_stepper_step(st_, simulation_time_seconds, paused_mode ? 1 : 0, &t) != 0)
+            return unexpected<StepError>{{cwf_hip_last_error(ws_.handle), {cwf_hip_last_context(ws_.handle)}}};
+        return StepTelemetry{t.simulation_time, t.time_step, t.applied_tolerance, t.paused_mode != 0,
+                             t.dt_increased != 0, t.dt_decreased != 0, t.dt_clamped_min != 0, t.dt_clamped_max != 0,
+                             pcg::PcgTelemetry{t.pcg.iterations, t.pcg.residual_norm, t.pcg.rhs_norm,
+                                               t.pcg.alpha_last, t.pcg.beta_last, t.pcg.converged != 0}};
+    }
+    [[nodiscard]] auto current_time() const noexcept -> double
+    {
+        double c = 0.0;
+        cwf_hip_stepper_time(st_, &c, nullptr);
+        return c;
+    }
+    [[nodiscard]] auto time_step() const noexcept -> double
+    {
+        double d = 0.0;
+        cwf_hip_stepper_time(st_, nullptr, &d);
+        return d;
+    }
+    void set_warm_start(bool enabled) noexcept { cwf_hip_stepper_set_warm_start(st_, enabled ? 1 : 0); }
+    // node state (0 displacement, 1 velocity, 2 acceleration), dof = 3n+k
+    bool state(int which, std::span<float> out) const
+    {
+        return cwf_hip_stepper_get_state(st_, which, out.data(), out.size(), CWF_PTR_HOST) == 0;
+    }
+    bool set_external_force(std::span<const float> f)
+    {
+        return cwf_hip_stepper_set_external_force(st_, f.data(), f.size(), CWF_PTR_HOST) == 0;
+    }
+    [[nodiscard]] auto dof_count() const noexcept -> std::size_t { return dofs_; }
+
+private:
+    pcg::MatrixFreeWorkspace ws_{};
+    cwf_hip_stepper *st_ = nullptr;
+    StepError init_error_{"stepper not initialised", {}};
+    std::size_t dofs_ = 0;
+};
+
+}  // namespace newmark
+}  // namespace cwf::hip

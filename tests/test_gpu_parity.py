@@ -225,3 +225,14 @@ def test_fast_mode_solve_close(case):
     # tolerance: the solve itself only guarantees |r| <= 1e-6 |rhs|; solutions agree to 1e-4 relative
     assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
     assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
+
+
+def test_cpp_mirror_single_tet_reference_outputs(tmp_path):
+    """tests/cpp/pcg_api_test.cpp: the reference's single-tet fixture through include/cwf_hip.hpp."""
+    import subprocess
+
+    from test_host import _build_cpp_test
+
+    exe = _build_cpp_test(tmp_path)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr

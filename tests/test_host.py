@@ -75,3 +75,21 @@ def test_kuhn_block_counts_match_survey_table():
     for key, (N, E) in {"c1": (1386, 6000), "c2": (343000, 1971054)}.items():
         sx, sy, sz = meshgen.CONFIGS[key]["shape"]
         assert (sx + 1) * (sy + 1) * (sz + 1) == N and 6 * sx * sy * sz == E
+
+
+def _build_cpp_test(tmp_path):
+    import subprocess
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.join(root, "civiwave-fem_amd", "lib")
+    exe = str(tmp_path / "pcg_api_test")
+    subprocess.run(["g++", "-std=c++20", "-O1", "-Wall", "-I/opt/rocm/include",
+                    os.path.join(root, "tests", "cpp", "pcg_api_test.cpp"), "-o", exe, f"-L{libdir}", "-lcwf_hip",
+                    f"-Wl,-rpath,{libdir}"], check=True)
+    return exe
+
+
+def test_cpp_mirror_header_compiles_and_links(tmp_path):
+    """include/cwf_hip.hpp (C++ mirror of cwf::gpu::pcg / Stepper) builds with the image's g++."""
+    assert _build_cpp_test(tmp_path)
