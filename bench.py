@@ -12,8 +12,11 @@ dominant kernel (K_eff, timed with hipEvents on the handle's stream inside the t
 bounded single-thread CPU baseline (the oracle restatement of the reference's solve_pcg).
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): weak scaling, one process per
-GPU, each rank owns one copy of the per-GPU workload ("replicas" until the partitioned solver
-lands).
+GPU. The global block stacks N copies of the per-GPU workload along z; rank r owns a contiguous range
+of node planes, builds only its slab sub-mesh (+ one ghost cell layer) and solves as one shard of the
+global system: RCCL all-gathers of the PCG scalars (p.Ap, r.r / r.z, 8-16 B per rank) and one halo of
+z per iteration over xGMI (csrc/comm.cpp). value = sum over ranks of owned DOFs x PCG iterations /
+max-over-ranks wall time.
 """
 from __future__ import annotations
 
@@ -74,10 +77,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo", init_method="env://")
+        dist.init_process_group("gloo", init_method="env://")  # bookkeeping only; the data path is RCCL
     import numpy as np
 
-    from cwf import _lib, pcg, scenarios
+    from cwf import _lib, pcg, scenarios, shard
     from cwf.stepper import Stepper
 
     def barrier():
@@ -85,11 +88,38 @@ def main():
             dist.barrier()
 
     device = local_rank if world > 1 else 0
-    case = scenarios.config_case(args.config, max_iterations=args.max_iterations)
-    P = case.packing
     mode = _lib.MODE_FAST if args.mode == "fast" else _lib.MODE_PARITY
-    sK, sM = case.scalars()
-    stepper = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode, device=device)
+    comm = None
+    if world == 1:
+        case = scenarios.config_case(args.config, max_iterations=args.max_iterations)
+        P = case.packing
+        sK, sM = case.scalars()
+        stepper = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode,
+                          device=device)
+        owned_dofs, local_nodes, local_tets = P.dof_count, P.node_count, P.element_count
+    else:
+        if mode != _lib.MODE_FAST:
+            raise SystemExit("multi-GPU runs the FAST path only")
+        case, node_global, begin = scenarios.slab_case(args.config, world, rank, max_iterations=args.max_iterations)
+        P = case.packing
+        sK, sM = case.scalars()
+        src = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=mode)  # host arrays only
+        sh = shard.build_shard(src, begin, rank, node_global)
+        system = sh.system(case.materials, 1.0, 0.0, device=device)
+        uid = [shard.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = shard.Comm.rccl(world, rank, uid[0], device)
+        comm.attach(system, sh)
+
+        class _LocalPacking:  # the Stepper's view of the shard: local node order, local vectors
+            external_force = sh.local_dofs(P.external_force)
+            bc_value = sh.local_dofs(P.bc_value)
+            dof_count = 3 * sh.local_nodes
+            node_count = sh.local_nodes
+
+        stepper = Stepper(_LocalPacking, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode,
+                          device=device, system=system)
+        owned_dofs, local_nodes, local_tets = 3 * sh.owned_nodes, sh.local_nodes, sh.local_elements
     L = _lib.load()
     h = stepper.system.handle()
     t_sim = 0.0
@@ -113,7 +143,7 @@ def main():
     keff_ms, keff_n = C.c_double(), C.c_uint64()
     L.cwf_hip_system_timing(h, C.byref(keff_ms), C.byref(keff_n))
     L.cwf_hip_system_set_timing(h, 0)
-    D = P.dof_count
+    D = owned_dofs
     local = np.array([elapsed, D * total_iters, total_iters, D], np.float64)
     if dist is not None:
         t = torch.from_numpy(local.copy())
@@ -126,7 +156,7 @@ def main():
         dof_iters, iters_sum, dofs_sum = local[1], local[2], local[3]
     avg_keff_ms = keff_ms.value / max(1, keff_n.value)
     # algorithmic bytes of one K_eff launch: 32 B/node + 72 B/tet (reference layout)
-    alg_bytes = 32.0 * P.node_count + 72.0 * P.element_count
+    alg_bytes = 32.0 * local_nodes + 72.0 * local_tets
     achieved = alg_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
     traffic = None
     if args.traffic and os.path.exists(args.traffic):
@@ -134,7 +164,7 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline(case, sK, sM, args.cpu_iterations)
         result = {
             "metric": "PCG DOF-iterations/sec per Newmark step (PCG-it/s x DOFs); DOF-updates/s and "
@@ -150,8 +180,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if args.mode == "fast" else "f64",
             "data": "synthetic (structured hex block -> Kuhn tets, gravity + tip load)",
-            "config": {"workload": case.name, "nodes": P.node_count, "tets": P.element_count, "dofs": D,
-                       "mode": args.mode, "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "config": {"workload": case.name, "nodes_per_gpu": local_nodes, "tets_per_gpu": local_tets,
+                       "dofs": int(dofs_sum), "mode": args.mode,
+                       "parallelism": f"node-range shards x{world} (RCCL halo + all-gather)" if world > 1
+                       else "single"},
             "pcg_iterations": int(iters_sum),
             "pcg_iterations_per_sec": iters_sum / world / elapsed,
             "dof_updates_per_sec": dofs_sum * args.steps / elapsed,
@@ -164,6 +196,8 @@ def main():
         print(json.dumps(result), flush=True)
     stepper.close()
     stepper.system.close()
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

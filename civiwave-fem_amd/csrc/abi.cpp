@@ -124,30 +124,45 @@ std::string pcg_error_message(int code, int iter, std::string *ctx)
     return "CG rho approached zero";  // pcg.cpp:889-892
 }
 
-// run solve_pcg on device buffers h->rhs (or rhs_dev) and h->x. x must already hold the warm start.
-int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
+// run solve_pcg on device buffers: rhs[i] and g[i]->x (holding the warm start) for every member of a
+// group -- one handle, or every rank of a sharded system driven from this process (LOCAL comm).
+int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
+                  const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
 {
+    cwf_hip_system *h = g[0];
     if (set.max_iterations == 0)
         return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
-    if (h->hist_cap < set.max_iterations + 1)
-    {
-        if (h->hist)
-            (void)hipFree(h->hist);
-        h->hist = nullptr;
-        const uint64_t cap = std::max<uint64_t>(set.max_iterations + 1, 1024);
-        if (hipMalloc(reinterpret_cast<void **>(&h->hist), cap * sizeof(double)) != hipSuccess)
-            return set_error(h, CWF_ERR_ALLOC, "failed to grow matrix-free workspace buffers",
-                             "history=" + std::to_string(cap));
-        h->hist_cap = cap;
-    }
+    const bool sharded = h->sharded();
+    if (sharded && h->mode != CWF_MODE_FAST)
+        return set_error(h, CWF_ERR_UNSUPPORTED, "sharded systems run in FAST mode only");
+    if (!sharded && g.size() != 1)
+        return set_error(h, CWF_ERR_ARGUMENT, "a group needs attached shards");
+    for (cwf_hip_system *m : g)
+        if (m->hist_cap < set.max_iterations + 1)
+        {
+            if (m->hist)
+                (void)hipFree(m->hist);
+            m->hist = nullptr;
+            const uint64_t cap = std::max<uint64_t>(set.max_iterations + 1, 1024);
+            if (hipMalloc(reinterpret_cast<void **>(&m->hist), cap * sizeof(double)) != hipSuccess)
+                return set_error(m, CWF_ERR_ALLOC, "failed to grow matrix-free workspace buffers",
+                                 "history=" + std::to_string(cap));
+            m->hist_cap = cap;
+        }
     hipStream_t st = h->stream;
     if (!set.warm_start)
-        HIPTRY(h, hipMemsetAsync(h->x, 0, h->ds.D * sizeof(float), st));
+        for (cwf_hip_system *m : g)
+            HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
-    if (fast)
-        fast_pcg_init(h, rhs_dev, set.relative_tolerance, st);
+    if (sharded)
+    {
+        if (int e = sharded_pcg_init(g, rhs, set.relative_tolerance))
+            return e;
+    }
+    else if (fast)
+        fast_pcg_init(h, rhs[0], set.relative_tolerance, st);
     else
-        parity_pcg_init(h, rhs_dev, set.relative_tolerance, st);
+        parity_pcg_init(h, rhs[0], set.relative_tolerance, st);
     HIPTRY(h, hipGetLastError());
     uint64_t enq = 0;
     constexpr uint64_t kMaxBatch = 64;
@@ -161,6 +176,7 @@ int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set
     uint64_t prev_enq = 0, prev_nb = 0;
     for (;;)
     {
+        // every member's control block is identical (rank-order folds); member 0's is polled
         HIPTRY(h, hipMemcpyAsync(h->ctl_host, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
         HIPTRY(h, hipStreamSynchronize(st));
         if (h->timing && prev_nb)
@@ -185,13 +201,19 @@ int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set
         for (uint64_t i = 0; i < nb; ++i)
         {
             hipEvent_t e0 = h->timing ? h->ev[2 * i] : nullptr, e1 = h->timing ? h->ev[2 * i + 1] : nullptr;
-            if (fast)
-                fast_pcg_iteration(h, rhs_dev, (unsigned)(enq + i), st, e0, e1);
+            if (sharded)
+            {
+                if (int e = sharded_pcg_iteration(g, rhs, (unsigned)(enq + i), e0, e1))
+                    return e;
+            }
+            else if (fast)
+                fast_pcg_iteration(h, rhs[0], (unsigned)(enq + i), st, e0, e1);
             else
-                parity_pcg_iteration(h, rhs_dev, st, e0, e1);
+                parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
         if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
-            fast_check_pcg(h, (unsigned)(enq + nb), st);
+            for (cwf_hip_system *m : g)
+                fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
         HIPTRY(h, hipGetLastError());
         prev_enq = enq;
         prev_nb = nb;
@@ -199,8 +221,16 @@ int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set
         if (set.check_interval <= 0)
             batch = std::min<uint64_t>(batch * 2, kMaxBatch);
     }
+    if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows
+    {
+        if (int e = comm_halo(g, &cwf_hip_system::x))
+            return e;
+        for (cwf_hip_system *m : g)
+            HIPTRY(m, hipStreamSynchronize(m->stream));
+    }
     const Ctl &c = *h->ctl_host;
-    h->hist_count = c.iterations + 1;
+    for (cwf_hip_system *m : g)
+        m->hist_count = c.iterations + 1;
     if (tel)
     {
         tel->iterations = c.iterations;
@@ -215,9 +245,18 @@ int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set
     {
         std::string ctx;
         std::string msg = pcg_error_message(c.error, c.error_iter, &ctx);
+        for (size_t i = 1; i < g.size(); ++i)
+            set_error(g[i], c.error, msg, ctx);
         return set_error(h, c.error, msg, ctx);
     }
     return 0;
+}
+
+int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
+{
+    if (h->comm && h->comm->kind == 0 && h->nranks > 1)
+        return set_error(h, CWF_ERR_UNSUPPORTED, "a LOCAL-communicator shard solves through cwf_hip_solve_pcg_group");
+    return run_pcg_group({h}, {rhs_dev}, set, tel);
 }
 
 }  // namespace
@@ -249,6 +288,11 @@ void cwf_hip_system_destroy(cwf_hip_system *h)
     (void)hipSetDevice(h->device);
     if (h->stream)
         (void)hipStreamSynchronize(h->stream);
+    if (h->comm && h->comm->kind == 0)  // give the LOCAL communicator's stream back
+    {
+        h->comm->members[h->rank] = nullptr;
+        h->stream = h->own_stream;
+    }
     for (void *p : h->owned)
         (void)hipFree(p);
     if (h->hist)
@@ -322,6 +366,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
 
     DevSys &s = h->ds;
     s.N = (uint32_t)N;
+    s.Nown = (uint32_t)N;
     s.E = (uint32_t)E;
     s.D = (uint32_t)(3 * N);
     s.M = (uint32_t)d->material_count;
@@ -450,22 +495,24 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 return bail(st);
             t.mat = tm;
         }
-        uint32_t *teo, *tno, *tn, *co, *npo, *nps;
+        // packed per-tile header and per-tile-node record: one dwordx4 load each
+        std::vector<uint4> hdr(ht.ntiles), tnode(ht.tile_nodes.size());
+        for (uint32_t k = 0; k < ht.ntiles; ++k)
+            hdr[k] = uint4{ht.tile_elem_off[k], ht.tile_elem_off[k + 1] - ht.tile_elem_off[k], ht.tile_node_off[k],
+                           ht.tile_node_off[k + 1] - ht.tile_node_off[k]};
+        for (size_t q = 0; q < tnode.size(); ++q)
+            tnode[q] = uint4{ht.tile_nodes[q], ht.tile_slot[q], ht.csr_off[q], ht.csr_off[q + 1]};
+        uint4 *dh, *dtn;
+        uint32_t *npo;
         uint16_t *ce;
         float *part;
-        if (int st = upload(h, &teo, ht.tile_elem_off.data(), ht.tile_elem_off.size()))
+        if (int st = upload(h, &dh, hdr.data(), hdr.size()))
             return bail(st);
-        if (int st = upload(h, &tno, ht.tile_node_off.data(), ht.tile_node_off.size()))
-            return bail(st);
-        if (int st = upload(h, &tn, ht.tile_nodes.data(), ht.tile_nodes.size()))
-            return bail(st);
-        if (int st = upload(h, &co, ht.csr_off.data(), ht.csr_off.size()))
+        if (int st = upload(h, &dtn, tnode.data(), tnode.size()))
             return bail(st);
         if (int st = upload(h, &ce, ht.csr_ent.data(), ht.csr_ent.size()))
             return bail(st);
         if (int st = upload(h, &npo, ht.node_part_off.data(), ht.node_part_off.size()))
-            return bail(st);
-        if (int st = upload(h, &nps, ht.node_part_slot.data(), ht.node_part_slot.size()))
             return bail(st);
         if (int st = dalloc(h, &part, 3 * ht.tile_nodes.size()))
             return bail(st);
@@ -474,13 +521,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.total_tile_nodes = (uint32_t)ht.tile_nodes.size();
         t.E = (uint32_t)E;
         t.planes = planes;
-        t.tile_elem_off = teo;
-        t.tile_node_off = tno;
-        t.tile_nodes = tn;
-        t.csr_off = co;
+        t.hdr = dh;
+        t.tnode = dtn;
         t.csr_ent = ce;
         t.node_part_off = npo;
-        t.node_part_slot = nps;
         t.part = part;
     }
     // solver scratch
@@ -559,10 +603,25 @@ int cwf_hip_keff_timed(cwf_hip_system *h, const float *x, float *y, int reps, do
     hipEvent_t a, b;
     HIPTRY(h, hipEventCreate(&a));
     HIPTRY(h, hipEventCreate(&b));
+    const char *dry = getenv("CWF_TIMED_PCG");  // diagnostic: time the PCG-mode tiles kernel instead
+    if (dry && h->mode == CWF_MODE_FAST && h->ds.iso)
+    {
+        Ctl c{};
+        c.active = 1;
+        c.beta = 0.5;
+        c.rho2[0] = c.rho2[1] = 1.0;
+        c.tol = 0.0;
+        HIPTRY(h, hipMemcpyAsync(h->ctl, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipMemsetAsync(h->part1, 0, h->part_cap * sizeof(double), h->stream));
+        HIPTRY(h, hipMemsetAsync(h->part2, 0, h->part_cap * sizeof(double), h->stream));
+        fast_tiles_pcg_dry(h, (unsigned)atoi(dry), 5, h->stream);
+    }
     HIPTRY(h, hipEventRecord(a, h->stream));
     for (int i = 0; i < reps; ++i)
     {
-        if (h->mode == CWF_MODE_FAST)
+        if (dry && h->mode == CWF_MODE_FAST && h->ds.iso)
+            fast_tiles_pcg_dry(h, (unsigned)atoi(dry), 1, h->stream);
+        else if (h->mode == CWF_MODE_FAST)
             fast_keff(h, x, y, false, nullptr, h->part0, h->stream);
         else
             parity_keff(h, x, y, false, nullptr, h->stream);
@@ -705,6 +764,50 @@ int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_setting
     if (residual_out)
         HIPTRY(h, hipMemcpyAsync(residual_out, h->r, n * sizeof(float), back, h->stream));
     HIPTRY(h, hipStreamSynchronize(h->stream));
+    return st;
+}
+
+int cwf_hip_solve_pcg_group(cwf_hip_system *const *members, int32_t count, const float *const *rhs,
+                            const cwf_pcg_settings *settings, float *const *x_inout, int kind,
+                            cwf_pcg_telemetry *telemetry)
+{
+    if (!members || count < 1 || !rhs || !settings || !x_inout)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    if (telemetry)
+        std::memset(telemetry, 0, sizeof *telemetry);
+    std::vector<cwf_hip_system *> g(members, members + count);
+    cwf_hip_comm *cm = g[0] ? g[0]->comm : nullptr;
+    for (int32_t i = 0; i < count; ++i)
+    {
+        if (int st = check_ready(g[i]))
+            return st;
+        if (!rhs[i] || !x_inout[i])
+            return set_error(g[i], CWF_ERR_ARGUMENT, "null pointer");
+        if (count > 1 && (!cm || cm->kind != 0 || g[i]->comm != cm || g[i]->rank != i || cm->nranks != count))
+            return set_error(g[i], CWF_ERR_ARGUMENT, "members must be every rank of one LOCAL communicator, in rank order",
+                             "member=" + std::to_string(i));
+    }
+    if (settings->max_iterations == 0)
+        return set_error(g[0], CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
+    std::vector<const float *> drhs(count);
+    for (int32_t i = 0; i < count; ++i)
+    {
+        cwf_hip_system *h = g[i];
+        if (int st = stage_in(h, rhs[i], h->rhs, h->ds.D, kind, &drhs[i]))
+            return st;
+        if (settings->warm_start)
+            HIPTRY(h, hipMemcpyAsync(h->x, x_inout[i], h->ds.D * sizeof(float),
+                                     kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                     h->stream));
+    }
+    int st = run_pcg_group(g, drhs, *settings, telemetry);
+    const hipMemcpyKind back = kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    for (int32_t i = 0; i < count; ++i)
+    {
+        cwf_hip_system *h = g[i];
+        HIPTRY(h, hipMemcpyAsync(x_inout[i], h->x, h->ds.D * sizeof(float), back, h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+    }
     return st;
 }
 

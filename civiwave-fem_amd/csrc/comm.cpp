@@ -1,0 +1,427 @@
+// comm.cpp -- communicators and the sharded FAST PCG schedule.
+//
+// Per PCG iteration a shard runs the same two kernels as one GPU, plus:
+//   tiles -> fold p.Ap shares -> all-gather(1 f64/rank) -> update -> fold r.r / r.z shares
+//         -> all-gather(2 f64/rank) -> halo(z)
+// Every rank folds the gathered per-rank scalars in rank order, so alpha / beta / convergence are
+// bitwise identical on all ranks and the control flow never diverges. Ghost rows are never
+// reduced: their search direction is rebuilt locally from the exchanged z (p = z + beta p_old is
+// the same fp32 expression on owner and ghost), so one halo of z per iteration suffices.
+// RCCL is loaded with dlopen (torch's copy when already in the process, else /opt/rocm/lib); the
+// LOCAL communicator runs all ranks of a decomposition in one process on one device (exchanges are
+// device copies on one shared stream) and exists to test the decomposition on a single GPU.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only; the entry points are resolved at run time
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "cwf_internal.hpp"
+
+namespace cwf
+{
+namespace
+{
+
+struct Rccl
+{
+    void *lib = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+const Rccl *rccl(std::string *why)
+{
+    static Rccl r;
+    static bool tried = false;
+    static std::string err;
+    if (!tried)
+    {
+        tried = true;
+        void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // the process's RCCL (torch's), if any
+        if (!lib)
+            lib = dlopen("librccl.so.1", RTLD_NOW);
+        if (!lib)
+            lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!lib)
+            err = std::string("dlopen librccl.so.1 failed: ") + dlerror();
+        else
+        {
+            bool ok = true;
+            auto sym = [&](auto &fn, const char *name) {
+                fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+                ok &= fn != nullptr;
+            };
+            sym(r.GetUniqueId, "ncclGetUniqueId");
+            sym(r.CommInitRank, "ncclCommInitRank");
+            sym(r.CommDestroy, "ncclCommDestroy");
+            sym(r.AllGather, "ncclAllGather");
+            sym(r.Send, "ncclSend");
+            sym(r.Recv, "ncclRecv");
+            sym(r.GroupStart, "ncclGroupStart");
+            sym(r.GroupEnd, "ncclGroupEnd");
+            sym(r.GetErrorString, "ncclGetErrorString");
+            if (ok)
+                r.lib = lib;
+            else
+                err = "librccl.so.1 lacks an expected entry point";
+        }
+    }
+    if (!r.lib && why)
+        *why = err;
+    return r.lib ? &r : nullptr;
+}
+
+int nccl_fail(cwf_hip_system *h, ncclResult_t e, const char *what)
+{
+    const Rccl *r = rccl(nullptr);
+    return set_error(h, CWF_ERR_COMM, std::string(what) + ": " + (r ? r->GetErrorString(e) : "rccl unavailable"),
+                     "nccl=" + std::to_string((int)e));
+}
+
+#define NCCLTRY(h, expr)                                                                                       \
+    do                                                                                                         \
+    {                                                                                                          \
+        ncclResult_t e__ = (expr);                                                                             \
+        if (e__ != ncclSuccess)                                                                                \
+            return nccl_fail((h), e__, #expr);                                                                 \
+    } while (0)
+
+#define HIPTRY(h, expr)                                                                                        \
+    do                                                                                                         \
+    {                                                                                                          \
+        hipError_t e__ = (expr);                                                                               \
+        if (e__ != hipSuccess)                                                                                 \
+            return hip_fail((h), e__, #expr);                                                                  \
+    } while (0)
+
+}  // namespace
+
+// in-place all-gather of `count` doubles per rank: slot r of buf is [r * count, (r + 1) * count)
+int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count)
+{
+    cwf_hip_system *h0 = g[0];
+    if (h0->nranks == 1)
+        return 0;
+    if (h0->comm->kind == 1)
+    {
+        const Rccl *r = rccl(nullptr);
+        double *b = h0->*buf;
+        NCCLTRY(h0, r->AllGather(b + (size_t)h0->rank * count, b, count, ncclFloat64,
+                                 static_cast<ncclComm_t>(h0->comm->nccl), h0->stream));
+        return 0;
+    }
+    for (cwf_hip_system *dst : g)
+        for (cwf_hip_system *src : g)
+            if (dst != src)
+                HIPTRY(dst, hipMemcpyAsync(dst->*buf + (size_t)src->rank * count, src->*buf + (size_t)src->rank * count,
+                                           count * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+    return 0;
+}
+
+// ghost rows of `vec` <- the owners' values
+int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec)
+{
+    for (cwf_hip_system *h : g)
+        halo_pack(h, h->*vec, h->stream);
+    cwf_hip_system *h0 = g[0];
+    if (h0->comm && h0->comm->kind == 1)
+    {
+        const Rccl *r = rccl(nullptr);
+        ncclComm_t c = static_cast<ncclComm_t>(h0->comm->nccl);
+        float *v = h0->*vec;
+        NCCLTRY(h0, r->GroupStart());
+        for (size_t k = 0; k < h0->nbr.size(); ++k)
+        {
+            const size_t ns = h0->send_off[k + 1] - h0->send_off[k], nr = h0->recv_off[k + 1] - h0->recv_off[k];
+            if (ns)
+                NCCLTRY(h0, r->Send(h0->sendbuf + 3 * h0->send_off[k], 3 * ns, ncclFloat32, h0->nbr[k], c, h0->stream));
+            if (nr)
+                NCCLTRY(h0, r->Recv(v + 3 * ((size_t)h0->ds.Nown + h0->recv_off[k]), 3 * nr, ncclFloat32, h0->nbr[k], c,
+                                    h0->stream));
+        }
+        NCCLTRY(h0, r->GroupEnd());
+        return 0;
+    }
+    // LOCAL: member m's ghosts from q = q's send segment for m
+    for (cwf_hip_system *m : g)
+        for (size_t k = 0; k < m->nbr.size(); ++k)
+        {
+            cwf_hip_system *q = g[m->nbr[k]];
+            const auto it = std::find(q->nbr.begin(), q->nbr.end(), m->rank);
+            if (it == q->nbr.end())
+                return set_error(m, CWF_ERR_COMM, "halo plans disagree", "rank=" + std::to_string(m->rank));
+            const size_t j = (size_t)(it - q->nbr.begin());
+            const size_t nr = m->recv_off[k + 1] - m->recv_off[k], ns = q->send_off[j + 1] - q->send_off[j];
+            if (nr != ns)
+                return set_error(m, CWF_ERR_COMM, "halo plans disagree",
+                                 "rank=" + std::to_string(m->rank) + " peer=" + std::to_string(q->rank));
+            if (nr)
+                HIPTRY(m, hipMemcpyAsync((m->*vec) + 3 * ((size_t)m->ds.Nown + m->recv_off[k]),
+                                         q->sendbuf + 3 * q->send_off[j], 3 * nr * sizeof(float),
+                                         hipMemcpyDeviceToDevice, m->stream));
+        }
+    return 0;
+}
+
+// solve_pcg prologue (pcg.cpp:744-828) for a sharded system: owned-row dots, gathered scalars, halos
+int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+{
+    for (cwf_hip_system *h : g)
+        parity_block_jacobi(h, h->inv, h->stream);
+    if (int st = comm_halo(g, &cwf_hip_system::x))  // warm start: ghost x from the owners
+        return st;
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        cwf_hip_system *h = g[i];
+        const uint32_t Down = 3u * h->ds.Nown;
+        fast_keff(h, h->x, h->Ap, true, nullptr, nullptr, h->stream);
+        launch_init_residual(h, rhs[i], h->stream);
+        fast_dot(rhs[i], rhs[i], nullptr, Down, h->part0, nullptr, h->stream);
+        fast_dot(h->r, h->r, nullptr, Down, h->part1, nullptr, h->stream);
+        fold_pair(h->part0, h->part1, fast_dot_blocks(Down), h->g_init + 2 * h->rank, h->stream);
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::g_init, 2))
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        fast_init_scalars_strided(h, h->g_init, h->g_init + 1, (uint32_t)h->nranks, 2u, rel_tol, h->stream);
+        launch_precond(h, h->ctl, h->stream);
+    }
+    if (int st = comm_halo(g, &cwf_hip_system::z))
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        const uint32_t Down = 3u * h->ds.Nown;
+        fast_dot(h->r, h->z, nullptr, Down, h->part0, nullptr, h->stream);
+        fold_pair(h->part0, nullptr, fast_dot_blocks(Down), h->g_rz0 + h->rank, h->stream);
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::g_rz0, 1))
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        fast_rho_from(h, h->g_rz0, (uint32_t)h->nranks, h->stream);
+        launch_p_init(h, h->stream);
+    }
+    return 0;
+}
+
+int sharded_pcg_iteration(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, unsigned it,
+                          hipEvent_t e0, hipEvent_t e1)
+{
+    if (e0)
+        (void)hipEventRecord(e0, g[0]->stream);
+    for (cwf_hip_system *h : g)
+        fast_tiles_pcg(h, it, h->stream);
+    if (e1)
+        (void)hipEventRecord(e1, g[0]->stream);
+    for (cwf_hip_system *h : g)
+        fast_fold_pap(h, h->stream);
+    if (int st = comm_allgather(g, &cwf_hip_system::g_pap, 1))
+        return st;
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        fast_update_pcg(g[i], rhs[i], it, g[i]->stream);
+        fast_fold_rrz(g[i], g[i]->stream);
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::g_rrz, 2))
+        return st;
+    return comm_halo(g, &cwf_hip_system::z);
+}
+
+}  // namespace cwf
+
+using namespace cwf;
+
+extern "C" {
+
+int cwf_hip_comm_unique_id(uint8_t *id)
+{
+    if (!id)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    std::string why;
+    const Rccl *r = rccl(&why);
+    if (!r)
+        return set_error(nullptr, CWF_ERR_COMM, why);
+    ncclUniqueId u;
+    NCCLTRY(nullptr, r->GetUniqueId(&u));
+    std::memcpy(id, u.internal, CWF_COMM_ID_BYTES);
+    return 0;
+}
+
+int cwf_hip_comm_create_rccl(int32_t nranks, int32_t rank, const uint8_t *id, int device, cwf_hip_comm **out)
+{
+    if (!id || !out)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "rank out of range");
+    std::string why;
+    const Rccl *r = rccl(&why);
+    if (!r)
+        return set_error(nullptr, CWF_ERR_COMM, why);
+    hipError_t he = hipSetDevice(device);
+    if (he != hipSuccess)
+        return hip_fail(nullptr, he, "hipSetDevice");
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, CWF_COMM_ID_BYTES);
+    ncclComm_t c = nullptr;
+    NCCLTRY(nullptr, r->CommInitRank(&c, nranks, u, rank));
+    cwf_hip_comm *cm = new (std::nothrow) cwf_hip_comm();
+    if (!cm)
+    {
+        (void)r->CommDestroy(c);
+        return set_error(nullptr, CWF_ERR_ALLOC, "host allocation failed");
+    }
+    cm->kind = 1;
+    cm->nranks = nranks;
+    cm->device = device;
+    cm->nccl = c;
+    *out = cm;
+    return 0;
+}
+
+int cwf_hip_comm_create_local(int32_t nranks, int device, cwf_hip_comm **out)
+{
+    if (!out)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    *out = nullptr;
+    if (nranks < 1)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "rank out of range");
+    hipError_t he = hipSetDevice(device);
+    if (he != hipSuccess)
+        return hip_fail(nullptr, he, "hipSetDevice");
+    cwf_hip_comm *cm = new (std::nothrow) cwf_hip_comm();
+    if (!cm)
+        return set_error(nullptr, CWF_ERR_ALLOC, "host allocation failed");
+    cm->kind = 0;
+    cm->nranks = nranks;
+    cm->device = device;
+    cm->members.assign(nranks, nullptr);
+    if ((he = hipStreamCreateWithFlags(&cm->stream, hipStreamNonBlocking)) != hipSuccess)
+    {
+        delete cm;
+        return hip_fail(nullptr, he, "hipStreamCreate");
+    }
+    *out = cm;
+    return 0;
+}
+
+void cwf_hip_comm_destroy(cwf_hip_comm *cm)
+{
+    if (!cm)
+        return;
+    (void)hipSetDevice(cm->device);
+    if (cm->kind == 1 && cm->nccl)
+    {
+        const Rccl *r = rccl(nullptr);
+        if (r)
+            (void)r->CommDestroy(static_cast<ncclComm_t>(cm->nccl));
+    }
+    for (cwf_hip_system *m : cm->members)
+        if (m)
+        {
+            m->comm = nullptr;  // a still-attached handle falls back to its own stream
+            if (m->own_stream)
+            {
+                m->stream = m->own_stream;
+                m->own_stream = nullptr;
+            }
+        }
+    if (cm->stream)
+    {
+        (void)hipStreamSynchronize(cm->stream);
+        (void)hipStreamDestroy(cm->stream);
+    }
+    delete cm;
+}
+
+int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, const cwf_shard_info *plan)
+{
+    if (!h || !cm || !plan)
+        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
+    if (h->comm)
+        return set_error(h, CWF_ERR_ARGUMENT, "handle already attached");
+    if (rank < 0 || rank >= cm->nranks || (cm->kind == 0 && cm->members[rank]))
+        return set_error(h, CWF_ERR_ARGUMENT, "rank out of range or taken", "rank=" + std::to_string(rank));
+    if (cm->device != h->device)
+        return set_error(h, CWF_ERR_ARGUMENT, "communicator and handle are on different devices");
+    if (plan->local_nodes != h->ds.N || plan->owned_nodes > h->ds.N)
+        return set_error(h, CWF_ERR_SIZE, "halo plan does not match the handle",
+                         "local_nodes=" + std::to_string(plan->local_nodes) + " handle_nodes=" + std::to_string(h->ds.N));
+    const uint32_t K = plan->neighbor_count;
+    if (K && (!plan->neighbor_ranks || !plan->send_offsets || !plan->recv_offsets ||
+              (plan->send_offsets[K] && !plan->send_nodes)))
+        return set_error(h, CWF_ERR_ARGUMENT, "null halo plan array");
+    for (uint32_t k = 0; k < K; ++k)
+        if (plan->neighbor_ranks[k] < 0 || plan->neighbor_ranks[k] >= cm->nranks || plan->neighbor_ranks[k] == rank)
+            return set_error(h, CWF_ERR_ARGUMENT, "bad neighbour rank", "k=" + std::to_string(k));
+    if (K && plan->owned_nodes + plan->recv_offsets[K] != plan->local_nodes)
+        return set_error(h, CWF_ERR_SIZE, "ghost ranges do not cover the ghost nodes");
+    const uint64_t nsend = K ? plan->send_offsets[K] : 0;
+    for (uint64_t i = 0; i < nsend; ++i)
+        if (plan->send_nodes[i] >= plan->owned_nodes)
+            return set_error(h, CWF_ERR_NODE_RANGE, "send list references a non-owned node", "i=" + std::to_string(i));
+    if (int st = hipSetDevice(h->device); st != hipSuccess)
+        return hip_fail(h, (hipError_t)st, "hipSetDevice");
+    const int n = cm->nranks;
+    auto alloc = [&](void **p, size_t bytes) -> int {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+        if (e != hipSuccess)
+            return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer", "bytes=" + std::to_string(bytes));
+        h->owned.push_back(*p);
+        h->bytes += std::max<size_t>(bytes, 16);
+        return 0;
+    };
+    void *p = nullptr;
+    if (int st = alloc(&p, 6 * (size_t)n * sizeof(double)))
+        return st;
+    h->g_pap = static_cast<double *>(p);
+    h->g_rrz = h->g_pap + n;
+    h->g_init = h->g_rrz + 2 * n;
+    h->g_rz0 = h->g_init + 2 * n;
+    HIPTRY(h, hipMemset(h->g_pap, 0, 6 * (size_t)n * sizeof(double)));
+    if (int st = alloc(&p, nsend * sizeof(uint32_t)))
+        return st;
+    h->send_idx = static_cast<uint32_t *>(p);
+    if (nsend)
+        HIPTRY(h, hipMemcpy(h->send_idx, plan->send_nodes, nsend * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (int st = alloc(&p, 3 * nsend * sizeof(float)))
+        return st;
+    h->sendbuf = static_cast<float *>(p);
+    h->nsend = nsend;
+    h->nbr.assign(plan->neighbor_ranks, plan->neighbor_ranks + K);
+    h->send_off.assign(plan->send_offsets, plan->send_offsets + K + 1);
+    h->recv_off.assign(plan->recv_offsets, plan->recv_offsets + K + 1);
+    if (!K)
+    {
+        h->send_off.assign(1, 0);
+        h->recv_off.assign(1, 0);
+    }
+    h->ds.Nown = (uint32_t)plan->owned_nodes;
+    h->comm = cm;
+    h->rank = rank;
+    h->nranks = n;
+    h->mode = CWF_MODE_FAST;
+    if (cm->kind == 0)
+    {
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+        h->own_stream = h->stream;
+        h->stream = cm->stream;
+        cm->members[rank] = h;
+    }
+    return 0;
+}
+
+}  // extern "C"

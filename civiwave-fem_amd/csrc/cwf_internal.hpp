@@ -35,14 +35,11 @@ struct DevTiles
     // g3 = -(g0 + g1 + g2) (partition of unity of the linear tet)
     const uint4 *planes = nullptr;
     const uint32_t *mat = nullptr;            // [E] material per element (tile order), NULL when M == 1
-    const uint32_t *tile_elem_off = nullptr;  // [ntiles+1]
-    const uint32_t *tile_node_off = nullptr;  // [ntiles+1]
-    const uint32_t *tile_nodes = nullptr;     // [total] global node ids; bit 31 = owner slot of the node
-    const uint32_t *csr_off = nullptr;        // [total+1]
+    const uint4 *hdr = nullptr;               // [ntiles] {first element, #elements, first tile node, #nodes}
+    const uint4 *tnode = nullptr;             // [total] {global node | owner bit 31, partial slot, csr begin, csr end}
     const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
-    const uint32_t *node_part_off = nullptr;  // [N+1]
-    const uint32_t *node_part_slot = nullptr; // [total]
-    float *part = nullptr;                    // [3*total] tile-node partial sums (scratch)
+    const uint32_t *node_part_off = nullptr;  // [N+1] node-major partial ranges
+    float *part = nullptr;                    // [3*total] tile-node partial sums, node-major (scratch)
 };
 
 struct HostTiles
@@ -50,7 +47,8 @@ struct HostTiles
     uint32_t ntiles = 0, max_tile_nodes = 0;
     std::vector<uint4> planes[3];
     std::vector<uint32_t> mat;
-    std::vector<uint32_t> tile_elem_off, tile_node_off, tile_nodes, csr_off, node_part_off, node_part_slot;
+    std::vector<uint32_t> tile_elem_off, tile_node_off, tile_nodes, csr_off, node_part_off, node_part_slot,
+        tile_slot;
     std::vector<uint16_t> csr_ent;
 };
 
@@ -62,6 +60,7 @@ struct DevSys
     uint32_t E = 0;  // tets
     uint32_t D = 0;  // dofs
     uint32_t M = 0;  // materials
+    uint32_t Nown = 0;  // owned nodes [0, Nown) (== N unless the handle is a shard; ghosts follow)
     const uint4 *erec = nullptr;
     const float *vol = nullptr;
     const uint32_t *mat = nullptr;
@@ -125,6 +124,31 @@ struct cwf_hip_system
     std::vector<hipEvent_t> ev;  // 2 per enqueued iteration of one batch
     double keff_ms = 0.0;
     uint64_t keff_count = 0;
+    // shard of a multi-rank system (cwf_hip_system_attach); nranks == 1 otherwise
+    cwf_hip_comm *comm = nullptr;
+    int rank = 0, nranks = 1;
+    hipStream_t own_stream = nullptr;  // the handle's stream while a LOCAL comm's stream is borrowed
+    std::vector<int32_t> nbr;
+    std::vector<uint64_t> send_off, recv_off;
+    uint32_t *send_idx = nullptr;  // [nsend] owned local node ids, per neighbour
+    float *sendbuf = nullptr;      // [3 nsend]
+    uint64_t nsend = 0;
+    // all-gathered per-rank scalars, slot of rank r at [r * count]
+    double *g_pap = nullptr;   // [nranks]      p.Ap
+    double *g_rrz = nullptr;   // [2 nranks]    {r.r, r.z}
+    double *g_init = nullptr;  // [2 nranks]    {rhs.rhs, r0.r0}
+    double *g_rz0 = nullptr;   // [nranks]      r0.z0
+    bool sharded() const { return nranks > 1 || comm != nullptr; }
+};
+
+struct cwf_hip_comm
+{
+    int kind = 0;  // 0 = LOCAL (one process, one device, shared stream), 1 = RCCL
+    int nranks = 1;
+    int device = 0;
+    void *nccl = nullptr;
+    hipStream_t stream = nullptr;                // LOCAL: the stream every member enqueues on
+    std::vector<cwf_hip_system *> members;       // LOCAL: by rank
 };
 
 namespace cwf
@@ -161,10 +185,26 @@ void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStrea
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st);
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
+void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_update_blocks(const DevSys &s);
 void fast_pcg_iteration(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr);
+
+// sharded FAST PCG (comm.cpp orchestrates, spmv_tiles.hip / kernels_fast.hip launch)
+void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> g_pap[rank]
+void fast_fold_rrz(cwf_hip_system *h, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
+void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st);
+void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st);
+void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count,
+                               uint32_t stride, double rel_tol, hipStream_t st);
+void fast_rho_from(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st);
+// comm.cpp
+int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);
+int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec);
+int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
+int sharded_pcg_iteration(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, unsigned it,
+                          hipEvent_t e0, hipEvent_t e1);
 
 // ---- stepper.hip ----
 void stepper_predictor(uint32_t D, const float *u, const float *v, const float *a, float *up, float *vp, double dt,

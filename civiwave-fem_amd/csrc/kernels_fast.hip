@@ -36,11 +36,12 @@ __device__ __forceinline__ double block_sum(double v, double *lds4)
 }
 
 // deterministic tree fold of `count` block partials by one 256-thread block
-__device__ __forceinline__ double tree_fold(const double *__restrict__ p, uint32_t count, double *red)
+__device__ __forceinline__ double tree_fold(const double *__restrict__ p, uint32_t count, double *red,
+                                            uint32_t stride = 1)
 {
     double v = 0.0;
     for (uint32_t i = threadIdx.x; i < count; i += kBlock)
-        v += p[i];
+        v += p[(size_t)i * stride];
     return block_sum(v, red);
 }
 
@@ -80,11 +81,12 @@ __global__ __launch_bounds__(kBlock) void k_dot_fast(const float *__restrict__ a
 // pcg.cpp:768-796 (norms, tolerance, early convergence)
 __global__ __launch_bounds__(kBlock) void k_fast_init_scalars(Ctl *ctl, const double *__restrict__ p_rhs,
                                                               const double *__restrict__ p_rr, uint32_t count,
-                                                              double rel_tol, double *__restrict__ hist)
+                                                              uint32_t stride, double rel_tol,
+                                                              double *__restrict__ hist)
 {
     __shared__ double red[4];
-    const double rhs_sq = tree_fold(p_rhs, count, red);
-    const double rr = tree_fold(p_rr, count, red);
+    const double rhs_sq = tree_fold(p_rhs, count, red, stride);
+    const double rr = tree_fold(p_rr, count, red, stride);
     if (threadIdx.x != 0)
         return;
     double rhs_norm = sqrt(rhs_sq);
@@ -158,11 +160,23 @@ void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStrea
     launch_init_residual(h, rhs, st);  // r = rhs - Ap, enforce (pure f32 ops, shared with parity)
     fast_dot(rhs, rhs, nullptr, s.D, h->part0, nullptr, st);
     fast_dot(h->r, h->r, nullptr, s.D, h->part1, nullptr, st);
-    k_fast_init_scalars<<<1, kBlock, 0, st>>>(h->ctl, h->part0, h->part1, nbD, rel_tol, h->hist);
+    k_fast_init_scalars<<<1, kBlock, 0, st>>>(h->ctl, h->part0, h->part1, nbD, 1u, rel_tol, h->hist);
     launch_precond(h, h->ctl, st);
     fast_dot(h->r, h->z, nullptr, s.D, h->part0, nullptr, st);
     k_fast_rho<<<1, kBlock, 0, st>>>(h->ctl, h->part0, nbD);
     launch_p_init(h, st);
+}
+
+// sharded prologue pieces (comm.cpp interleaves them with the all-gathers and halos)
+void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count,
+                               uint32_t stride, double rel_tol, hipStream_t st)
+{
+    k_fast_init_scalars<<<1, kBlock, 0, st>>>(h->ctl, p_rhs, p_rr, count, stride, rel_tol, h->hist);
+}
+
+void fast_rho_from(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st)
+{
+    k_fast_rho<<<1, kBlock, 0, st>>>(h->ctl, p_rz, count);
 }
 
 // one iteration = 2 kernels: K_eff tiles (+ beta/convergence of the previous update + p-update)

@@ -1,34 +1,34 @@
 // spmv_tiles.hip -- FAST-mode K_eff and the fused FAST PCG iteration (2 kernels / iteration).
 //
-// k_keff_tiles (256-thread workgroups looping over tiles of <= 512 Morton-ordered tets):
-//   a) gather the tile's distinct nodes into LDS: x (apply_keff) or, inside PCG, the on-the-fly
-//      search direction p_new = z + beta p_old (the p-update pass of pcg.cpp:897-914 is fused here);
-//   b) every element: stream its 48-B record from 3 SoA planes (each dwordx4 wave-load is one
-//      contiguous 1 KiB run), corners' values from LDS, fp32 strain -> stress -> 12 nodal forces
-//      scaled by V*s_K, stored to LDS as f[12][512] (bank-conflict free);
-//   c) every tile node: fold its (element, corner) forces in ascending element order through the
-//      tile's local CSR (deterministic, no atomics) and store the 12-B tile-node partial;
-//   d) PCG only: the workgroup's fp64 share of p.Ap (one partial per workgroup).
-// k_keff_finalize (apply_keff only): y = sum of the node's tile partials (ascending tile) + m s_M x,
-//   Dirichlet identity rows.
-// k_pcg_update_tiles (PCG only, grid-stride over nodes): Ap from the partials (never stored),
-//   recompute p_new, x += alpha p, r -= alpha Ap, Dirichlet enforce, z = M^-1 r, store x r z p;
-//   fp64 r.r and r.z shares per workgroup.
-// Scalars without atomics or fences: every workgroup of a consumer kernel folds the producer's
-// (<= 2048) workgroup partials itself in a fixed order, so alpha (update kernel) and |r|,
-// convergence, beta (tiles-kernel preamble, pcg.cpp:862-895) are computed identically everywhere;
-// the host passes the iteration index, and rho is double-buffered by iteration parity, so no
+// k_keff_tiles (one workgroup per tile of <= 512 Morton-ordered tets):
+//   a) tile-node phase: one 16-B record per tile node {node|owner, partial slot, csr begin, csr end}
+//      and the node's value gathered into LDS: x (apply_keff) or, inside PCG, the new search direction
+//      p = z + beta p_old formed on the fly (the p-update pass of pcg.cpp:897-914 is fused here);
+//   b) element phase: 48-B records from 3 SoA planes (every dwordx4 wave-load is one contiguous 1 KiB
+//      run), corner values from LDS, fp32 strain -> stress -> 12 nodal forces scaled by V*s_K, stored
+//      to LDS as f[12][512] (bank-conflict free);
+//   c) fold phase: every tile node sums its (element, corner) forces in ascending element order through
+//      the tile's local CSR (deterministic, no atomics) and stores a 12-B partial at its node-major
+//      slot; PCG adds the tile's fp64 share of p.Ap.
+// k_keff_finalize (apply_keff): y = node's partials (ascending tile) + m s_M x, Dirichlet identity rows.
+// k_pcg_update_tiles (PCG, 1024-thread workgroups, grid-stride): Ap from the node-major partials (never
+//   stored), the same p expression, x += alpha p, r -= alpha Ap, Dirichlet, z = M^-1 r, store x r z p,
+//   fp64 r.r / r.z shares.
+// Scalars without atomics or fences: every consumer workgroup folds the producer's partials itself in a
+// fixed order (alpha in the update kernel, |r| / convergence / beta in the tiles-kernel preamble,
+// pcg.cpp:840-895); the host passes the iteration index and rho is double-buffered by parity, so no
 // device scalar is read after being written inside one kernel.
+#include <algorithm>
+
 #include "cwf_internal.hpp"
 
 namespace cwf
 {
 namespace
 {
-constexpr int kBlock = 256;
 constexpr int kMaxM = 16;
-constexpr unsigned kMaxTileBlocks = 2048;
-constexpr unsigned kMaxUpdateBlocks = 1024;
+constexpr int kUpdThreads = 1024;
+constexpr unsigned kMaxUpdateBlocks = 256;
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -38,45 +38,57 @@ __device__ __forceinline__ double wave_sum(double v)
     return v;
 }
 
-// 256-thread block sum, fixed order; result valid in every thread
-__device__ __forceinline__ double block_sum(double v, double *red4)
+// NT-thread block sum in a fixed order; result valid in every thread. red: NT/64 doubles.
+template <int NT> __device__ __forceinline__ double block_sum(double v, double *red)
 {
     v = wave_sum(v);
     if ((threadIdx.x & 63) == 0)
-        red4[threadIdx.x >> 6] = v;
+        red[threadIdx.x >> 6] = v;
     __syncthreads();
-    const double t = (red4[0] + red4[1]) + (red4[2] + red4[3]);
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w)
+        t += red[w];
     __syncthreads();
     return t;
 }
 
-// fixed-order fold of `count` doubles by the whole block (valid in every thread)
-__device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigned count, double *red4)
+template <int NT>
+__device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigned count, double *red,
+                                           unsigned stride = 1)
 {
     double v = 0.0;
-    for (unsigned i = threadIdx.x; i < count; i += kBlock)
-        v += p[i];
-    return block_sum(v, red4);
+    for (unsigned i = threadIdx.x; i < count; i += NT)
+        v += p[(size_t)i * stride];
+    return block_sum<NT>(v, red);
 }
 
-// pcg.cpp:862-895 for iteration `it` >= 1 from the update kernel's r.r / r.z shares.
-// Returns false when the solve is over (converged or rho breakdown); writes beta for this iteration.
+// pcg.cpp:862-895 for iteration `it` >= 1 from the update kernel's r.r / r.z shares (stride 1), or
+// from the all-gathered per-rank {r.r, r.z} pairs of a sharded system (stride 2, rank order).
+// Returns false when the solve is over (converged or rho breakdown); *beta_out = beta for this iteration.
+template <int NT>
 __device__ __forceinline__ bool residual_step(Ctl *ctl, const double *__restrict__ prr, const double *__restrict__ prz,
-                                              unsigned nparts, unsigned it, double *__restrict__ hist, double *red4,
-                                              float *beta_out)
+                                              unsigned nparts, unsigned stride, unsigned it,
+                                              double *__restrict__ hist, double *red, float *beta_out,
+                                              bool dry = false)
 {
     if (it == 0)
     {
         *beta_out = 0.f;
         return true;
     }
-    const double rr = fold_all(prr, nparts, red4);
-    const double rz = fold_all(prz, nparts, red4);
+    const double rr = fold_all<NT>(prr, nparts, red, stride);
+    const double rz = fold_all<NT>(prz, nparts, red, stride);
     const double res = sqrt(rr);
     const double rho_old = ctl->rho2[(it - 1) & 1u];
     const bool conv = res <= ctl->tol;
     const bool err = !conv && fabs(rho_old) < 1.0e-18;
     const double beta = (conv || err) ? 0.0 : rz / rho_old;
+    if (dry)  // diagnostic timing: full work, no side effects
+    {
+        *beta_out = (float)beta;
+        return true;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0)
     {
         ctl->res = res;
@@ -135,163 +147,279 @@ __device__ __forceinline__ uint32_t dsrc(bool iso, uint32_t t)
     return iso ? (t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7) : t;
 }
 
+// value of one tile node: x (apply, optionally sanitised) or p_new = z + beta p_old (PCG)
+template <bool SANITIZE, int MODE>
+__device__ __forceinline__ void gather_node(const DevSys &s, const float *__restrict__ x, const float *__restrict__ z,
+                                            float beta, uint32_t g, float u[3])
+{
+    if constexpr (MODE == 1)
+    {
+        // constrained dofs stay 0 (z_c = 0, p_c = 0)
+        u[0] = fmaf(beta, x[3u * g + 0], z[3u * g + 0]);
+        u[1] = fmaf(beta, x[3u * g + 1], z[3u * g + 1]);
+        u[2] = fmaf(beta, x[3u * g + 2], z[3u * g + 2]);
+    }
+    else
+    {
+        u[0] = x[3u * g + 0];
+        u[1] = x[3u * g + 1];
+        u[2] = x[3u * g + 2];
+        if constexpr (SANITIZE)
+        {
+            const uint32_t mk = s.mask[g];
+            u[0] = (mk & 1u) ? 0.f : u[0];
+            u[1] = (mk & 2u) ? 0.f : u[1];
+            u[2] = (mk & 4u) ? 0.f : u[2];
+        }
+    }
+}
+
+// strain -> stress -> 12 nodal forces of one tet (48-B record q0..q2, corner values from LDS), scaled by
+// V s_K and stored to LDS as f[12][kTileElems] (fp32 counterpart of pcg.cpp:140-220)
+template <bool ISO>
+__device__ __forceinline__ void element_forces(const DevSys &s, uint4 q0, uint4 q1, uint4 q2, uint32_t mi, uint32_t j,
+                                               const float *sp, uint32_t ms, const float *dtab, float sK, float *sf)
+{
+    constexpr int kTab = ISO ? 12 : 36;
+    float g[12];
+    g[0] = __uint_as_float(q0.z);
+    g[1] = __uint_as_float(q0.w);
+    g[2] = __uint_as_float(q1.x);
+    g[3] = __uint_as_float(q1.y);
+    g[4] = __uint_as_float(q1.z);
+    g[5] = __uint_as_float(q1.w);
+    g[6] = __uint_as_float(q2.x);
+    g[7] = __uint_as_float(q2.y);
+    g[8] = __uint_as_float(q2.z);
+    g[9] = -(g[0] + g[3] + g[6]);
+    g[10] = -(g[1] + g[4] + g[7]);
+    g[11] = -(g[2] + g[5] + g[8]);
+    const uint32_t li[4] = {q0.x & 0xffffu, q0.x >> 16, q0.y & 0xffffu, q0.y >> 16};
+    float eps[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        const float u0 = sp[li[a]], u1 = sp[ms + li[a]], u2 = sp[2 * ms + li[a]];
+        const float gx = g[3 * a], gy = g[3 * a + 1], gz = g[3 * a + 2];
+        eps[0] = fmaf(gx, u0, eps[0]);
+        eps[1] = fmaf(gy, u1, eps[1]);
+        eps[2] = fmaf(gz, u2, eps[2]);
+        eps[3] = fmaf(gx, u1, fmaf(gy, u0, eps[3]));
+        eps[4] = fmaf(gy, u2, fmaf(gz, u1, eps[4]));
+        eps[5] = fmaf(gx, u2, fmaf(gz, u0, eps[5]));
+    }
+    float sig[6];
+    if (mi < (uint32_t)kMaxM)
+        stress_f32<ISO>(dtab + kTab * mi, eps, sig);
+    else
+    {
+        float tab[36];
+        for (int t = 0; t < kTab; ++t)
+            tab[t] = (float)s.dmat[36u * mi + dsrc(ISO, t)];
+        stress_f32<ISO>(tab, eps, sig);
+    }
+    const float vol = __uint_as_float(q2.w) * sK;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        const float ax = g[3 * a], ay = g[3 * a + 1], az = g[3 * a + 2];
+        sf[(3 * a + 0) * kTileElems + j] = vol * fmaf(az, sig[5], fmaf(ay, sig[3], ax * sig[0]));
+        sf[(3 * a + 1) * kTileElems + j] = vol * fmaf(az, sig[4], fmaf(ax, sig[3], ay * sig[1]));
+        sf[(3 * a + 2) * kTileElems + j] = vol * fmaf(ax, sig[5], fmaf(ay, sig[4], az * sig[2]));
+    }
+}
+
 struct PcgArgs
 {
-    const float *z;           // z (PCG) -- x holds p_old
+    const float *z;           // z (PCG); x holds p_old
     Ctl *ctl;
-    double *part_dot;         // out: per-workgroup p.Ap share
+    double *part_dot;         // out: per-tile p.Ap share
     const double *prr, *prz;  // in: update kernel's r.r / r.z shares of the previous iteration
     unsigned nupd;
+    unsigned stride;          // 1, or 2 for the gathered {r.r, r.z} pairs of a sharded system
     unsigned it;
     double *hist;
+    unsigned abl;  // diagnostic ablation bits (CWF_ABLATE), 0 in normal runs
 };
 
 // MODE 0: apply (gather x, optional sanitize); MODE 1: PCG (gather z, p_old -> p_new)
-template <bool ISO, bool SANITIZE, int MODE>
-__global__ __launch_bounds__(kBlock) void k_keff_tiles(DevSys s, const float *__restrict__ x, PcgArgs pa)
+template <bool ISO, bool SANITIZE, int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__restrict__ x, PcgArgs pa)
 {
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
-    float *sf = lds;                    // [12][kTileElems]
-    float *sp = lds + 12 * kTileElems;  // [3][max_tile_nodes]
+    float *sf = lds;                                                 // [12][kTileElems]
+    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * kTileElems);  // [4*kTileElems] local CSR
+    float *sp = lds + 14 * kTileElems;                               // [3][max_tile_nodes]
     __shared__ float dtab[kMaxM * 36];
-    __shared__ double red[4];
-    float beta = 0.f;
+    __shared__ double red[NT / 64];
     if constexpr (MODE == 1)
     {
         if (!pa.ctl->active)
             return;
-        if (!residual_step(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.it, pa.hist, red, &beta))
-            return;
     }
     const DevTiles &T = s.t;
+    const uint4 hd = T.hdr[blockIdx.x];
+    const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
     const uint32_t ms = T.max_tile_nodes;
-    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
-    for (uint32_t i = threadIdx.x; i < nm * kTab; i += kBlock)
-        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
-    const float sK = (float)s.sK, sM = (float)s.sM;
-    const uint4 *P0 = T.planes, *P1 = T.planes + T.E, *P2 = T.planes + 2u * T.E;
-    double pap = 0.0;
-    for (uint32_t tile = blockIdx.x; tile < T.ntiles; tile += gridDim.x)
+    const float sK = (float)s.sK;
+    // (a) issue every load that does not depend on beta: the first tile-node record and its value(s),
+    //     and the tile's local CSR (4*ne u16 entries starting at 4*e0) staged into LDS
+    const uint32_t i0 = threadIdx.x;
+    uint4 tn0 = uint4{0u, 0u, 0u, 0u};
+    float v0[3] = {0.f, 0.f, 0.f}, w0[3] = {0.f, 0.f, 0.f};
+    if (i0 < nn)
     {
-        const uint32_t e0 = T.tile_elem_off[tile], ne = T.tile_elem_off[tile + 1] - e0;
-        const uint32_t nb = T.tile_node_off[tile], nn = T.tile_node_off[tile + 1] - nb;
-        __syncthreads();  // previous tile's LDS reads are done
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlock)
+        tn0 = T.tnode[nb + i0];
+        const uint32_t g = tn0.x & 0x7fffffffu;
+        v0[0] = x[3u * g + 0];
+        v0[1] = x[3u * g + 1];
+        v0[2] = x[3u * g + 2];
+        if constexpr (MODE == 1)
         {
-            const uint32_t g = T.tile_nodes[nb + i] & 0x7fffffffu;
-            float u0, u1, u2;
-            if constexpr (MODE == 1)
-            {
-                // p_new = z + beta p_old; constrained dofs stay 0 (z_c = 0, p_c = 0)
-                u0 = fmaf(beta, x[3u * g + 0], pa.z[3u * g + 0]);
-                u1 = fmaf(beta, x[3u * g + 1], pa.z[3u * g + 1]);
-                u2 = fmaf(beta, x[3u * g + 2], pa.z[3u * g + 2]);
-            }
-            else
-            {
-                u0 = x[3u * g + 0];
-                u1 = x[3u * g + 1];
-                u2 = x[3u * g + 2];
-                if constexpr (SANITIZE)
-                {
-                    const uint32_t mk = s.mask[g];
-                    u0 = (mk & 1u) ? 0.f : u0;
-                    u1 = (mk & 2u) ? 0.f : u1;
-                    u2 = (mk & 4u) ? 0.f : u2;
-                }
-            }
-            sp[i] = u0;
-            sp[ms + i] = u1;
-            sp[2 * ms + i] = u2;
+            w0[0] = pa.z[3u * g + 0];
+            w0[1] = pa.z[3u * g + 1];
+            w0[2] = pa.z[3u * g + 2];
         }
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < ne; j += kBlock)
+        else if constexpr (SANITIZE)
         {
-            const uint32_t e = e0 + j;
-            const uint4 q0 = P0[e], q1 = P1[e], q2 = P2[e];
-            float g[12];
-            g[0] = __uint_as_float(q0.z);
-            g[1] = __uint_as_float(q0.w);
-            g[2] = __uint_as_float(q1.x);
-            g[3] = __uint_as_float(q1.y);
-            g[4] = __uint_as_float(q1.z);
-            g[5] = __uint_as_float(q1.w);
-            g[6] = __uint_as_float(q2.x);
-            g[7] = __uint_as_float(q2.y);
-            g[8] = __uint_as_float(q2.z);
-            g[9] = -(g[0] + g[3] + g[6]);
-            g[10] = -(g[1] + g[4] + g[7]);
-            g[11] = -(g[2] + g[5] + g[8]);
-            const uint32_t li[4] = {q0.x & 0xffffu, q0.x >> 16, q0.y & 0xffffu, q0.y >> 16};
-            float eps[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            const uint32_t mk = s.mask[g];
+            v0[0] = (mk & 1u) ? 0.f : v0[0];
+            v0[1] = (mk & 2u) ? 0.f : v0[1];
+            v0[2] = (mk & 4u) ? 0.f : v0[2];
+        }
+    }
+    // the thread's element records (kPer per thread), consumed after the gather barrier
+    constexpr int kPer = kTileElems / NT;
+    uint4 pq[kPer][3];
+    {
+        const uint4 *P0 = T.planes, *P1 = T.planes + T.E, *P2 = T.planes + 2u * T.E;
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
-            {
-                const float u0 = sp[li[a]], u1 = sp[ms + li[a]], u2 = sp[2 * ms + li[a]];
-                const float gx = g[3 * a], gy = g[3 * a + 1], gz = g[3 * a + 2];
-                eps[0] = fmaf(gx, u0, eps[0]);
-                eps[1] = fmaf(gy, u1, eps[1]);
-                eps[2] = fmaf(gz, u2, eps[2]);
-                eps[3] = fmaf(gx, u1, fmaf(gy, u0, eps[3]));
-                eps[4] = fmaf(gy, u2, fmaf(gz, u1, eps[4]));
-                eps[5] = fmaf(gx, u2, fmaf(gz, u0, eps[5]));
-            }
-            const uint32_t mi = T.mat ? T.mat[e] : 0u;
-            float sig[6];
-            if (mi < (uint32_t)kMaxM)
-                stress_f32<ISO>(dtab + kTab * mi, eps, sig);
-            else
-            {
-                float tab[36];
-                for (int t = 0; t < kTab; ++t)
-                    tab[t] = (float)s.dmat[36u * mi + dsrc(ISO, t)];
-                stress_f32<ISO>(tab, eps, sig);
-            }
-            const float vol = __uint_as_float(q2.w) * sK;
+        for (int k = 0; k < kPer; ++k)
+        {
+            const uint32_t j = threadIdx.x + k * NT;
+            const uint32_t e = e0 + (j < ne ? j : 0u);
+            pq[k][0] = P0[e];
+            pq[k][1] = P1[e];
+            pq[k][2] = P2[e];
+        }
+    }
+    {
+        const uint2 *src = reinterpret_cast<const uint2 *>(T.csr_ent + 4ull * e0);  // 8-B aligned
+        uint2 *dst = reinterpret_cast<uint2 *>(sc);
+        for (uint32_t k = threadIdx.x; k < ne; k += NT)
+            dst[k] = src[k];
+    }
+    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
+    for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
+        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
+    float beta = 0.f;
+    if constexpr (MODE == 1)
+    {
+        // pcg.cpp:862-895 of the previous update; its fold latency overlaps the loads above
+        if (pa.abl & 1u)
+            beta = (float)pa.ctl->beta;
+        else if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta,
+                                       pa.abl & 32u))
+            return;
+    }
+    if (i0 < nn)
+    {
+        if constexpr (MODE == 1)
+        {
+            // p_new = z + beta p_old; constrained dofs stay 0 (z_c = 0, p_c = 0)
+            v0[0] = fmaf(beta, v0[0], w0[0]);
+            v0[1] = fmaf(beta, v0[1], w0[1]);
+            v0[2] = fmaf(beta, v0[2], w0[2]);
+        }
+        sp[i0] = v0[0];
+        sp[ms + i0] = v0[1];
+        sp[2 * ms + i0] = v0[2];
+    }
+    for (uint32_t i = i0 + NT; i < nn; i += NT)
+    {
+        const uint4 tn = T.tnode[nb + i];
+        float u[3];
+        gather_node<SANITIZE, MODE>(s, x, pa.z, beta, tn.x & 0x7fffffffu, u);
+        sp[i] = u[0];
+        sp[ms + i] = u[1];
+        sp[2 * ms + i] = u[2];
+    }
+    __syncthreads();
+    // (b) elements (records prefetched at kernel entry)
+    if (!(pa.abl & 16u))
+    {
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+        for (int k = 0; k < kPer; ++k)
+        {
+            const uint32_t j = threadIdx.x + k * NT;
+            if (j < ne)
+                element_forces<ISO>(s, pq[k][0], pq[k][1], pq[k][2], T.mat ? T.mat[e0 + j] : 0u, j, sp, ms, dtab,
+                                    sK, sf);
+        }
+    }
+    __syncthreads();
+    // (c) fold per tile node
+    double pap = 0.0;
+    const float sM = (float)s.sM;
+    for (uint32_t i = threadIdx.x; i < ((pa.abl & 8u) ? 0u : nn); i += NT)
+    {
+        const uint4 tn = i == threadIdx.x ? tn0 : T.tnode[nb + i];
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+        const uint32_t qb = 4u * e0;
+        const uint32_t qe = tn.w - qb;
+        uint32_t q = tn.z - qb;
+        // 4 independent (entry, force) LDS chains in flight; the sums stay in ascending-entry order
+        for (; q + 4 <= qe; q += 4)
+        {
+            uint32_t ent[4];
+            float f[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                ent[u] = sc[q + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
             {
-                const float ax = g[3 * a], ay = g[3 * a + 1], az = g[3 * a + 2];
-                sf[(3 * a + 0) * kTileElems + j] = vol * fmaf(az, sig[5], fmaf(ay, sig[3], ax * sig[0]));
-                sf[(3 * a + 1) * kTileElems + j] = vol * fmaf(az, sig[4], fmaf(ax, sig[3], ay * sig[1]));
-                sf[(3 * a + 2) * kTileElems + j] = vol * fmaf(ax, sig[5], fmaf(ay, sig[4], az * sig[2]));
+                const uint32_t el = ent[u] >> 2, c = 3u * (ent[u] & 3u);
+                f[u][0] = sf[(c + 0) * kTileElems + el];
+                f[u][1] = sf[(c + 1) * kTileElems + el];
+                f[u][2] = sf[(c + 2) * kTileElems + el];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                a0 += f[u][0];
+                a1 += f[u][1];
+                a2 += f[u][2];
             }
         }
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlock)
+        for (; q < qe; ++q)
         {
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-            const uint32_t qb = T.csr_off[nb + i], qe = T.csr_off[nb + i + 1];
-            for (uint32_t q = qb; q < qe; ++q)
+            const uint32_t ent = sc[q];
+            const uint32_t el = ent >> 2, c = 3u * (ent & 3u);
+            a0 += sf[(c + 0) * kTileElems + el];
+            a1 += sf[(c + 1) * kTileElems + el];
+            a2 += sf[(c + 2) * kTileElems + el];
+        }
+        float *o = T.part + 3ull * tn.y;
+        o[0] = a0;
+        o[1] = a1;
+        o[2] = a2;
+        if (MODE == 1 && !(pa.abl & 4u) && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
+        {
+            const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
+            pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+            if (tn.x & 0x80000000u)  // the node's owner slot adds its mass term m s_M |p|^2 once
             {
-                const uint32_t ent = T.csr_ent[q];
-                const uint32_t el = ent >> 2, c = 3u * (ent & 3u);
-                a0 += sf[(c + 0) * kTileElems + el];
-                a1 += sf[(c + 1) * kTileElems + el];
-                a2 += sf[(c + 2) * kTileElems + el];
-            }
-            float *o = T.part + 3ull * (nb + i);
-            o[0] = a0;
-            o[1] = a1;
-            o[2] = a2;
-            if constexpr (MODE == 1)
-            {
-                const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
-                pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
-                const uint32_t tg = T.tile_nodes[nb + i];
-                if (tg & 0x80000000u)  // the node's owner slot adds its mass term m s_M |p|^2 once
-                {
-                    const float m = s.mass[tg & 0x7fffffffu] * sM;
-                    pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
-                           (double)(m * p2) * (double)p2;
-                }
+                const float m = s.mass[tn.x & 0x7fffffffu] * sM;
+                pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
+                       (double)(m * p2) * (double)p2;
             }
         }
     }
     if constexpr (MODE == 1)
     {
-        const double t = block_sum(pap, red);
+        const double t = block_sum<NT>(pap, red);
         if (threadIdx.x == 0)
             pa.part_dot[blockIdx.x] = t;
     }
@@ -299,29 +427,55 @@ __global__ __launch_bounds__(kBlock) void k_keff_tiles(DevSys s, const float *__
 
 // pcg.cpp:862-895 for the last iteration of a batch (the next batch's tiles kernel repeats it
 // idempotently): one workgroup
-__global__ __launch_bounds__(kBlock) void k_pcg_check(Ctl *ctl, const double *__restrict__ prr,
-                                                      const double *__restrict__ prz, unsigned nparts, unsigned it,
-                                                      double *__restrict__ hist)
+__global__ __launch_bounds__(256) void k_pcg_check(Ctl *ctl, const double *__restrict__ prr,
+                                                   const double *__restrict__ prz, unsigned nparts, unsigned stride,
+                                                   unsigned it, double *__restrict__ hist)
 {
     __shared__ double red[4];
     if (!ctl->active)
         return;
     float beta;
-    (void)residual_step(ctl, prr, prz, nparts, it, hist, red, &beta);
+    (void)residual_step<256>(ctl, prr, prz, nparts, stride, it, hist, red, &beta);
+}
+
+// one workgroup: out[0] = fold(a[0..n)), out[1] = fold(b[0..n)) (b may be NULL), fixed order
+__global__ __launch_bounds__(256) void k_fold_pair(const double *__restrict__ a, const double *__restrict__ b,
+                                                   unsigned n, double *__restrict__ out)
+{
+    __shared__ double red[4];
+    const double ta = fold_all<256>(a, n, red);
+    const double tb = b ? fold_all<256>(b, n, red) : 0.0;
+    if (threadIdx.x == 0)
+    {
+        out[0] = ta;
+        if (b)
+            out[1] = tb;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_halo_pack(const uint32_t *__restrict__ idx, uint64_t n,
+                                                   const float *__restrict__ v, float *__restrict__ out)
+{
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull)
+    {
+        const uint32_t q = idx[i];
+        out[3 * i + 0] = v[3ull * q + 0];
+        out[3 * i + 1] = v[3ull * q + 1];
+        out[3 * i + 2] = v[3ull * q + 2];
+    }
 }
 
 template <bool SANITIZE>
-__global__ __launch_bounds__(kBlock) void k_keff_finalize(DevSys s, const float *__restrict__ x,
-                                                          float *__restrict__ y)
+__global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__restrict__ x, float *__restrict__ y)
 {
     const DevTiles &T = s.t;
-    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = blockIdx.x * 256 + threadIdx.x;
     if (n >= s.N)
         return;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
     {
-        const float *pp = T.part + 3ull * T.node_part_slot[q];
+        const float *pp = T.part + 3ull * q;
         a0 += pp[0];
         a1 += pp[1];
         a2 += pp[2];
@@ -337,19 +491,17 @@ __global__ __launch_bounds__(kBlock) void k_keff_finalize(DevSys s, const float 
     y[3u * n + 2] = (mk & 4u) ? x2 : y2;
 }
 
-__global__ __launch_bounds__(kBlock) void k_pcg_update_tiles(DevSys s, const float *__restrict__ rhs,
-                                                             const float *__restrict__ inv, float *__restrict__ x,
-                                                             float *__restrict__ r, float *__restrict__ z,
-                                                             float *__restrict__ p, Ctl *__restrict__ ctl,
-                                                             const double *__restrict__ part_dot, unsigned ntp,
-                                                             double *__restrict__ prr, double *__restrict__ prz,
-                                                             unsigned it)
+__global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
+    DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, float *__restrict__ x,
+    float *__restrict__ r, float *__restrict__ z, float *__restrict__ p, Ctl *__restrict__ ctl,
+    const double *__restrict__ part_dot, unsigned ntp, double *__restrict__ prr, double *__restrict__ prz,
+    unsigned it)
 {
-    __shared__ double red[4];
+    __shared__ double red[kUpdThreads / 64];
     if (!ctl->active)
         return;
     // pcg.cpp:840-852: alpha = rho / (p . Ap)
-    const double denom = fold_all(part_dot, ntp, red);
+    const double denom = fold_all<kUpdThreads>(part_dot, ntp, red);
     if (fabs(denom) < 1.0e-18)
     {
         if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -372,12 +524,19 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update_tiles(DevSys s, const flo
     const float alpha = (float)alpha_d, beta = (float)ctl->beta;
     const float sM = (float)s.sM;
     double rr = 0.0, rz = 0.0;
-    for (uint32_t n = blockIdx.x * kBlock + threadIdx.x; n < s.N; n += gridDim.x * kBlock)
+    for (uint32_t n = blockIdx.x * kUpdThreads + threadIdx.x; n < s.N; n += gridDim.x * kUpdThreads)
     {
+        if (n >= s.Nown)  // ghost node of a shard: only its search direction (the tiles kernel's p) is kept
+        {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                p[3u * n + k] = fmaf(beta, p[3u * n + k], z[3u * n + k]);
+            continue;
+        }
         float a0 = 0.f, a1 = 0.f, a2 = 0.f;
         for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
         {
-            const float *pp = T.part + 3ull * T.node_part_slot[q];
+            const float *pp = T.part + 3ull * q;
             a0 += pp[0];
             a1 += pp[1];
             a2 += pp[2];
@@ -415,8 +574,8 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update_tiles(DevSys s, const flo
             rz += (double)rv[k] * (double)zk;
         }
     }
-    const double t0 = block_sum(rr, red);
-    const double t1 = block_sum(rz, red);
+    const double t0 = block_sum<kUpdThreads>(rr, red);
+    const double t1 = block_sum<kUpdThreads>(rz, red);
     if (threadIdx.x == 0)
     {
         prr[blockIdx.x] = t0;
@@ -428,15 +587,35 @@ inline unsigned grid_for(uint32_t n, uint32_t b) { return (n + b - 1) / b; }
 
 inline size_t tiles_lds(const DevSys &s)
 {
-    return sizeof(float) * (12 * kTileElems + 3 * (size_t)s.t.max_tile_nodes);
+    // element forces [12][kTileElems] f32 + local CSR [4*kTileElems] u16 + node values [3][max_tile_nodes]
+    return sizeof(float) * (14 * kTileElems + 3 * (size_t)s.t.max_tile_nodes);
+}
+
+template <bool ISO, bool SAN, int MODE>
+void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st)
+{
+    const size_t lds = tiles_lds(s);
+    if (nt == 512)
+        k_keff_tiles<ISO, SAN, MODE, 512><<<s.t.ntiles, 512, lds, st>>>(s, x, pa);
+    else
+        k_keff_tiles<ISO, SAN, MODE, 256><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
 }
 }  // namespace
 
-unsigned fast_tile_blocks(const DevSys &s) { return s.t.ntiles < kMaxTileBlocks ? s.t.ntiles : kMaxTileBlocks; }
+unsigned fast_tile_blocks(const DevSys &s) { return s.t.ntiles; }
 unsigned fast_update_blocks(const DevSys &s)
 {
-    const unsigned g = grid_for(s.N, kBlock);
+    const unsigned g = grid_for(s.N, kUpdThreads);
     return g < kMaxUpdateBlocks ? (g ? g : 1u) : kMaxUpdateBlocks;
+}
+
+static int tile_threads()
+{
+    static int nt = [] {
+        const char *e = getenv("CWF_TILE_THREADS");
+        return e && atoi(e) == 512 ? 512 : 256;
+    }();
+    return nt;
 }
 
 void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, double *part,
@@ -448,47 +627,94 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
         return;
     if (s.t.ntiles)
     {
-        const size_t lds = tiles_lds(s);
-        const unsigned g = fast_tile_blocks(s);
         PcgArgs none{};
+        const int nt = tile_threads();
         if (s.iso)
-            sanitize ? k_keff_tiles<true, true, 0><<<g, kBlock, lds, st>>>(s, x, none)
-                     : k_keff_tiles<true, false, 0><<<g, kBlock, lds, st>>>(s, x, none);
+            sanitize ? launch_tiles<true, true, 0>(s, x, none, nt, st) : launch_tiles<true, false, 0>(s, x, none, nt, st);
         else
-            sanitize ? k_keff_tiles<false, true, 0><<<g, kBlock, lds, st>>>(s, x, none)
-                     : k_keff_tiles<false, false, 0><<<g, kBlock, lds, st>>>(s, x, none);
+            sanitize ? launch_tiles<false, true, 0>(s, x, none, nt, st)
+                     : launch_tiles<false, false, 0>(s, x, none, nt, st);
     }
-    const unsigned g = grid_for(s.N, kBlock);
+    const unsigned g = grid_for(s.N, 256);
     if (sanitize)
-        k_keff_finalize<true><<<g, kBlock, 0, st>>>(s, x, y);
+        k_keff_finalize<true><<<g, 256, 0, st>>>(s, x, y);
     else
-        k_keff_finalize<false><<<g, kBlock, 0, st>>>(s, x, y);
+        k_keff_finalize<false><<<g, 256, 0, st>>>(s, x, y);
 }
 
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    PcgArgs pa{h->z, h->ctl, h->part0, h->part1, h->part2, fast_update_blocks(s), it, h->hist};
-    const unsigned g = fast_tile_blocks(s);
-    const size_t lds = tiles_lds(s);
+    if (!s.t.ntiles)
+        return;
+    static const unsigned abl = [] {
+        const char *e = getenv("CWF_ABLATE");
+        return e ? (unsigned)atoi(e) : 0u;
+    }();
+    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->part1, h->part2, fast_update_blocks(s), 1u, it, h->hist,
+               abl};
+    if (h->sharded())
+    {
+        pa.prr = h->g_rrz;
+        pa.prz = h->g_rrz + 1;
+        pa.nupd = (unsigned)h->nranks;
+        pa.stride = 2u;
+    }
     if (s.iso)
-        k_keff_tiles<true, false, 1><<<g, kBlock, lds, st>>>(s, h->p, pa);
+        launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
     else
-        k_keff_tiles<false, false, 1><<<g, kBlock, lds, st>>>(s, h->p, pa);
+        launch_tiles<false, false, 1>(s, h->p, pa, tile_threads(), st);
 }
 
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    k_pcg_update_tiles<<<fast_update_blocks(s), kBlock, 0, st>>>(s, rhs, h->inv, h->x, h->r, h->z, h->p, h->ctl,
-                                                                 h->part0, fast_tile_blocks(s), h->part1, h->part2,
-                                                                 it);
+    const bool sh = h->sharded();
+    k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
+        s, rhs, h->inv, h->x, h->r, h->z, h->p, h->ctl, sh ? h->g_pap : h->part0,
+        sh ? (unsigned)h->nranks : fast_tile_blocks(s), h->part1, h->part2, it);
+}
+
+// diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
+void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st)
+{
+    const DevSys &s = h->ds;
+    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->part1, h->part2, fast_update_blocks(s), 1u, 1u, h->hist,
+               abl | 32u};
+    for (int i = 0; i < reps; ++i)
+        launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
 }
 
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
-    k_pcg_check<<<1, kBlock, 0, st>>>(h->ctl, h->part1, h->part2, fast_update_blocks(h->ds), it, h->hist);
+    if (h->sharded())
+        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
+    else
+        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->part1, h->part2, fast_update_blocks(h->ds), 1u, it, h->hist);
+}
+
+void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st)
+{
+    k_fold_pair<<<1, 256, 0, st>>>(a, b, n, out);
+}
+
+void fast_fold_pap(cwf_hip_system *h, hipStream_t st)
+{
+    fold_pair(h->part0, nullptr, fast_tile_blocks(h->ds), h->g_pap + h->rank, st);
+}
+
+void fast_fold_rrz(cwf_hip_system *h, hipStream_t st)
+{
+    fold_pair(h->part1, h->part2, fast_update_blocks(h->ds), h->g_rrz + 2 * h->rank, st);
+}
+
+void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st)
+{
+    if (!h->nsend)
+        return;
+    const uint64_t g = std::min<uint64_t>((h->nsend + 255) / 256, 1024);
+    k_halo_pack<<<(unsigned)g, 256, 0, st>>>(h->send_idx, h->nsend, v, h->sendbuf);
 }
 
 }  // namespace cwf

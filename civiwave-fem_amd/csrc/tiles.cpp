@@ -172,6 +172,11 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out)
     std::vector<uint32_t> cur(out.node_part_off.begin(), out.node_part_off.end() - 1);
     for (uint64_t s = 0; s < total; ++s)
         out.node_part_slot[cur[out.tile_nodes[s]]++] = (uint32_t)s;
+    // node-major partial position of every tile node: the update pass then streams a node's
+    // partials contiguously (part[node_part_off[n] .. node_part_off[n+1]), ascending tile)
+    out.tile_slot.resize(total);
+    for (uint64_t q = 0; q < total; ++q)
+        out.tile_slot[out.node_part_slot[q]] = (uint32_t)q;
     // owner slot = the node's first (lowest-tile) slot: bit 31 of tile_nodes
     for (uint64_t n = 0; n < N; ++n)
         if (out.node_part_off[n + 1] > out.node_part_off[n])

@@ -68,6 +68,17 @@ class StepTelemetryC(C.Structure):
     ]
 
 
+class ShardInfoC(C.Structure):
+    _fields_ = [
+        ("owned_nodes", C.c_uint64), ("local_nodes", C.c_uint64), ("local_elements", C.c_uint64),
+        ("neighbor_count", C.c_uint32), ("reserved", C.c_uint32), ("neighbor_ranks", C.c_void_p),
+        ("send_offsets", C.c_void_p), ("send_nodes", C.c_void_p), ("recv_offsets", C.c_void_p),
+        ("node_global", C.c_void_p), ("element_source", C.c_void_p), ("node_source", C.c_void_p),
+    ]
+
+
+COMM_ID_BYTES = 128
+
 _lib = None
 
 
@@ -115,6 +126,15 @@ def load() -> C.CDLL:
         "cwf_hip_stepper_set_external_force": ([P, P, u64, i32], i32),
         "cwf_hip_stepper_set_warm_start": ([P, i32], i32),
         "cwf_hip_stepper_time": ([P, P, P], i32),
+        "cwf_shard_build": ([P, P, P, i32, i32, P], i32),
+        "cwf_shard_get": ([P, P, P], i32),
+        "cwf_shard_destroy": ([P], None),
+        "cwf_hip_comm_unique_id": ([P], i32),
+        "cwf_hip_comm_create_rccl": ([i32, i32, P, i32, P], i32),
+        "cwf_hip_comm_create_local": ([i32, i32, P], i32),
+        "cwf_hip_comm_destroy": ([P], None),
+        "cwf_hip_system_attach": ([P, P, i32, P], i32),
+        "cwf_hip_solve_pcg_group": ([P, i32, P, P, P, i32, P], i32),
         "cwf_preprocess_tets": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),
     }
     for name, (args, res) in sig.items():

@@ -54,6 +54,21 @@ def kuhn_block(nx: int, ny: int, nz: int, h: float = 1.0) -> TetMesh:
                                   "CORNER": np.array([(nz * B + ny) * A + nx], np.uint32)}, (nx, ny, nz))
 
 
+def kuhn_slab(nx: int, ny: int, nz: int, kc0: int, kc1: int, h: float = 1.0):
+    """Cells k in [kc0, kc1) of the nx*ny*nz Kuhn block (nodes on planes kc0..kc1), numbered
+    compactly but in the global order -> (TetMesh, global node id per sub-mesh node). Elements keep
+    the global (k-slowest) order, so a rank's sub-mesh feeds cwf_shard_build directly."""
+    A, B = nx + 1, ny + 1
+    sub = kuhn_block(nx, ny, kc1 - kc0, h)
+    kk = np.arange(kc0, kc1 + 1, dtype=np.float64).repeat(A * B)
+    sub.coords[:, 2] = kk if h == 1.0 else h * kk  # the same expression kuhn_block uses
+    node_global = np.arange(sub.node_count, dtype=np.uint64) + np.uint64(kc0 * A * B)
+    groups = {k: v for k, v in sub.node_groups.items() if k != "CORNER"}
+    if kc1 == nz:
+        groups["CORNER"] = np.array([((kc1 - kc0) * B + ny) * A + nx], np.uint32)
+    return TetMesh(sub.coords, sub.tets, groups, (nx, ny, kc1 - kc0)), node_global
+
+
 def jitter_and_permute(mesh: TetMesh, h: float, jitter: float = 0.15, seed_jitter: int = 12345,
                        seed_perm: int = 42) -> TetMesh:
     """C4: jitter interior nodes by +-jitter*h and randomly permute node/element order.

@@ -124,25 +124,29 @@ class MatrixFreeSystem:
                    packing.reduction_partials, (packing.offsets, packing.element_indices, packing.local_indices),
                    mode, device, packing.position0)
 
+    def desc(self) -> "_lib.SystemDesc":
+        """The C descriptor over this object's host arrays (kept alive by the object)."""
+        p = _lib.ptr
+        adj = self.adjacency
+        if adj is not None:
+            adj = (np.ascontiguousarray(adj[0], np.uint32), np.ascontiguousarray(adj[1], np.uint32),
+                   np.ascontiguousarray(adj[2], np.uint8))
+        self._keep = adj  # keep the buffers alive across the C calls
+        return _lib.SystemDesc(
+            self.node_count, self.element_count, self.dof_count, p(self.element_connectivity),
+            p(self.element_gradients), p(self.element_volume), p(self.element_material_index),
+            p(self.material_stiffness), self.material_stiffness.size // 36, p(self.lumped_mass), p(self.bc_mask),
+            p(adj[0]) if adj is not None else None,
+            p(adj[1]) if adj is not None else None,
+            p(adj[2]) if adj is not None else None,
+            self.stiffness_scale, self.mass_factor, self.reduction_block, self.reduction_partials, self.mode, 0,
+            p(self.node_coords) if self.node_coords is not None else None)
+
     # -- handle management --------------------------------------------------------------
     def handle(self):
         if self._h is None:
             L = _lib.load()
-            p = _lib.ptr
-            adj = self.adjacency
-            if adj is not None:
-                adj = (np.ascontiguousarray(adj[0], np.uint32), np.ascontiguousarray(adj[1], np.uint32),
-                       np.ascontiguousarray(adj[2], np.uint8))
-            self._keep = adj  # keep the buffers alive across the create call
-            desc = _lib.SystemDesc(
-                self.node_count, self.element_count, self.dof_count, p(self.element_connectivity),
-                p(self.element_gradients), p(self.element_volume), p(self.element_material_index),
-                p(self.material_stiffness), self.material_stiffness.size // 36, p(self.lumped_mass), p(self.bc_mask),
-                p(adj[0]) if adj is not None else None,
-                p(adj[1]) if adj is not None else None,
-                p(adj[2]) if adj is not None else None,
-                self.stiffness_scale, self.mass_factor, self.reduction_block, self.reduction_partials, self.mode, 0,
-                p(self.node_coords) if self.node_coords is not None else None)
+            desc = self.desc()
             h = C.c_void_p()
             st = L.cwf_hip_system_create(C.byref(desc), self.device, C.byref(h))
             if st:

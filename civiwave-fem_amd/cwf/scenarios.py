@@ -63,3 +63,28 @@ def config_case(key: str, max_iterations: int = 2000) -> Case:
                       max_iterations=max_iterations)
     case.name = f"{key}: {c['name']}"
     return case
+
+
+def slab_case_shape(shape, nranks: int, rank: int, h: float = 0.1, max_iterations: int = 2000, **cfg_kw):
+    """Weak-scaling decomposition of an nx*ny*nz block: the global block stacks `nranks` copies along
+    z (nz * nranks cells); rank r owns a contiguous range of node planes and gets the sub-mesh of every
+    cell touching them (its ghost layer). Returns (case over the sub-mesh, global node id per sub-mesh
+    node, rank_node_begin [nranks + 1] in global node ids)."""
+    nx, ny, nz1 = shape
+    nz = nz1 * nranks
+    A, B = nx + 1, ny + 1
+    planes = [(nz + 1) * r // nranks for r in range(nranks + 1)]
+    kc0, kc1 = max(planes[rank] - 1, 0), min(planes[rank + 1], nz)
+    tm, node_global = meshgen.kuhn_slab(nx, ny, nz, kc0, kc1, h)
+    mesh = pack.from_tetmesh(tm)
+    cfg = make_config(max_iterations=max_iterations, **cfg_kw)
+    case = Case(f"kuhn{nx}x{ny}x{nz}/slab{rank}of{nranks}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
+    begin = np.asarray([p * A * B for p in planes], np.uint64)
+    return case, node_global, begin
+
+
+def slab_case(key: str, nranks: int, rank: int, max_iterations: int = 2000):
+    """slab_case_shape for BASELINE config `key` (weak scaling: `key`'s block per rank)."""
+    c = meshgen.CONFIGS[key]
+    return slab_case_shape(c["shape"], nranks, rank, h=c["h"], max_iterations=max_iterations, xi=c["xi"],
+                           w=c["w"], tol=c["tol"])

@@ -204,6 +204,65 @@ int cwf_hip_stepper_set_warm_start(cwf_hip_stepper *st, int enabled);
 int cwf_hip_stepper_time(const cwf_hip_stepper *st, double *current_time, double *time_step);
 
 /* ---------------------------------------------------------------------------------------
+ * Multi-GPU: node-range shards with a ghost element layer (the north
+ * star's "mesh shards ... RCCL all-reduce for the PCG dot products and halo-DOF exchange").
+ * The reference itself is single-device; its src/gpu/sharding.cpp:38-144 (plan_shards) only
+ * splits packed buffers under Vulkan's 2 GiB cap, which HBM handles do not need.
+ * ------------------------------------------------------------------------------------- */
+
+/* Host-only (no GPU needed). Rank `rank` of `nranks` owns global nodes
+ * [rank_node_begin[rank], rank_node_begin[rank+1]). `desc` is the global mesh or any sub-mesh
+ * holding every element that touches an owned node (in ascending global element order);
+ * node_global_ids maps desc node -> global id (NULL = identity). The shard's local system has
+ * the owned nodes first (ascending global id), then the ghosts grouped by owner rank. */
+typedef struct cwf_shard cwf_shard;
+typedef struct cwf_shard_info
+{
+    uint64_t owned_nodes;          /* local ids [0, owned_nodes) */
+    uint64_t local_nodes;          /* owned + ghost */
+    uint64_t local_elements;
+    uint32_t neighbor_count;
+    uint32_t reserved;
+    const int32_t *neighbor_ranks; /* [neighbor_count], ascending */
+    const uint64_t *send_offsets;  /* [neighbor_count + 1] into send_nodes */
+    const uint32_t *send_nodes;    /* owned local ids each neighbour needs, ascending global id */
+    const uint64_t *recv_offsets;  /* [neighbor_count + 1]: ghosts of neighbour k are local ids
+                                      owned_nodes + [recv_offsets[k], recv_offsets[k+1]) */
+    const uint64_t *node_global;   /* [local_nodes] global node id */
+    const uint64_t *element_source; /* [local_elements] element index in the input desc */
+    const uint64_t *node_source;    /* [local_nodes] node index in the input desc */
+} cwf_shard_info;
+
+int cwf_shard_build(const cwf_system_desc *desc, const uint64_t *node_global_ids, const uint64_t *rank_node_begin,
+                    int32_t nranks, int32_t rank, cwf_shard **out);
+/* local_desc: the shard's local system (arrays owned by the shard; adjacency NULL) */
+int cwf_shard_get(const cwf_shard *shard, cwf_system_desc *local_desc, cwf_shard_info *info);
+void cwf_shard_destroy(cwf_shard *shard);
+
+/* Communicators. RCCL: one process per GPU (ncclCommInitRank; the 128-byte unique id is made by
+ * rank 0 and broadcast by the caller, e.g. over torch.distributed). LOCAL: every rank's handle
+ * lives in this process on one device (exchanges are device copies on one shared stream); it runs
+ * the identical sharded kernels and exists to test the decomposition on a single GPU. */
+#define CWF_COMM_ID_BYTES 128
+typedef struct cwf_hip_comm cwf_hip_comm;
+int cwf_hip_comm_unique_id(uint8_t *id);
+int cwf_hip_comm_create_rccl(int32_t nranks, int32_t rank, const uint8_t *id, int device, cwf_hip_comm **out);
+int cwf_hip_comm_create_local(int32_t nranks, int device, cwf_hip_comm **out);
+void cwf_hip_comm_destroy(cwf_hip_comm *comm); /* after every attached handle is destroyed */
+
+/* Make `h` (created from a shard's local desc) rank `rank` of `comm` with the shard's halo plan.
+ * Afterwards solve_pcg / stepper_step are collective: scalars are all-gathered and folded in rank
+ * order on every rank (identical control flow everywhere), ghost DOFs are refreshed by the halo
+ * exchange, and vectors are local [3 * local_nodes] with only the owned rows meaningful on output
+ * (x is halo-consistent). FAST mode only. */
+int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *comm, int32_t rank, const cwf_shard_info *plan);
+/* solve_pcg over all ranks of a LOCAL communicator (members in rank order); for RCCL call
+ * cwf_hip_solve_pcg on each rank's handle. Telemetry is identical on every rank. */
+int cwf_hip_solve_pcg_group(cwf_hip_system *const *members, int32_t count, const float *const *rhs,
+                            const cwf_pcg_settings *settings, float *const *x_inout, int ptr_kind,
+                            cwf_pcg_telemetry *telemetry);
+
+/* ---------------------------------------------------------------------------------------
  * Host-side preprocessing (no GPU needed): tet gradients/volume/lumped mass/CSR exactly as
  * mesh::pre::run + pack::build_packed_buffers (preprocess.cpp:268-405, pack.cpp:41-200).
  * Outputs are caller-allocated: grads[E*24], volume[E], mass[N] (f64) and mass32[N],

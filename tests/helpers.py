@@ -37,3 +37,22 @@ def kuhn16_reference_case():
     i = np.arange(D)
     rhs = (ez[i // 3] * (i % 3 == 2).astype(np.float32)).astype(np.float32)  # float * bool (keeps -0.0)
     return case, rhs
+
+
+def shard_oracle(sh, case, sK, sM):
+    """oracle System over a shard's local arrays (CSR ascending element per node)."""
+    E, N = sh.local_elements, sh.local_nodes
+    conn = sh.connectivity.reshape(E, 8)[:, :4].astype(np.int64)
+    inc_node = conn.reshape(-1)
+    order = np.argsort(inc_node, kind="stable")  # ascending element within a node
+    offsets = np.zeros(N + 1, np.uint32)
+    np.add.at(offsets, inc_node + 1, 1)
+    offsets = np.cumsum(offsets).astype(np.uint32)
+    elem = (order // 4).astype(np.uint32)
+    loc = (order % 4).astype(np.uint8)
+    src = sh.node_source.astype(np.int64)
+    P = case.packing
+    packed = O.Packed(N, E, sh.connectivity, sh.gradients, sh.volume, sh.material_index, P.lumped_mass64[src],
+                      sh.lumped_mass, offsets, elem, loc)
+    stiff = np.concatenate([np.asarray(m.stiffness, np.float64).reshape(-1) for m in case.materials])
+    return O.System(packed, stiff, sh.bc_mask, sK, sM, 256)

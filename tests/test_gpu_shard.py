@@ -1,0 +1,82 @@
+"""Sharded FAST PCG on one GPU (LOCAL communicator: every rank's handle in this process, exchanges
+as device copies). The kernels, the per-iteration schedule (p.Ap all-gather, r.r / r.z all-gather,
+z halo) and the ghost-row handling are the ones RCCL ranks run; only the transport differs.
+Tolerance: the sharded solve must converge to the single-process oracle solution within 1e-4
+relative (the solve guarantees |r| <= 1e-6 |rhs|) in the same iteration count +-10%."""
+import numpy as np
+import pytest
+
+from cwf import _lib, pcg, scenarios, shard
+from helpers import oracle_system
+
+pytestmark = pytest.mark.gpu
+
+
+def _sharded_solve(glob, nranks, rel_tol=1e-6, max_iterations=800, from_slabs=None):
+    sK, sM = glob.scalars()
+    P = glob.packing
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs = [], [], [], []
+    for r in range(nranks):
+        if from_slabs:
+            case, node_global, begin = scenarios.slab_case_shape(from_slabs, nranks, r, tol=rel_tol)
+            src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
+            sh = shard.build_shard(src, begin, r, node_global)
+            rhs.append(sh.local_dofs(case.static_rhs()))
+        else:
+            src = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_FAST)
+            sh = shard.build_shard(src, shard.slab_ranges(P.node_count, nranks), r)
+            rhs.append(sh.local_dofs(glob.static_rhs()))
+        s = sh.system(glob.materials, sK, sM)
+        comm.attach(s, sh)
+        systems.append(s)
+        shards.append(sh)
+        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    tel = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(max_iterations, rel_tol), xs).value()
+    x = np.zeros((P.node_count, 3), np.float32)
+    for sh, xl in zip(shards, xs):
+        x[sh.node_global[: sh.owned_nodes].astype(np.int64)] = xl.reshape(-1, 3)[: sh.owned_nodes]
+        # x is halo-consistent on return: ghost rows carry the owners' values
+    for sh, xl in zip(shards, xs):
+        assert np.array_equal(xl.reshape(-1, 3)[sh.owned_nodes:], x[sh.node_global[sh.owned_nodes:].astype(np.int64)])
+    comm.close()
+    return tel, x.reshape(-1)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_local_sharded_solve_matches_oracle(nranks):
+    glob = scenarios.block_case(10, 6, 12, h=0.1, tol=1e-6)
+    sK, sM = glob.scalars()
+    tel, x = _sharded_solve(glob, nranks)
+    ref = oracle_system(glob.packing, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 800, 1e-6)
+    assert tel.converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    n_ref = ref["telemetry"].iterations
+    assert abs(tel.iterations - n_ref) <= max(3, n_ref // 10)
+
+
+def test_local_sharded_from_slab_submeshes():
+    """The bench's decomposition: every rank builds only its slab sub-mesh (+ ghost layer)."""
+    nranks = 3
+    shape = (8, 5, 4)
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=1e-6)
+    sK, sM = glob.scalars()
+    tel, x = _sharded_solve(glob, nranks, from_slabs=shape)
+    ref = oracle_system(glob.packing, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 800, 1e-6)
+    assert tel.converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+
+
+def test_local_group_requires_group_call():
+    glob = scenarios.block_case(4, 3, 4, h=0.1)
+    sK, sM = glob.scalars()
+    P = glob.packing
+    comm = shard.Comm.local(2)
+    src = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_FAST)
+    sh = shard.build_shard(src, shard.slab_ranges(P.node_count, 2), 0)
+    s = sh.system(glob.materials, sK, sM)
+    comm.attach(s, sh)
+    rhs = sh.local_dofs(glob.static_rhs())
+    e = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, 1e-6), pcg.PcgVectors(np.zeros_like(rhs), None))
+    assert not e.has_value() and "solve_pcg_group" in e.error().message
+    comm.close()

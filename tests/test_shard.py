@@ -1,0 +1,109 @@
+"""Node-range shards (cwf_shard_build) on the CPU: partition invariants, halo
+plan symmetry, sub-mesh input, and that the oracle's parity K_eff on every shard reproduces the
+global K_eff on the owned rows bit for bit (the complete-rows property the sharded solver relies on)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from cwf import pcg, scenarios, shard
+from cwf import _lib
+
+from helpers import assert_bitwise, shard_oracle as _local_oracle
+
+
+def _global_case():
+    return scenarios.block_case(5, 4, 7, h=0.1)
+
+
+def _system(case, mode=_lib.MODE_FAST):
+    sK, sM = case.scalars()
+    return pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=mode)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 5])
+def test_partition_invariants(nranks):
+    case = _global_case()
+    P = case.packing
+    sysm = _system(case)
+    begin = shard.slab_ranges(P.node_count, nranks)
+    shards = [shard.build_shard(sysm, begin, r) for r in range(nranks)]
+    conn = P.connectivity.reshape(-1, 8)[:, :4].astype(np.int64)
+    owned_all = np.concatenate([s.node_global[: s.owned_nodes] for s in shards])
+    assert np.array_equal(np.sort(owned_all), np.arange(P.node_count))
+    for s in shards:
+        lo, hi = int(begin[s.rank]), int(begin[s.rank + 1])
+        own = s.node_global[: s.owned_nodes].astype(np.int64)
+        assert np.array_equal(own, np.arange(lo, hi))  # owned first, ascending global id
+        touches = np.any((conn >= lo) & (conn < hi), axis=1)
+        assert np.array_equal(s.element_source, np.nonzero(touches)[0])  # ascending global element order
+        ghosts = s.node_global[s.owned_nodes:].astype(np.int64)
+        want = np.setdiff1d(np.unique(conn[touches]), own)
+        assert np.array_equal(np.sort(ghosts), want)
+        owners = np.searchsorted(begin.astype(np.int64), ghosts, side="right") - 1
+        assert np.all(np.diff(owners) >= 0)  # grouped by owner rank
+        for k, q in enumerate(s.neighbor_ranks):
+            a, b = int(s.recv_offsets[k]), int(s.recv_offsets[k + 1])
+            assert np.all(owners[a:b] == q)
+        # local connectivity maps back to the global one
+        lc = s.connectivity.reshape(-1, 8)
+        assert np.all(lc[:, 4:] == 0xFFFFFFFF)
+        assert np.array_equal(s.node_global[lc[:, :4].astype(np.int64)].astype(np.int64), conn[touches])
+    # halo symmetry: r's send list to q == q's ghosts from r (same order)
+    for s in shards:
+        for k, q in enumerate(s.neighbor_ranks):
+            t = shards[q]
+            j = list(t.neighbor_ranks).index(s.rank)
+            sent = s.node_global[s.send_nodes[int(s.send_offsets[k]):int(s.send_offsets[k + 1])].astype(np.int64)]
+            recv = t.node_global[t.owned_nodes + int(t.recv_offsets[j]): t.owned_nodes + int(t.recv_offsets[j + 1])]
+            assert np.array_equal(sent, recv)
+
+
+def test_submesh_input_matches_global():
+    """The bench feeds every rank its own slab sub-mesh (scenarios.slab_case); the shard must equal the
+    one cut from the global mesh."""
+    nranks = 3
+    glob = scenarios.block_case(4, 3, 3 * nranks, h=0.1)
+    gsys = _system(glob)
+    for r in range(nranks):
+        sub, node_global, begin = scenarios.slab_case_shape((4, 3, 3), nranks, r)
+        a = shard.build_shard(gsys, begin, r)
+        b = shard.build_shard(_system(sub), begin, r, node_global)
+        assert a.owned_nodes == b.owned_nodes and a.local_nodes == b.local_nodes
+        assert np.array_equal(a.node_global, b.node_global)
+        assert np.array_equal(a.connectivity, b.connectivity)
+        assert np.array_equal(a.neighbor_ranks, b.neighbor_ranks)
+        assert np.array_equal(a.send_nodes, b.send_nodes)
+        assert_bitwise(a.gradients, b.gradients, "gradients")
+        assert_bitwise(a.volume, b.volume, "volume")
+        assert_bitwise(a.lumped_mass[: a.owned_nodes], b.lumped_mass[: b.owned_nodes], "owned masses")
+        assert np.array_equal(a.bc_mask, b.bc_mask)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_shard_rows_bitwise(nranks):
+    case = _global_case()
+    P = case.packing
+    sK, sM = case.scalars()
+    sysm = _system(case)
+    ref = O.System(O.Packed(P.node_count, P.element_count, P.connectivity, P.gradients, P.volume, P.material_index,
+                            P.lumped_mass64, P.lumped_mass, P.offsets, P.element_indices, P.local_indices),
+                   np.concatenate([np.asarray(m.stiffness, np.float64).reshape(-1) for m in case.materials]),
+                   P.bc_mask, sK, sM, 256)
+    x = ((np.arange(P.dof_count, dtype=np.uint64) * 2654435761) % 1000).astype(np.float32) / np.float32(1000.0)
+    y = ref.apply_keff(x)
+    begin = shard.slab_ranges(P.node_count, nranks)
+    for r in range(nranks):
+        s = shard.build_shard(sysm, begin, r)
+        loc = _local_oracle(s, case, sK, sM)
+        yl = loc.apply_keff(s.local_dofs(x))
+        own = s.node_global[: s.owned_nodes].astype(np.int64)
+        assert_bitwise(yl[: 3 * s.owned_nodes], y.reshape(-1, 3)[own].reshape(-1), f"rank {r} owned rows")
+
+
+def test_shard_errors():
+    case = _global_case()
+    sysm = _system(case)
+    with pytest.raises(RuntimeError, match="outside every rank"):
+        shard.build_shard(sysm, np.array([0, 10], np.uint64), 0)
+    with pytest.raises(RuntimeError, match="rank out of range"):
+        shard.build_shard(sysm, shard.slab_ranges(case.packing.node_count, 2), 2)
