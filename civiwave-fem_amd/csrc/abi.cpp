@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
@@ -201,13 +202,11 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (uint64_t i = 0; i < nb; ++i)
         {
             hipEvent_t e0 = h->timing ? h->ev[2 * i] : nullptr, e1 = h->timing ? h->ev[2 * i + 1] : nullptr;
-            if (sharded)
+            if (fast)
             {
-                if (int e = sharded_pcg_iteration(g, rhs, (unsigned)(enq + i), e0, e1))
+                if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
                     return e;
             }
-            else if (fast)
-                fast_pcg_iteration(h, rhs[0], (unsigned)(enq + i), st, e0, e1);
             else
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
@@ -483,11 +482,48 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
         }
         DevTiles &t = s.t;
-        uint4 *planes;
-        if (int st = dalloc(h, &planes, 3 * E))
-            return bail(st);
-        for (int q = 0; q < 3; ++q)
-            HIPTRY(h, hipMemcpy(planes + q * E, ht.planes[q].data(), E * sizeof(uint4), hipMemcpyHostToDevice));
+        // GEO: stream 8-B corner ids + tile-node coordinates and recompute gradients/volume on the fly,
+        // when the desc carries coordinates that reproduce its gradients (CWF_GEO=0 forces the records)
+        const char *ge = getenv("CWF_GEO");
+        t.geo = (!ge || ge[0] != '0') && !ht.tcoord[0].empty() && geometry_matches(d) ? 1 : 0;
+        {
+            const char *fo = getenv("CWF_TILE_FOLD");
+            t.acc = fo && fo[0] == 'a' ? 1 : 0;
+            const char *pp = getenv("CWF_TILE_PIPE");
+            t.pipe = t.geo && !t.acc && !(pp && pp[0] == '0') ? 1 : 0;
+            uint32_t deg = 1;
+            for (size_t q = 0; q + 1 < ht.csr_off.size(); ++q)
+                deg = std::max(deg, ht.csr_off[q + 1] - ht.csr_off[q]);
+            while ((1u << t.deg_log2) < deg)
+                ++t.deg_log2;
+        }
+        if (getenv("CWF_VERBOSE"))
+            fprintf(stderr, "[cwf] tiles: %u tiles, %zu tile nodes (%.3f per node), max %u nodes/tile, %s records\n",
+                    ht.ntiles, ht.tile_nodes.size(), N ? (double)ht.tile_nodes.size() / (double)N : 0.0,
+                    ht.max_tile_nodes, t.geo ? "8-B geometric" : "48-B gradient");
+        if (t.geo)
+        {
+            uint2 *eid;
+            float *tc;
+            if (int st = upload(h, &eid, ht.eid.data(), E))
+                return bail(st);
+            const size_t T3 = ht.tile_nodes.size();
+            if (int st = dalloc(h, &tc, 3 * T3))
+                return bail(st);
+            for (int q = 0; q < 3; ++q)
+                HIPTRY(h, hipMemcpy(tc + q * T3, ht.tcoord[q].data(), T3 * sizeof(float), hipMemcpyHostToDevice));
+            t.eid = eid;
+            t.tcoord = tc;
+        }
+        else
+        {
+            uint4 *planes;
+            if (int st = dalloc(h, &planes, 3 * E))
+                return bail(st);
+            for (int q = 0; q < 3; ++q)
+                HIPTRY(h, hipMemcpy(planes + q * E, ht.planes[q].data(), E * sizeof(uint4), hipMemcpyHostToDevice));
+            t.planes = planes;
+        }
         if (!ht.mat.empty())
         {
             uint32_t *tm;
@@ -495,14 +531,20 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 return bail(st);
             t.mat = tm;
         }
-        // packed per-tile header and per-tile-node record: one dwordx4 load each
-        std::vector<uint4> hdr(ht.ntiles), tnode(ht.tile_nodes.size());
+        // per-tile header (one scalar dwordx4 load) and 8-B tile-node records {node|owner, csr range};
+        // partials are tile-major (a tile's block is one contiguous store) and the update pass gathers a
+        // node's slots through part_slot
+        std::vector<uint4> hdr(ht.ntiles);
+        std::vector<uint2> tnode(ht.tile_nodes.size());
         for (uint32_t k = 0; k < ht.ntiles; ++k)
-            hdr[k] = uint4{ht.tile_elem_off[k], ht.tile_elem_off[k + 1] - ht.tile_elem_off[k], ht.tile_node_off[k],
-                           ht.tile_node_off[k + 1] - ht.tile_node_off[k]};
-        for (size_t q = 0; q < tnode.size(); ++q)
-            tnode[q] = uint4{ht.tile_nodes[q], ht.tile_slot[q], ht.csr_off[q], ht.csr_off[q + 1]};
-        uint4 *dh, *dtn;
+        {
+            const uint32_t e0 = ht.tile_elem_off[k], nb = ht.tile_node_off[k], nb1 = ht.tile_node_off[k + 1];
+            hdr[k] = uint4{e0, ht.tile_elem_off[k + 1] - e0, nb, nb1 - nb};
+            for (uint32_t q = nb; q < nb1; ++q)
+                tnode[q] = uint2{ht.tile_nodes[q], (ht.csr_off[q] - 4u * e0) | ((ht.csr_off[q + 1] - 4u * e0) << 16)};
+        }
+        uint4 *dh;
+        uint2 *dtn;
         uint32_t *npo;
         uint16_t *ce;
         float *part;
@@ -510,22 +552,28 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(st);
         if (int st = upload(h, &dtn, tnode.data(), tnode.size()))
             return bail(st);
+        ht.csr_ent.resize(ht.csr_ent.size() + 8, 0);  // the pipelined kernel reads a tile's entries as 16-B words
         if (int st = upload(h, &ce, ht.csr_ent.data(), ht.csr_ent.size()))
             return bail(st);
         if (int st = upload(h, &npo, ht.node_part_off.data(), ht.node_part_off.size()))
             return bail(st);
+        uint32_t *ps;
+        if (int st = upload(h, &ps, ht.node_part_slot.data(), ht.node_part_slot.size()))
+            return bail(st);
+        t.part_slot = ps;
         if (int st = dalloc(h, &part, 3 * ht.tile_nodes.size()))
             return bail(st);
         t.ntiles = ht.ntiles;
         t.max_tile_nodes = ht.max_tile_nodes;
         t.total_tile_nodes = (uint32_t)ht.tile_nodes.size();
         t.E = (uint32_t)E;
-        t.planes = planes;
         t.hdr = dh;
         t.tnode = dtn;
         t.csr_ent = ce;
         t.node_part_off = npo;
         t.part = part;
+        if (t.pipe)
+            t.pipe_grid = fast_pipe_grid(s);
     }
     // solver scratch
     const uint64_t D = 3 * N;
@@ -534,9 +582,12 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(st);
     if (int st = dalloc(h, &h->inv, 9 * N))
         return bail(st);
+    if (int st = dalloc(h, &h->inv6, 6 * N))
+        return bail(st);
     const uint64_t chunks = (D + d->reduction_block - 1) / d->reduction_block;
     h->part_cap = std::max<uint64_t>(
-        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), (uint64_t)s.t.ntiles, 1});
+        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), (uint64_t)s.t.ntiles,
+         (uint64_t)s.t.pipe_grid, 1});
     if (int st = dalloc(h, &h->part0, h->part_cap))
         return bail(st);
     if (int st = dalloc(h, &h->part1, h->part_cap))
@@ -547,8 +598,15 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         return bail(st);
     if (int st = dalloc(h, &h->scal, 8))
         return bail(st);
+    // folded per-rank scalars (one rank until cwf_hip_system_attach): p.Ap, {r.r, r.z}, {rhs.rhs, r0.r0}, r0.z0
+    if (int st = dalloc(h, &h->g_pap, 6))
+        return bail(st);
+    h->g_rrz = h->g_pap + 1;
+    h->g_init = h->g_rrz + 2;
+    h->g_rz0 = h->g_init + 2;
     HIPTRY(h, hipMemset(h->x, 0, D * sizeof(float)));
     HIPTRY(h, hipMemset(h->ctl, 0, sizeof(Ctl)));
+    HIPTRY(h, hipMemset(h->g_pap, 0, 6 * sizeof(double)));
     HIPTRY(h, hipDeviceSynchronize());
     *out = h;
     return 0;

@@ -179,7 +179,7 @@ int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*ve
 int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
 {
     for (cwf_hip_system *h : g)
-        parity_block_jacobi(h, h->inv, h->stream);
+        fast_block_inverse(h, h->stream);
     if (int st = comm_halo(g, &cwf_hip_system::x))  // warm start: ghost x from the owners
         return st;
     for (size_t i = 0; i < g.size(); ++i)
@@ -217,8 +217,9 @@ int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<c
     return 0;
 }
 
-int sharded_pcg_iteration(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, unsigned it,
-                          hipEvent_t e0, hipEvent_t e1)
+// one FAST PCG iteration of every member (a single unsharded handle is the group {h} with one rank)
+int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
+                             unsigned it, hipEvent_t e0, hipEvent_t e1)
 {
     if (e0)
         (void)hipEventRecord(e0, g[0]->stream);
@@ -237,7 +238,7 @@ int sharded_pcg_iteration(const std::vector<cwf_hip_system *> &g, const std::vec
     }
     if (int st = comm_allgather(g, &cwf_hip_system::g_rrz, 2))
         return st;
-    return comm_halo(g, &cwf_hip_system::z);
+    return g[0]->sharded() ? comm_halo(g, &cwf_hip_system::z) : 0;
 }
 
 }  // namespace cwf

@@ -23,7 +23,7 @@ namespace cwf
 
 // FAST-mode element tiles (tiles.cpp): element-centric K_eff with deterministic LDS folds
 constexpr int kTileElems = 512;      // elements per tile (= per 256-thread workgroup)
-constexpr int kMaxTileNodes = 2048;  // distinct nodes per tile (u16 local corner ids, LDS bound)
+constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two node slots per thread)
 
 struct DevTiles
 {
@@ -31,14 +31,23 @@ struct DevTiles
     uint32_t max_tile_nodes = 0;
     uint32_t total_tile_nodes = 0;
     uint32_t E = 0;
+    int geo = 0;  // 1: geometry recomputed from tile-node coordinates (eid + tcoord), 0: 48-B planes
+    int acc = 0;  // 1: fixed-point LDS accumulation (no local CSR fold)
+    int pipe = 0; // 1: persistent software-pipelined tiles kernel (GEO, CSR fold)
+    uint32_t pipe_grid = 0;  // its resident grid (occupancy x CUs, whole XCD groups)
+    uint32_t deg_log2 = 0;  // ceil(log2(largest number of (element, corner) pairs of one tile node))
     // [3][E] 48-B records: {idx01, idx23, g0x, g0y} {g0z, g1x, g1y, g1z} {g2x, g2y, g2z, vol};
     // g3 = -(g0 + g1 + g2) (partition of unity of the linear tet)
     const uint4 *planes = nullptr;
+    const uint2 *eid = nullptr;      // [E] {idx01, idx23} local corner ids (GEO)
+    const float *tcoord = nullptr;   // [3][total] tile-relative node coordinates, tile-major (GEO)
     const uint32_t *mat = nullptr;            // [E] material per element (tile order), NULL when M == 1
     const uint4 *hdr = nullptr;               // [ntiles] {first element, #elements, first tile node, #nodes}
-    const uint4 *tnode = nullptr;             // [total] {global node | owner bit 31, partial slot, csr begin, csr end}
+    const uint2 *tnode = nullptr;             // [total] {local node | owner bit 31, csr begin | csr end << 16}
+                                              // (csr range relative to the tile's first entry 4*e0)
     const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
-    const uint32_t *node_part_off = nullptr;  // [N+1] node-major partial ranges
+    const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile)
+    const uint32_t *part_slot = nullptr;      // [total] partial index of each of those slots
     float *part = nullptr;                    // [3*total] tile-node partial sums, node-major (scratch)
 };
 
@@ -50,9 +59,14 @@ struct HostTiles
     std::vector<uint32_t> tile_elem_off, tile_node_off, tile_nodes, csr_off, node_part_off, node_part_slot,
         tile_slot;
     std::vector<uint16_t> csr_ent;
+    std::vector<uint2> eid;        // [E] local corner ids
+    std::vector<float> tcoord[3];  // [total] tile-relative coordinates (when node_coords are given)
 };
 
 int build_tiles(const cwf_system_desc *d, HostTiles &out);
+// true when the supplied gradients / volumes are those of the supplied node coordinates (so FAST may
+// recompute them on the fly instead of streaming them)
+bool geometry_matches(const cwf_system_desc *d);
 
 struct DevSys
 {
@@ -109,7 +123,8 @@ struct cwf_hip_system
     uint64_t bytes = 0;
     // solver scratch (f32 dofs) and partials
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
-    float *inv = nullptr;  // block Jacobi [9N]
+    float *inv = nullptr;   // block Jacobi [9N]
+    float *inv6 = nullptr;  // FAST: symmetric block inverse packed [6N]
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
     uint64_t part_cap = 0;
     cwf::Ctl *ctl = nullptr;       // device
@@ -187,14 +202,13 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
 unsigned fast_tile_blocks(const DevSys &s);
+unsigned fast_pipe_grid(const DevSys &s);
 unsigned fast_update_blocks(const DevSys &s);
-void fast_pcg_iteration(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr,
-                        hipEvent_t e1 = nullptr);
-
 // sharded FAST PCG (comm.cpp orchestrates, spmv_tiles.hip / kernels_fast.hip launch)
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> g_pap[rank]
 void fast_fold_rrz(cwf_hip_system *h, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
 void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st);
+void fast_block_inverse(cwf_hip_system *h, hipStream_t st);  // parity BJ, symmetrised + packed to inv6
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st);
 void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count,
                                uint32_t stride, double rel_tol, hipStream_t st);
@@ -203,8 +217,8 @@ void fast_rho_from(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStr
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);
 int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec);
 int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
-int sharded_pcg_iteration(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, unsigned it,
-                          hipEvent_t e0, hipEvent_t e1);
+int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
+                             unsigned it, hipEvent_t e0, hipEvent_t e1);
 
 // ---- stepper.hip ----
 void stepper_predictor(uint32_t D, const float *u, const float *v, const float *a, float *up, float *vp, double dt,

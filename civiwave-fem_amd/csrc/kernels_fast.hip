@@ -155,7 +155,7 @@ void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStrea
 {
     const DevSys &s = h->ds;
     const uint32_t nbD = fast_dot_blocks(s.D);
-    parity_block_jacobi(h, h->inv, st);
+    fast_block_inverse(h, st);
     fast_keff(h, h->x, h->Ap, true, nullptr, nullptr, st);
     launch_init_residual(h, rhs, st);  // r = rhs - Ap, enforce (pure f32 ops, shared with parity)
     fast_dot(rhs, rhs, nullptr, s.D, h->part0, nullptr, st);
@@ -177,19 +177,6 @@ void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const dou
 void fast_rho_from(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st)
 {
     k_fast_rho<<<1, kBlock, 0, st>>>(h->ctl, p_rz, count);
-}
-
-// one iteration = 2 kernels: K_eff tiles (+ beta/convergence of the previous update + p-update)
-// and the fused update (+ alpha)
-void fast_pcg_iteration(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st, hipEvent_t e0,
-                        hipEvent_t e1)
-{
-    if (e0)
-        (void)hipEventRecord(e0, st);
-    fast_tiles_pcg(h, it, st);
-    if (e1)
-        (void)hipEventRecord(e1, st);
-    fast_update_pcg(h, rhs, it, st);
 }
 
 }  // namespace cwf

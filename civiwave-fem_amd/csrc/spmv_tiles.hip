@@ -28,7 +28,7 @@ namespace
 {
 constexpr int kMaxM = 16;
 constexpr int kUpdThreads = 1024;
-constexpr unsigned kMaxUpdateBlocks = 256;
+constexpr unsigned kMaxUpdateBlocks = 2048;  // 2 resident per CU; shares folded once by k_fold_pair
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -57,8 +57,21 @@ template <int NT>
 __device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigned count, double *red,
                                            unsigned stride = 1)
 {
+    // thread t sums p[t], p[t + NT], ... in that order; 8 loads are issued before their adds so a long
+    // fold costs count / (8 NT) memory round trips instead of count / NT
     double v = 0.0;
-    for (unsigned i = threadIdx.x; i < count; i += NT)
+    unsigned i = threadIdx.x;
+    for (; i + 7u * NT < count; i += 8u * NT)
+    {
+        double q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            q[u] = p[(size_t)(i + u * NT) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v += q[u];
+    }
+    for (; i < count; i += NT)
         v += p[(size_t)i * stride];
     return block_sum<NT>(v, red);
 }
@@ -174,27 +187,15 @@ __device__ __forceinline__ void gather_node(const DevSys &s, const float *__rest
     }
 }
 
-// strain -> stress -> 12 nodal forces of one tet (48-B record q0..q2, corner values from LDS), scaled by
-// V s_K and stored to LDS as f[12][kTileElems] (fp32 counterpart of pcg.cpp:140-220)
+// strain -> stress -> 12 nodal forces of one tet from its corner gradients g[12] (corner-major xyz), its
+// local corner ids and V s_K; corner values from LDS, forces stored to LDS as f[12][kTileElems]
+// (fp32 counterpart of pcg.cpp:140-220)
 template <bool ISO>
-__device__ __forceinline__ void element_forces(const DevSys &s, uint4 q0, uint4 q1, uint4 q2, uint32_t mi, uint32_t j,
-                                               const float *sp, uint32_t ms, const float *dtab, float sK, float *sf)
+__device__ __forceinline__ void element_force_values(const DevSys &s, const float g[12], const uint32_t li[4], float vol,
+                                                     uint32_t mi, const float *sp, uint32_t ms, const float *dtab,
+                                                     float f[12])
 {
     constexpr int kTab = ISO ? 12 : 36;
-    float g[12];
-    g[0] = __uint_as_float(q0.z);
-    g[1] = __uint_as_float(q0.w);
-    g[2] = __uint_as_float(q1.x);
-    g[3] = __uint_as_float(q1.y);
-    g[4] = __uint_as_float(q1.z);
-    g[5] = __uint_as_float(q1.w);
-    g[6] = __uint_as_float(q2.x);
-    g[7] = __uint_as_float(q2.y);
-    g[8] = __uint_as_float(q2.z);
-    g[9] = -(g[0] + g[3] + g[6]);
-    g[10] = -(g[1] + g[4] + g[7]);
-    g[11] = -(g[2] + g[5] + g[8]);
-    const uint32_t li[4] = {q0.x & 0xffffu, q0.x >> 16, q0.y & 0xffffu, q0.y >> 16};
     float eps[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -218,15 +219,92 @@ __device__ __forceinline__ void element_forces(const DevSys &s, uint4 q0, uint4 
             tab[t] = (float)s.dmat[36u * mi + dsrc(ISO, t)];
         stress_f32<ISO>(tab, eps, sig);
     }
-    const float vol = __uint_as_float(q2.w) * sK;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
     {
         const float ax = g[3 * a], ay = g[3 * a + 1], az = g[3 * a + 2];
-        sf[(3 * a + 0) * kTileElems + j] = vol * fmaf(az, sig[5], fmaf(ay, sig[3], ax * sig[0]));
-        sf[(3 * a + 1) * kTileElems + j] = vol * fmaf(az, sig[4], fmaf(ax, sig[3], ay * sig[1]));
-        sf[(3 * a + 2) * kTileElems + j] = vol * fmaf(ax, sig[5], fmaf(ay, sig[4], az * sig[2]));
+        f[3 * a + 0] = vol * fmaf(az, sig[5], fmaf(ay, sig[3], ax * sig[0]));
+        f[3 * a + 1] = vol * fmaf(az, sig[4], fmaf(ax, sig[3], ay * sig[1]));
+        f[3 * a + 2] = vol * fmaf(ax, sig[5], fmaf(ay, sig[4], az * sig[2]));
     }
+}
+
+template <bool ISO>
+__device__ __forceinline__ void element_forces(const DevSys &s, const float g[12], const uint32_t li[4], float vol,
+                                               uint32_t mi, uint32_t j, const float *sp, uint32_t ms,
+                                               const float *dtab, float *sf)
+{
+    float f[12];
+    element_force_values<ISO>(s, g, li, vol, mi, sp, ms, dtab, f);
+#pragma unroll
+    for (int c = 0; c < 12; ++c)
+        sf[c * kTileElems + j] = f[c];
+}
+
+// 48-B record {idx01, idx23, g0x, g0y}{g0z g1x g1y g1z}{g2x g2y g2z vol}: gradients as stored
+__device__ __forceinline__ void record_geometry(uint4 q0, uint4 q1, uint4 q2, float g[12], uint32_t li[4], float *vol)
+{
+    g[0] = __uint_as_float(q0.z);
+    g[1] = __uint_as_float(q0.w);
+    g[2] = __uint_as_float(q1.x);
+    g[3] = __uint_as_float(q1.y);
+    g[4] = __uint_as_float(q1.z);
+    g[5] = __uint_as_float(q1.w);
+    g[6] = __uint_as_float(q2.x);
+    g[7] = __uint_as_float(q2.y);
+    g[8] = __uint_as_float(q2.z);
+    g[9] = -(g[0] + g[3] + g[6]);
+    g[10] = -(g[1] + g[4] + g[7]);
+    g[11] = -(g[2] + g[5] + g[8]);
+    li[0] = q0.x & 0xffffu;
+    li[1] = q0.x >> 16;
+    li[2] = q0.y & 0xffffu;
+    li[3] = q0.y >> 16;
+    *vol = __uint_as_float(q2.w);
+}
+
+// on-the-fly geometry of a linear tet from its corner coordinates (tile-relative f32, staged in LDS):
+// with edge columns c_k = x_k - x_0, the rows of [c1 c2 c3]^-1 are the gradients of N_1..N_3
+// (r1 = c2 x c3 / det, r2 = c3 x c1 / det, r3 = c1 x c2 / det), grad N_0 = -(r1 + r2 + r3) and
+// V = |det| / 6 -- the quantities preprocess.cpp:284-379 tabulates, recomputed instead of streamed
+__device__ __forceinline__ void coord_geometry(uint2 id, const float *sx, uint32_t ms, float g[12], uint32_t li[4],
+                                               float *vol)
+{
+    li[0] = id.x & 0xffffu;
+    li[1] = id.x >> 16;
+    li[2] = id.y & 0xffffu;
+    li[3] = id.y >> 16;
+    float c[3][3];  // c[k] = x_{k+1} - x_0
+    const float x0 = sx[li[0]], y0 = sx[ms + li[0]], z0 = sx[2 * ms + li[0]];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        c[k][0] = sx[li[k + 1]] - x0;
+        c[k][1] = sx[ms + li[k + 1]] - y0;
+        c[k][2] = sx[2 * ms + li[k + 1]] - z0;
+    }
+    float r[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        const float *u = c[(k + 1) % 3], *v = c[(k + 2) % 3];
+        r[k][0] = u[1] * v[2] - u[2] * v[1];
+        r[k][1] = u[2] * v[0] - u[0] * v[2];
+        r[k][2] = u[0] * v[1] - u[1] * v[0];
+    }
+    const float det = c[0][0] * r[0][0] + c[0][1] * r[0][1] + c[0][2] * r[0][2];
+    const float inv = 1.0f / det;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        g[3 * (k + 1) + 0] = r[k][0] * inv;
+        g[3 * (k + 1) + 1] = r[k][1] * inv;
+        g[3 * (k + 1) + 2] = r[k][2] * inv;
+    }
+    g[0] = -(g[3] + g[6] + g[9]);
+    g[1] = -(g[4] + g[7] + g[10]);
+    g[2] = -(g[5] + g[8] + g[11]);
+    *vol = fabsf(det) * (1.0f / 6.0f);
 }
 
 struct PcgArgs
@@ -234,39 +312,41 @@ struct PcgArgs
     const float *z;           // z (PCG); x holds p_old
     Ctl *ctl;
     double *part_dot;         // out: per-tile p.Ap share
-    const double *prr, *prz;  // in: update kernel's r.r / r.z shares of the previous iteration
+    const double *prr, *prz;  // in: folded {r.r, r.z} of the previous update (per rank)
     unsigned nupd;
-    unsigned stride;          // 1, or 2 for the gathered {r.r, r.z} pairs of a sharded system
+    unsigned stride;
     unsigned it;
     double *hist;
     unsigned abl;  // diagnostic ablation bits (CWF_ABLATE), 0 in normal runs
 };
 
-// MODE 0: apply (gather x, optional sanitize); MODE 1: PCG (gather z, p_old -> p_new)
-template <bool ISO, bool SANITIZE, int MODE, int NT>
+// MODE 0: apply (gather x, optional sanitize); MODE 1: PCG (gather z, p_old -> p_new).
+// GEO: 8-B element records + per-tile-node coordinates (geometry recomputed); else 48-B records.
+template <bool ISO, bool SANITIZE, int MODE, int NT, bool GEO>
 __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__restrict__ x, PcgArgs pa)
 {
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
-    float *sf = lds;                                                 // [12][kTileElems]
+    const DevTiles &T = s.t;
+    const uint32_t ms = T.max_tile_nodes;
+    float *sf = lds;                                                     // [12][kTileElems]
     uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * kTileElems);  // [4*kTileElems] local CSR
-    float *sp = lds + 14 * kTileElems;                               // [3][max_tile_nodes]
-    __shared__ float dtab[kMaxM * 36];
+    float *sp = lds + 14 * kTileElems;                                   // [3][ms] node values
+    float *sx = sp + 3 * ms;                                             // [3][ms] node coordinates (GEO)
+    __shared__ float dtab[kMaxM * kTab];
     __shared__ double red[NT / 64];
     if constexpr (MODE == 1)
     {
         if (!pa.ctl->active)
             return;
     }
-    const DevTiles &T = s.t;
     const uint4 hd = T.hdr[blockIdx.x];
     const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
-    const uint32_t ms = T.max_tile_nodes;
     const float sK = (float)s.sK;
-    // (a) issue every load that does not depend on beta: the first tile-node record and its value(s),
-    //     and the tile's local CSR (4*ne u16 entries starting at 4*e0) staged into LDS
+    // (a) issue every load that does not depend on beta: the first tile-node record, its coordinates
+    //     and value(s), the thread's element records and the tile's local CSR (staged into LDS)
     const uint32_t i0 = threadIdx.x;
-    uint4 tn0 = uint4{0u, 0u, 0u, 0u};
+    uint2 tn0 = uint2{0u, 0u};
     float v0[3] = {0.f, 0.f, 0.f}, w0[3] = {0.f, 0.f, 0.f};
     if (i0 < nn)
     {
@@ -289,19 +369,32 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
             v0[2] = (mk & 4u) ? 0.f : v0[2];
         }
     }
-    // the thread's element records (kPer per thread), consumed after the gather barrier
-    constexpr int kPer = kTileElems / NT;
-    uint4 pq[kPer][3];
+    if constexpr (GEO)
     {
-        const uint4 *P0 = T.planes, *P1 = T.planes + T.E, *P2 = T.planes + 2u * T.E;
-#pragma unroll
-        for (int k = 0; k < kPer; ++k)
+        const uint32_t T3 = T.total_tile_nodes;
+        for (uint32_t i = threadIdx.x; i < nn; i += NT)
         {
-            const uint32_t j = threadIdx.x + k * NT;
-            const uint32_t e = e0 + (j < ne ? j : 0u);
-            pq[k][0] = P0[e];
-            pq[k][1] = P1[e];
-            pq[k][2] = P2[e];
+            sx[i] = T.tcoord[nb + i];
+            sx[ms + i] = T.tcoord[T3 + nb + i];
+            sx[2 * ms + i] = T.tcoord[2 * T3 + nb + i];
+        }
+    }
+    constexpr int kPer = kTileElems / NT;
+    uint4 pq[kPer][GEO ? 1 : 3];
+    uint2 pid[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+    {
+        const uint32_t j = threadIdx.x + k * NT;
+        const uint32_t e = e0 + (j < ne ? j : 0u);
+        if constexpr (GEO)
+            pid[k] = T.eid[e];
+        else
+        {
+            const uint4 *P = T.planes;
+            pq[k][0] = P[e];
+            pq[k][GEO ? 0 : 1] = P[T.E + e];
+            pq[k][GEO ? 0 : 2] = P[2u * T.E + e];
         }
     }
     {
@@ -320,7 +413,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
         if (pa.abl & 1u)
             beta = (float)pa.ctl->beta;
         else if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta,
-                                       pa.abl & 32u))
+                                    pa.abl & 32u))
             return;
     }
     if (i0 < nn)
@@ -338,7 +431,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     }
     for (uint32_t i = i0 + NT; i < nn; i += NT)
     {
-        const uint4 tn = T.tnode[nb + i];
+        const uint2 tn = T.tnode[nb + i];
         float u[3];
         gather_node<SANITIZE, MODE>(s, x, pa.z, beta, tn.x & 0x7fffffffu, u);
         sp[i] = u[0];
@@ -346,7 +439,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
         sp[2 * ms + i] = u[2];
     }
     __syncthreads();
-    // (b) elements (records prefetched at kernel entry)
+    // (b) elements
     if (!(pa.abl & 16u))
     {
 #pragma unroll
@@ -354,21 +447,27 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
         {
             const uint32_t j = threadIdx.x + k * NT;
             if (j < ne)
-                element_forces<ISO>(s, pq[k][0], pq[k][1], pq[k][2], T.mat ? T.mat[e0 + j] : 0u, j, sp, ms, dtab,
-                                    sK, sf);
+            {
+                float g[12], vol;
+                uint32_t li[4];
+                if constexpr (GEO)
+                    coord_geometry(pid[k], sx, ms, g, li, &vol);
+                else
+                    record_geometry(pq[k][0], pq[k][GEO ? 0 : 1], pq[k][GEO ? 0 : 2], g, li, &vol);
+                element_forces<ISO>(s, g, li, vol * sK, T.mat ? T.mat[e0 + j] : 0u, j, sp, ms, dtab, sf);
+            }
         }
     }
     __syncthreads();
-    // (c) fold per tile node
+    // (c) fold per tile node (tile-major partials: the tile's block is one contiguous store)
     double pap = 0.0;
     const float sM = (float)s.sM;
     for (uint32_t i = threadIdx.x; i < ((pa.abl & 8u) ? 0u : nn); i += NT)
     {
-        const uint4 tn = i == threadIdx.x ? tn0 : T.tnode[nb + i];
+        const uint2 tn = i == threadIdx.x ? tn0 : T.tnode[nb + i];
         float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-        const uint32_t qb = 4u * e0;
-        const uint32_t qe = tn.w - qb;
-        uint32_t q = tn.z - qb;
+        const uint32_t qe = tn.y >> 16;
+        uint32_t q = tn.y & 0xffffu;
         // 4 independent (entry, force) LDS chains in flight; the sums stay in ascending-entry order
         for (; q + 4 <= qe; q += 4)
         {
@@ -401,7 +500,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
             a1 += sf[(c + 1) * kTileElems + el];
             a2 += sf[(c + 2) * kTileElems + el];
         }
-        float *o = T.part + 3ull * tn.y;
+        float *o = T.part + 3ull * (nb + i);
         o[0] = a0;
         o[1] = a1;
         o[2] = a2;
@@ -425,6 +524,437 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     }
 }
 
+// Fixed-point variant (CWF_TILE_FOLD=acc): the tile's element forces are accumulated per tile node with
+// 32-bit integer LDS atomics after scaling by a per-tile power of two (block max |f|, headroom for the
+// tile's largest node degree). Integer addition is associative, so the tile sums are exact and
+// independent of atomic order (deterministic) while no force array, local CSR or fold pass is needed:
+// 13 KB of LDS per tile instead of 34 KB, and no CSR stream. The resolution is 2^-24..2^-25 of the
+// tile's largest force, at or below fp32 accumulation's own rounding.
+template <bool ISO, bool SANITIZE, int MODE, int NT, bool GEO>
+__global__ __launch_bounds__(NT) void k_keff_tiles_acc(DevSys s, const float *__restrict__ x, PcgArgs pa)
+{
+    constexpr int kTab = ISO ? 12 : 36;
+    extern __shared__ float lds[];
+    const DevTiles &T = s.t;
+    const uint32_t ms = T.max_tile_nodes;
+    float *sp = lds;                                                        // [3][ms] node values
+    float *sx = sp + 3 * ms;                                                // [3][ms] coordinates (GEO)
+    int *acc = reinterpret_cast<int *>(sx + (GEO ? 3 * ms : 0));            // [3][ms] fixed-point sums
+    __shared__ float dtab[kMaxM * kTab];
+    __shared__ double red[NT / 64];
+    __shared__ float wmax[NT / 64];
+    if constexpr (MODE == 1)
+    {
+        if (!pa.ctl->active)
+            return;
+    }
+    const uint4 hd = T.hdr[blockIdx.x];
+    const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
+    const float sK = (float)s.sK;
+    const uint32_t i0 = threadIdx.x;
+    uint2 tn0 = uint2{0u, 0u};
+    float v0[3] = {0.f, 0.f, 0.f}, w0[3] = {0.f, 0.f, 0.f};
+    if (i0 < nn)
+    {
+        tn0 = T.tnode[nb + i0];
+        const uint32_t g = tn0.x & 0x7fffffffu;
+        v0[0] = x[3u * g + 0];
+        v0[1] = x[3u * g + 1];
+        v0[2] = x[3u * g + 2];
+        if constexpr (MODE == 1)
+        {
+            w0[0] = pa.z[3u * g + 0];
+            w0[1] = pa.z[3u * g + 1];
+            w0[2] = pa.z[3u * g + 2];
+        }
+        else if constexpr (SANITIZE)
+        {
+            const uint32_t mk = s.mask[g];
+            v0[0] = (mk & 1u) ? 0.f : v0[0];
+            v0[1] = (mk & 2u) ? 0.f : v0[1];
+            v0[2] = (mk & 4u) ? 0.f : v0[2];
+        }
+    }
+    if constexpr (GEO)
+    {
+        const uint32_t T3 = T.total_tile_nodes;
+        for (uint32_t i = threadIdx.x; i < nn; i += NT)
+        {
+            sx[i] = T.tcoord[nb + i];
+            sx[ms + i] = T.tcoord[T3 + nb + i];
+            sx[2 * ms + i] = T.tcoord[2 * T3 + nb + i];
+        }
+    }
+    constexpr int kPer = kTileElems / NT;
+    uint4 pq[kPer][GEO ? 1 : 3];
+    uint2 pid[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+    {
+        const uint32_t j = threadIdx.x + k * NT;
+        const uint32_t e = e0 + (j < ne ? j : 0u);
+        if constexpr (GEO)
+            pid[k] = T.eid[e];
+        else
+        {
+            const uint4 *P = T.planes;
+            pq[k][0] = P[e];
+            pq[k][GEO ? 0 : 1] = P[T.E + e];
+            pq[k][GEO ? 0 : 2] = P[2u * T.E + e];
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < 3 * nn; i += NT)
+        acc[(i / nn) * ms + (i % nn)] = 0;
+    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
+    for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
+        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
+    float beta = 0.f;
+    if constexpr (MODE == 1)
+    {
+        if (pa.abl & 1u)
+            beta = (float)pa.ctl->beta;
+        else if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta,
+                                    pa.abl & 32u))
+            return;
+    }
+    if (i0 < nn)
+    {
+        if constexpr (MODE == 1)
+        {
+            v0[0] = fmaf(beta, v0[0], w0[0]);
+            v0[1] = fmaf(beta, v0[1], w0[1]);
+            v0[2] = fmaf(beta, v0[2], w0[2]);
+        }
+        sp[i0] = v0[0];
+        sp[ms + i0] = v0[1];
+        sp[2 * ms + i0] = v0[2];
+    }
+    for (uint32_t i = i0 + NT; i < nn; i += NT)
+    {
+        const uint2 tn = T.tnode[nb + i];
+        float u[3];
+        gather_node<SANITIZE, MODE>(s, x, pa.z, beta, tn.x & 0x7fffffffu, u);
+        sp[i] = u[0];
+        sp[ms + i] = u[1];
+        sp[2 * ms + i] = u[2];
+    }
+    __syncthreads();
+    // (b) element forces in registers + the tile's largest magnitude
+    float f[kPer][12];
+    uint32_t li[kPer][4];
+    float fmx = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+    {
+        const uint32_t j = threadIdx.x + k * NT;
+        float g[12], vol;
+        if constexpr (GEO)
+            coord_geometry(pid[k], sx, ms, g, li[k], &vol);
+        else
+            record_geometry(pq[k][0], pq[k][GEO ? 0 : 1], pq[k][GEO ? 0 : 2], g, li[k], &vol);
+        if (j < ne)
+        {
+            element_force_values<ISO>(s, g, li[k], vol * sK, T.mat ? T.mat[e0 + j] : 0u, sp, ms, dtab, f[k]);
+#pragma unroll
+            for (int c = 0; c < 12; ++c)
+                fmx = fmaxf(fmx, fabsf(f[k][c]));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        fmx = fmaxf(fmx, __shfl_xor(fmx, o, 64));
+    if ((threadIdx.x & 63) == 0)
+        wmax[threadIdx.x >> 6] = fmx;
+    __syncthreads();
+    float M = 0.f;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w)
+        M = fmaxf(M, wmax[w]);
+    // scale 2^sc with M 2^sc < 2^(30 - ceil(log2 maxdeg)): a node's <= maxdeg terms stay below 2^30
+    int ex = 0;
+    (void)frexpf(M, &ex);
+    const int sc = M > 0.f ? 30 - (int)T.deg_log2 - ex : 0;
+    // (c) exact fixed-point accumulation
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+    {
+        const uint32_t j = threadIdx.x + k * NT;
+        if (j < ne)
+        {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    atomicAdd(&acc[c * ms + li[k][a]], __float2int_rn(ldexpf(f[k][3 * a + c], sc)));
+        }
+    }
+    __syncthreads();
+    // (d) tile-node partials (tile-major, contiguous) + the p.Ap share
+    double pap = 0.0;
+    const float sM = (float)s.sM;
+    for (uint32_t i = threadIdx.x; i < nn; i += NT)
+    {
+        const uint2 tn = i == threadIdx.x ? tn0 : T.tnode[nb + i];
+        const float a0 = ldexpf((float)acc[i], -sc), a1 = ldexpf((float)acc[ms + i], -sc),
+                    a2 = ldexpf((float)acc[2 * ms + i], -sc);
+        float *o = T.part + 3ull * (nb + i);
+        o[0] = a0;
+        o[1] = a1;
+        o[2] = a2;
+        if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)
+        {
+            const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
+            pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+            if (tn.x & 0x80000000u)
+            {
+                const float m = s.mass[tn.x & 0x7fffffffu] * sM;
+                pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
+                       (double)(m * p2) * (double)p2;
+            }
+        }
+    }
+    if constexpr (MODE == 1)
+    {
+        const double t = block_sum<NT>(pap, red);
+        if (threadIdx.x == 0)
+            pa.part_dot[blockIdx.x] = t;
+    }
+}
+
+// Persistent, software-pipelined form of k_keff_tiles (GEO records, CSR fold; the default FAST path).
+// A resident grid (occupancy x CUs) walks the tiles; while a workgroup computes tile t from LDS, the
+// loads of its next tile t' (tile-node records, coordinates, corner ids, local CSR, then the z/p
+// gathers) are already in flight in registers, so each tile's memory chain overlaps the previous
+// tile's element and fold work instead of being exposed. Tiles are dealt XCD-contiguously (workgroup
+// b runs on XCD b % 8 and walks that XCD's eighth of the Morton-ordered tiles) so neighbouring tiles,
+// which share nodes, share an L2. beta (the residual step) and the material table are set up once
+// per workgroup; the p.Ap share is one per workgroup.
+struct PipeNext
+{
+    uint2 tn;          // record of tile node threadIdx.x
+    float c[3];        // its coordinates
+    float v[3], w[3];  // x / p_old and z (MODE 1) at that node
+    uint2 id[2];       // corner ids of elements threadIdx.x, threadIdx.x + 256
+    uint4 csr;         // 8 local-CSR entries (16 B) of the tile
+};
+
+template <bool SANITIZE, int MODE>
+__device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, PipeNext &n)
+{
+    const DevTiles &T = s.t;
+    const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
+    const uint32_t i = threadIdx.x;
+    n.tn = i < nn ? T.tnode[nb + i] : uint2{0u, 0u};
+    const uint32_t T3 = T.total_tile_nodes;
+    const uint32_t q = nb + (i < nn ? i : 0u);
+    n.c[0] = T.tcoord[q];
+    n.c[1] = T.tcoord[T3 + q];
+    n.c[2] = T.tcoord[2 * T3 + q];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+        const uint32_t j = i + k * 256u;
+        n.id[k] = T.eid[e0 + (j < ne ? j : 0u)];
+    }
+    const uint4 *src = reinterpret_cast<const uint4 *>(T.csr_ent + 4ull * e0);  // 4 ne u16 = ne / 2 uint4
+    n.csr = i < (ne + 1) / 2 ? src[i] : uint4{0u, 0u, 0u, 0u};
+}
+
+template <bool SANITIZE, int MODE>
+__device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *__restrict__ x,
+                                                  const float *__restrict__ z, uint32_t nn, PipeNext &n)
+{
+    const uint32_t g = n.tn.x & 0x7fffffffu;  // node 0 for idle lanes (harmless, in range)
+    (void)nn;
+    n.v[0] = x[3u * g + 0];
+    n.v[1] = x[3u * g + 1];
+    n.v[2] = x[3u * g + 2];
+    if constexpr (MODE == 1)
+    {
+        n.w[0] = z[3u * g + 0];
+        n.w[1] = z[3u * g + 1];
+        n.w[2] = z[3u * g + 2];
+    }
+    else if constexpr (SANITIZE)
+    {
+        const uint32_t mk = s.mask[g];
+        n.v[0] = (mk & 1u) ? 0.f : n.v[0];
+        n.v[1] = (mk & 2u) ? 0.f : n.v[1];
+        n.v[2] = (mk & 4u) ? 0.f : n.v[2];
+    }
+}
+
+template <bool ISO, bool SANITIZE, int MODE>
+__global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa)
+{
+    constexpr int NT = 256;
+    constexpr int kTab = ISO ? 12 : 36;
+    extern __shared__ float lds[];
+    const DevTiles &T = s.t;
+    const uint32_t ms = T.max_tile_nodes;
+    float *sf = lds;                                                     // [12][kTileElems]
+    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * kTileElems);  // [4*kTileElems] local CSR
+    float *sp = lds + 14 * kTileElems;                                   // [3][ms] node values
+    float *sx = sp + 3 * ms;                                             // [3][ms] node coordinates
+    __shared__ float dtab[kMaxM * kTab];
+    __shared__ double red[NT / 64];
+    if constexpr (MODE == 1)
+    {
+        if (!pa.ctl->active)
+            return;
+    }
+    // this workgroup's tiles: XCD-contiguous ranges, stride = workgroups per XCD
+    const uint32_t nxcd = 8u, xcd = blockIdx.x % nxcd, lb = blockIdx.x / nxcd, nbx = gridDim.x / nxcd;
+    const uint32_t t_end = (uint32_t)(((uint64_t)(xcd + 1) * T.ntiles) / nxcd);
+    uint32_t t = (uint32_t)(((uint64_t)xcd * T.ntiles) / nxcd) + lb;
+    PipeNext cur;
+    uint4 hd = t < t_end ? T.hdr[t] : uint4{0u, 0u, 0u, 0u};
+    if (t < t_end)
+    {
+        pipe_issue_records<SANITIZE, MODE>(s, hd, cur);
+        pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hd.w, cur);
+    }
+    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
+    for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
+        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
+    float beta = 0.f;
+    if constexpr (MODE == 1)
+    {
+        // pcg.cpp:862-895 of the previous update, once per workgroup
+        if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta, pa.abl & 32u))
+            return;
+    }
+    const float sK = (float)s.sK, sM = (float)s.sM;
+    double pap = 0.0;
+    for (; t < t_end; t += nbx)
+    {
+        const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
+        // (a) LDS fill of tile t from the prefetched registers (second node slot, if any, loads directly)
+        const uint32_t i0 = threadIdx.x;
+        if (i0 < nn)
+        {
+            float v0 = cur.v[0], v1 = cur.v[1], v2 = cur.v[2];
+            if constexpr (MODE == 1)
+            {
+                v0 = fmaf(beta, v0, cur.w[0]);
+                v1 = fmaf(beta, v1, cur.w[1]);
+                v2 = fmaf(beta, v2, cur.w[2]);
+            }
+            sp[i0] = v0;
+            sp[ms + i0] = v1;
+            sp[2 * ms + i0] = v2;
+            sx[i0] = cur.c[0];
+            sx[ms + i0] = cur.c[1];
+            sx[2 * ms + i0] = cur.c[2];
+        }
+        for (uint32_t i = i0 + NT; i < nn; i += NT)
+        {
+            const uint2 tn = T.tnode[nb + i];
+            float u[3];
+            gather_node<SANITIZE, MODE>(s, x, pa.z, beta, tn.x & 0x7fffffffu, u);
+            sp[i] = u[0];
+            sp[ms + i] = u[1];
+            sp[2 * ms + i] = u[2];
+            const uint32_t T3 = T.total_tile_nodes;
+            sx[i] = T.tcoord[nb + i];
+            sx[ms + i] = T.tcoord[T3 + nb + i];
+            sx[2 * ms + i] = T.tcoord[2 * T3 + nb + i];
+        }
+        if (i0 < (ne + 1) / 2)
+            reinterpret_cast<uint4 *>(sc)[i0] = cur.csr;
+        const uint2 tn_own = cur.tn;
+        const uint2 id0 = cur.id[0], id1 = cur.id[1];
+        __syncthreads();
+        // (b) next tile's records in flight during this tile's element and fold work
+        const uint32_t tn_next = t + nbx;
+        uint4 hdn = uint4{0u, 0u, 0u, 0u};
+        if (tn_next < t_end)
+        {
+            hdn = T.hdr[tn_next];
+            pipe_issue_records<SANITIZE, MODE>(s, hdn, cur);
+        }
+        // (c) elements of tile t
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+        {
+            const uint32_t j = threadIdx.x + k * NT;
+            if (j < ne)
+            {
+                float g[12], vol;
+                uint32_t li[4];
+                coord_geometry(k ? id1 : id0, sx, ms, g, li, &vol);
+                element_forces<ISO>(s, g, li, vol * sK, T.mat ? T.mat[e0 + j] : 0u, j, sp, ms, dtab, sf);
+            }
+        }
+        __syncthreads();
+        // (d) next tile's gathers (its node records have arrived by now)
+        if (tn_next < t_end)
+            pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hdn.w, cur);
+        // (e) fold per tile node -> tile-major partials (+ p.Ap)
+        for (uint32_t i = threadIdx.x; i < nn; i += NT)
+        {
+            const uint2 tn = i == threadIdx.x ? tn_own : T.tnode[nb + i];
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+            const uint32_t qe = tn.y >> 16;
+            uint32_t q = tn.y & 0xffffu;
+            for (; q + 4 <= qe; q += 4)
+            {
+                uint32_t ent[4];
+                float f[4][3];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    ent[u] = sc[q + u];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    const uint32_t el = ent[u] >> 2, c = 3u * (ent[u] & 3u);
+                    f[u][0] = sf[(c + 0) * kTileElems + el];
+                    f[u][1] = sf[(c + 1) * kTileElems + el];
+                    f[u][2] = sf[(c + 2) * kTileElems + el];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                {
+                    a0 += f[u][0];
+                    a1 += f[u][1];
+                    a2 += f[u][2];
+                }
+            }
+            for (; q < qe; ++q)
+            {
+                const uint32_t ent = sc[q];
+                const uint32_t el = ent >> 2, c = 3u * (ent & 3u);
+                a0 += sf[(c + 0) * kTileElems + el];
+                a1 += sf[(c + 1) * kTileElems + el];
+                a2 += sf[(c + 2) * kTileElems + el];
+            }
+            float *o = T.part + 3ull * (nb + i);
+            o[0] = a0;
+            o[1] = a1;
+            o[2] = a2;
+            if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
+            {
+                const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
+                pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+                if (tn.x & 0x80000000u)  // the node's owner slot adds its mass term m s_M |p|^2 once
+                {
+                    const float m = s.mass[tn.x & 0x7fffffffu] * sM;
+                    pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
+                           (double)(m * p2) * (double)p2;
+                }
+            }
+        }
+        __syncthreads();  // LDS is refilled by the next tile
+        hd = hdn;
+    }
+    if constexpr (MODE == 1)
+    {
+        const double tt = block_sum<NT>(pap, red);
+        if (threadIdx.x == 0)
+            pa.part_dot[blockIdx.x] = tt;
+    }
+}
+
 // pcg.cpp:862-895 for the last iteration of a batch (the next batch's tiles kernel repeats it
 // idempotently): one workgroup
 __global__ __launch_bounds__(256) void k_pcg_check(Ctl *ctl, const double *__restrict__ prr,
@@ -439,18 +969,39 @@ __global__ __launch_bounds__(256) void k_pcg_check(Ctl *ctl, const double *__res
 }
 
 // one workgroup: out[0] = fold(a[0..n)), out[1] = fold(b[0..n)) (b may be NULL), fixed order
-__global__ __launch_bounds__(256) void k_fold_pair(const double *__restrict__ a, const double *__restrict__ b,
-                                                   unsigned n, double *__restrict__ out)
+__global__ __launch_bounds__(1024) void k_fold_pair(const double *__restrict__ a, const double *__restrict__ b,
+                                                    unsigned n, double *__restrict__ out)
 {
-    __shared__ double red[4];
-    const double ta = fold_all<256>(a, n, red);
-    const double tb = b ? fold_all<256>(b, n, red) : 0.0;
+    __shared__ double red[16];
+    const double ta = fold_all<1024>(a, n, red);
+    const double tb = b ? fold_all<1024>(b, n, red) : 0.0;
     if (threadIdx.x == 0)
     {
         out[0] = ta;
         if (b)
             out[1] = tb;
     }
+}
+
+// FAST: symmetrise the block inverse (upper triangle wins, so k_precond and the update agree) and
+// pack it to 6 floats per node for the update pass
+__global__ __launch_bounds__(256) void k_sym_inverse(uint32_t N, float *__restrict__ inv9, float *__restrict__ inv6)
+{
+    const uint32_t n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= N)
+        return;
+    float *a = inv9 + 9ull * n;
+    const float a00 = a[0], a01 = a[1], a02 = a[2], a11 = a[4], a12 = a[5], a22 = a[8];
+    a[3] = a01;
+    a[6] = a02;
+    a[7] = a12;
+    float *b = inv6 + 6ull * n;
+    b[0] = a00;
+    b[1] = a01;
+    b[2] = a02;
+    b[3] = a11;
+    b[4] = a12;
+    b[5] = a22;
 }
 
 __global__ __launch_bounds__(256) void k_halo_pack(const uint32_t *__restrict__ idx, uint64_t n,
@@ -475,7 +1026,7 @@ __global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
     {
-        const float *pp = T.part + 3ull * q;
+        const float *pp = T.part + 3ull * T.part_slot[q];
         a0 += pp[0];
         a1 += pp[1];
         a2 += pp[2];
@@ -536,7 +1087,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         float a0 = 0.f, a1 = 0.f, a2 = 0.f;
         for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
         {
-            const float *pp = T.part + 3ull * q;
+            const float *pp = T.part + 3ull * T.part_slot[q];
             a0 += pp[0];
             a1 += pp[1];
             a2 += pp[2];
@@ -563,7 +1114,10 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             p[d] = pk;
             rv[k] = rw;
         }
-        const float *iv = inv + 9u * n;
+        // symmetric block inverse, 6 floats per node {a00 a01 a02 a11 a12 a22} (three 8-B loads)
+        const float2 *i2 = reinterpret_cast<const float2 *>(inv + 6ull * n);
+        const float2 u0 = i2[0], u1 = i2[1], u2 = i2[2];
+        const float iv[9] = {u0.x, u0.y, u1.x, u0.y, u1.y, u2.x, u1.x, u2.x, u2.y};
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
@@ -587,22 +1141,61 @@ inline unsigned grid_for(uint32_t n, uint32_t b) { return (n + b - 1) / b; }
 
 inline size_t tiles_lds(const DevSys &s)
 {
-    // element forces [12][kTileElems] f32 + local CSR [4*kTileElems] u16 + node values [3][max_tile_nodes]
-    return sizeof(float) * (14 * kTileElems + 3 * (size_t)s.t.max_tile_nodes);
+    // element forces [12][kTileElems] f32 + local CSR [4*kTileElems] u16 + node values [3][ms]
+    // (+ node coordinates [3][ms] with GEO records)
+    return sizeof(float) * (14 * kTileElems + (s.t.geo ? 6 : 3) * (size_t)s.t.max_tile_nodes);
+}
+
+template <bool ISO, bool SAN, int MODE, bool GEO>
+void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st)
+{
+    if (s.t.acc)
+    {
+        const size_t lds = sizeof(float) * (GEO ? 9 : 6) * (size_t)s.t.max_tile_nodes;
+        if (nt == 512)
+            k_keff_tiles_acc<ISO, SAN, MODE, 512, GEO><<<s.t.ntiles, 512, lds, st>>>(s, x, pa);
+        else
+            k_keff_tiles_acc<ISO, SAN, MODE, 256, GEO><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
+        return;
+    }
+    const size_t lds = tiles_lds(s);
+    if (nt == 512)
+        k_keff_tiles<ISO, SAN, MODE, 512, GEO><<<s.t.ntiles, 512, lds, st>>>(s, x, pa);
+    else
+        k_keff_tiles<ISO, SAN, MODE, 256, GEO><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
+}
+
+template <bool ISO>
+unsigned pipe_grid_query(const DevSys &s)
+{
+    int dev = 0, bpc = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1>, 256, tiles_lds(s));
+    unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
+    g = g < 8u ? 8u : g - g % 8u;  // whole XCD groups
+    const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
+    return g < need ? g : (need ? need : 8u);
 }
 
 template <bool ISO, bool SAN, int MODE>
 void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st)
 {
-    const size_t lds = tiles_lds(s);
-    if (nt == 512)
-        k_keff_tiles<ISO, SAN, MODE, 512><<<s.t.ntiles, 512, lds, st>>>(s, x, pa);
+    if (s.t.pipe)
+    {
+        k_keff_tiles_pipe<ISO, SAN, MODE><<<s.t.pipe_grid, 256, tiles_lds(s), st>>>(s, x, pa);
+        return;
+    }
+    if (s.t.geo)
+        launch_tiles_g<ISO, SAN, MODE, true>(s, x, pa, nt, st);
     else
-        k_keff_tiles<ISO, SAN, MODE, 256><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
+        launch_tiles_g<ISO, SAN, MODE, false>(s, x, pa, nt, st);
 }
 }  // namespace
 
-unsigned fast_tile_blocks(const DevSys &s) { return s.t.ntiles; }
+unsigned fast_tile_blocks(const DevSys &s) { return s.t.pipe ? s.t.pipe_grid : s.t.ntiles; }
+
+unsigned fast_pipe_grid(const DevSys &s) { return s.iso ? pipe_grid_query<true>(s) : pipe_grid_query<false>(s); }
 unsigned fast_update_blocks(const DevSys &s)
 {
     const unsigned g = grid_for(s.N, kUpdThreads);
@@ -652,15 +1245,9 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
         const char *e = getenv("CWF_ABLATE");
         return e ? (unsigned)atoi(e) : 0u;
     }();
-    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->part1, h->part2, fast_update_blocks(s), 1u, it, h->hist,
-               abl};
-    if (h->sharded())
-    {
-        pa.prr = h->g_rrz;
-        pa.prz = h->g_rrz + 1;
-        pa.nupd = (unsigned)h->nranks;
-        pa.stride = 2u;
-    }
+    // beta / convergence from the folded per-rank {r.r, r.z} pairs (one pair on a single GPU)
+    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it,
+               h->hist, abl};
     if (s.iso)
         launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
     else
@@ -670,33 +1257,36 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    const bool sh = h->sharded();
-    k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
-        s, rhs, h->inv, h->x, h->r, h->z, h->p, h->ctl, sh ? h->g_pap : h->part0,
-        sh ? (unsigned)h->nranks : fast_tile_blocks(s), h->part1, h->part2, it);
+    k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(s, rhs, h->inv6, h->x, h->r, h->z, h->p, h->ctl,
+                                                                      h->g_pap, (unsigned)h->nranks, h->part1,
+                                                                      h->part2, it);
 }
 
 // diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->part1, h->part2, fast_update_blocks(s), 1u, 1u, h->hist,
-               abl | 32u};
+    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
+               h->hist, abl | 32u};
     for (int i = 0; i < reps; ++i)
         launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
 }
 
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
-    if (h->sharded())
-        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
-    else
-        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->part1, h->part2, fast_update_blocks(h->ds), 1u, it, h->hist);
+    k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
+}
+
+void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
+{
+    parity_block_jacobi(h, h->inv, st);
+    if (h->ds.N)
+        k_sym_inverse<<<grid_for(h->ds.N, 256), 256, 0, st>>>(h->ds.N, h->inv, h->inv6);
 }
 
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st)
 {
-    k_fold_pair<<<1, 256, 0, st>>>(a, b, n, out);
+    k_fold_pair<<<1, 1024, 0, st>>>(a, b, n, out);
 }
 
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st)

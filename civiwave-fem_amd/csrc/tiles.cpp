@@ -77,6 +77,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out)
         out.planes[q].resize(E);
     if (d->material_count > 1)
         out.mat.resize(E);
+    out.eid.resize(E);
     out.csr_ent.reserve(E * 4);
     std::vector<uint32_t> stamp(N, 0xFFFFFFFFu), local(N, 0);
     std::vector<uint32_t> nodes;
@@ -130,6 +131,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out)
             std::memcpy(&q1, g + 2, 16);    // g0z g1x g1y g1z
             std::memcpy(&q2, g + 6, 12);    // g2x g2y g2z
             std::memcpy(&q2.w, &d->element_volume[src], 4);
+            out.eid[e0 + j] = uint2{q0.x, q0.y};
             out.planes[0][e0 + j] = q0;
             out.planes[1][e0 + j] = q1;
             out.planes[2][e0 + j] = q2;
@@ -154,6 +156,14 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out)
         {
             out.tile_nodes.push_back(nodes[i]);
             out.csr_off.push_back((uint32_t)(base + cnt[i + 1]));
+        }
+        if (d->node_coords && nn)
+        {
+            // tile-relative f32 coordinates (origin = the tile's first node) keep the edge vectors exact
+            const double *o = d->node_coords + 3ull * nodes[0];
+            for (uint32_t i = 0; i < nn; ++i)
+                for (int k = 0; k < 3; ++k)
+                    out.tcoord[k].push_back((float)(d->node_coords[3ull * nodes[i] + k] - o[k]));
         }
         out.max_tile_nodes = std::max(out.max_tile_nodes, nn);
         out.tile_elem_off.push_back((uint32_t)e);
@@ -182,6 +192,51 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out)
         if (out.node_part_off[n + 1] > out.node_part_off[n])
             out.tile_nodes[out.node_part_slot[out.node_part_off[n]]] |= 0x80000000u;
     return 0;
+}
+
+bool geometry_matches(const cwf_system_desc *d)
+{
+    if (!d->node_coords)
+        return false;
+    const double *X = d->node_coords;
+    for (uint64_t e = 0; e < d->element_count; ++e)
+    {
+        const uint32_t *c = d->element_connectivity + 8 * e;
+        double ed[3][3];
+        for (int k = 0; k < 3; ++k)
+            for (int q = 0; q < 3; ++q)
+                ed[k][q] = X[3ull * c[k + 1] + q] - X[3ull * c[0] + q];
+        double r[3][3];
+        for (int k = 0; k < 3; ++k)
+        {
+            const double *u = ed[(k + 1) % 3], *v = ed[(k + 2) % 3];
+            r[k][0] = u[1] * v[2] - u[2] * v[1];
+            r[k][1] = u[2] * v[0] - u[0] * v[2];
+            r[k][2] = u[0] * v[1] - u[1] * v[0];
+        }
+        const double det = ed[0][0] * r[0][0] + ed[0][1] * r[0][1] + ed[0][2] * r[0][2];
+        if (!(std::fabs(det) > 0.0))
+            return false;
+        double g[4][3];
+        for (int k = 0; k < 3; ++k)
+            for (int q = 0; q < 3; ++q)
+                g[k + 1][q] = r[k][q] / det;
+        for (int q = 0; q < 3; ++q)
+            g[0][q] = -(g[1][q] + g[2][q] + g[3][q]);
+        double gmax = 0.0;
+        for (int a = 0; a < 4; ++a)
+            for (int q = 0; q < 3; ++q)
+                gmax = std::max(gmax, std::fabs(g[a][q]));
+        const float *G = d->element_gradients + 24 * e;
+        for (int a = 0; a < 4; ++a)
+            for (int q = 0; q < 3; ++q)
+                if (std::fabs((double)G[3 * a + q] - g[a][q]) > 1e-5 * gmax)
+                    return false;
+        const double vol = std::fabs(det) / 6.0;
+        if (std::fabs((double)d->element_volume[e] - vol) > 1e-5 * vol)
+            return false;
+    }
+    return true;
 }
 
 }  // namespace cwf

@@ -77,6 +77,7 @@ class PackingResult:
     offsets: np.ndarray  # u32 [N+1]
     element_indices: np.ndarray  # u32 [4E]
     local_indices: np.ndarray  # u8 [4E]
+    position64: np.ndarray | None = None  # f64 [N,3] the preprocess input (FAST tiles: order + geometry)
 
 
 def _group_nodes(mesh: Mesh, gid: int) -> np.ndarray:
@@ -203,7 +204,7 @@ def build_packed_buffers(mesh: Mesh, cfg: Config, load_time_seconds: float = 0.0
     return PackingResult(N, E, D, rb, max(1, (D + rb - 1) // rb), mesh.coords.astype(np.float32),
                          _safe_f32(loads), bc_mask, bc_value, pre["mass32"], pre["mass64"], pre["conn8"],
                          pre["grads"], pre["volume"], pre["material_index"], pre["offsets"], pre["adj_elem"],
-                         pre["adj_local"])
+                         pre["adj_local"], np.ascontiguousarray(mesh.coords, np.float64))
 
 
 def _safe_f32(v: np.ndarray) -> np.ndarray:

@@ -122,7 +122,8 @@ class MatrixFreeSystem:
                    packing.lumped_mass, packing.bc_mask, packing.node_count, packing.element_count,
                    packing.dof_count, stiffness_scale, mass_factor, packing.reduction_block,
                    packing.reduction_partials, (packing.offsets, packing.element_indices, packing.local_indices),
-                   mode, device, packing.position0)
+                   mode, device, packing.position64 if getattr(packing, "position64", None) is not None
+                   else packing.position0)
 
     def desc(self) -> "_lib.SystemDesc":
         """The C descriptor over this object's host arrays (kept alive by the object)."""

@@ -43,7 +43,7 @@ def main():
         rd = 2 * f * 1024 if f is not None else None
         wr = w * 1024 if w is not None else None
         bw = (rd + wr) / (avg * 1e-9) / 1e9 if rd is not None and wr is not None else None
-        short = name.split("(")[0][-70:]
+        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][-70:]
         print(f"{short:70s} {calls:6d} {avg / 1e3:8.2f} {pct:6.2f} "
               f"{(rd or 0) / 1e6:8.2f} {(wr or 0) / 1e6:8.2f} {(bw or 0):8.1f}")
         out[short] = dict(calls=calls, avg_ns=avg, pct=pct, read_bytes=rd, write_bytes=wr,
