@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--max-iterations", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iterations", type=int, default=40)
-    ap.add_argument("--traffic", default=None, help="PMC summary json (profiles/*.json) for roofline.traffic")
+    ap.add_argument("--traffic", default="auto",
+                    help="PMC summary json for roofline.traffic; 'auto' = newest profiles/r*_<config>_<mode>_pmc.json")
     return ap.parse_args()
 
 
@@ -155,12 +156,24 @@ def main():
     else:
         dof_iters, iters_sum, dofs_sum = local[1], local[2], local[3]
     avg_keff_ms = keff_ms.value / max(1, keff_n.value)
-    # algorithmic bytes of one K_eff launch: 32 B/node + 72 B/tet (reference layout)
-    alg_bytes = 32.0 * local_nodes + 72.0 * local_tets
+    # algorithmic bytes of one K_eff launch: the handle's own layout, every array the
+    # kernel touches counted once (it reads less than the reference layout's 32 B/node + 72 B/tet,
+    # which is reported beside it as the layout-independent comparator)
+    lay_b, ref_b = C.c_uint64(), C.c_uint64()
+    L.cwf_hip_system_keff_traffic(h, C.byref(lay_b), C.byref(ref_b))
+    alg_bytes, ref_bytes = float(lay_b.value), float(ref_b.value)
     achieved = alg_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
-    traffic = None
-    if args.traffic and os.path.exists(args.traffic):
-        traffic = json.load(open(args.traffic)).get("hbm_bytes_per_launch")
+    ref_equiv = ref_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
+    traffic, traffic_src = None, None
+    tpath = args.traffic
+    if tpath == "auto":
+        import glob
+
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{args.config}_{args.mode}_pmc.json")))
+        tpath = cands[-1] if cands and world == 1 else None
+    if tpath and os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        traffic_src = os.path.relpath(tpath, ROOT)
     result = None
     if rank == 0:
         cpu = None
@@ -189,8 +202,12 @@ def main():
             "dof_updates_per_sec": dofs_sum * args.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": "k_keff_" + args.mode, "avg_launch_ms": avg_keff_ms,
-                         "launches": int(keff_n.value), "algorithmic_bytes_per_launch": alg_bytes},
+                         "traffic_source": traffic_src,
+                         "kernel": "k_keff_tiles_pipe" if args.mode == "fast" else "k_keff_parity",
+                         "avg_launch_ms": avg_keff_ms, "launches": int(keff_n.value),
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "reference_layout_bytes_per_launch": ref_bytes,
+                         "reference_layout_equiv_gbs": ref_equiv},
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -702,6 +702,27 @@ int cwf_hip_system_memory(const cwf_hip_system *h, uint64_t *bytes)
     return 0;
 }
 
+int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes, uint64_t *reference_layout_bytes)
+{
+    if (!h || !layout_bytes || !reference_layout_bytes)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    const DevSys &s = h->ds;
+    const uint64_t N = s.N, E = s.E, T = s.t.total_tile_nodes;
+    *reference_layout_bytes = 32 * N + 72 * E;
+    if (h->mode == CWF_MODE_FAST && s.t.ntiles)
+    {
+        // per tile: 16-B header; per tet: corner ids (8 B GEO, 48-B records otherwise) + 4 u16 local-CSR
+        // entries (+ material id when M > 1); per tile node: {node, csr range} 8 B, coordinates 12 B (GEO),
+        // partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B
+        const uint64_t rec = s.t.geo ? 8 : 48;
+        *layout_bytes = 16ull * s.t.ntiles + E * (rec + 8 + (s.t.mat ? 4 : 0)) + T * (8 + (s.t.geo ? 12 : 0) + 12) +
+                        N * (24 + 4);
+    }
+    else  // PARITY node gather: 64-B element records + vol + CSR incidences, per node x in / y out + mass + mask
+        *layout_bytes = E * (64 + 4 + 16 + (s.M > 1 ? 4 : 0)) + N * (4 + 12 + 12 + 4 + 4);
+    return 0;
+}
+
 int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, int kind)
 {
     if (int st = check_ready(h))

@@ -127,6 +127,11 @@ int cwf_hip_system_set_scalars(cwf_hip_system *h, double stiffness_scale, double
 int cwf_hip_system_set_mode(cwf_hip_system *h, int mode);
 /* bytes of HBM held by the handle */
 int cwf_hip_system_memory(const cwf_hip_system *h, uint64_t *bytes);
+/* Algorithmic (compulsory) HBM bytes of one PCG-loop K_eff launch (measurement support, not a
+ * reference interface): `layout_bytes` = every array the handle's own K_eff kernel touches, counted
+ * once (the headline roofline uses the build's own layout when it reads less);
+ * `reference_layout_bytes` = 32 N + 72 E, the same SpMV over the reference's packed layout. */
+int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes, uint64_t *reference_layout_bytes);
 
 /* Live kernel timing (measurement support, not a reference interface): when enabled, every
  * K_eff launch inside solve_pcg / stepper_step is bracketed by hipEvents on the handle's stream;
