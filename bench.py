@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--mode", default="fast", choices=["fast", "parity"])
     ap.add_argument("--max-iterations", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--keff-sample", type=int, default=4,
+                    help="hipEvent-time every k-th K_eff launch of the timed steps (1 = all)")
     ap.add_argument("--cpu-iterations", type=int, default=40)
     ap.add_argument("--traffic", default="auto",
                     help="PMC summary json for roofline.traffic; 'auto' = newest profiles/r*_<config>_<mode>_pmc.json")
@@ -129,7 +131,7 @@ def main():
         t_sim += case.cfg.time.initial_dt
     import ctypes as C
 
-    L.cwf_hip_system_set_timing(h, 1)
+    L.cwf_hip_system_set_timing(h, args.keff_sample)
     torch.cuda.synchronize()
     barrier()
     total_iters = 0

@@ -187,6 +187,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             {
                 if (prev_enq + i >= h->ctl_host->iterations)
                     break;
+                if ((prev_enq + i) % (uint64_t)h->timing)
+                    continue;
                 float ms = 0.f;
                 if (hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]) == hipSuccess)
                 {
@@ -201,7 +203,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         const uint64_t nb = std::min<uint64_t>(batch, set.max_iterations - enq);
         for (uint64_t i = 0; i < nb; ++i)
         {
-            hipEvent_t e0 = h->timing ? h->ev[2 * i] : nullptr, e1 = h->timing ? h->ev[2 * i + 1] : nullptr;
+            const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
+            hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
             if (fast)
             {
                 if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
@@ -633,7 +636,7 @@ int cwf_hip_system_set_timing(cwf_hip_system *h, int enabled)
 {
     if (int st = check_ready(h))
         return st;
-    h->timing = enabled ? 1 : 0;
+    h->timing = enabled > 0 ? enabled : 0;  // time every `enabled`-th PCG-loop K_eff launch
     h->keff_ms = 0.0;
     h->keff_count = 0;
     return 0;

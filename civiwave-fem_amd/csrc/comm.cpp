@@ -221,12 +221,8 @@ int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<c
 int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
                              unsigned it, hipEvent_t e0, hipEvent_t e1)
 {
-    if (e0)
-        (void)hipEventRecord(e0, g[0]->stream);
-    for (cwf_hip_system *h : g)
-        fast_tiles_pcg(h, it, h->stream);
-    if (e1)
-        (void)hipEventRecord(e1, g[0]->stream);
+    for (size_t i = 0; i < g.size(); ++i)  // member 0's launch carries the timing events
+        fast_tiles_pcg(g[i], it, g[i]->stream, i ? nullptr : e0, i ? nullptr : e1);
     for (cwf_hip_system *h : g)
         fast_fold_pap(h, h->stream);
     if (int st = comm_allgather(g, &cwf_hip_system::g_pap, 1))

@@ -197,7 +197,7 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
 void fast_dot(const float *a, const float *b, const float *c, uint32_t D, double *pab, double *pac, hipStream_t st);
 void fast_fold(const double *part, uint32_t count, double *out, hipStream_t st);
 void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
-void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
+void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st);
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
@@ -205,6 +205,7 @@ unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
 unsigned fast_update_blocks(const DevSys &s);
 // sharded FAST PCG (comm.cpp orchestrates, spmv_tiles.hip / kernels_fast.hip launch)
+bool fast_direct_fold(const cwf_hip_system *h);  // unsharded: consumers fold per-workgroup shares
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> g_pap[rank]
 void fast_fold_rrz(cwf_hip_system *h, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
 void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st);

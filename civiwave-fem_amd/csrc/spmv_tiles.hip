@@ -20,6 +20,8 @@
 // device scalar is read after being written inside one kernel.
 #include <algorithm>
 
+#include <hip/hip_ext.h>
+
 #include "cwf_internal.hpp"
 
 namespace cwf
@@ -1178,18 +1180,29 @@ unsigned pipe_grid_query(const DevSys &s)
     return g < need ? g : (need ? need : 8u);
 }
 
+// e0/e1 (optional): hipExtLaunchKernel stamps them from the dispatch packet itself, so the timed
+// interval is the kernel's own execution (what rocprofv3 --kernel-trace reports), not marker latency
 template <bool ISO, bool SAN, int MODE>
-void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st)
+void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st,
+                  hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
     if (s.t.pipe)
     {
-        k_keff_tiles_pipe<ISO, SAN, MODE><<<s.t.pipe_grid, 256, tiles_lds(s), st>>>(s, x, pa);
+        if (e0 && e1)
+            hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE>, dim3(s.t.pipe_grid), dim3(256),
+                                  (uint32_t)tiles_lds(s), st, e0, e1, 0, s, x, pa);
+        else
+            k_keff_tiles_pipe<ISO, SAN, MODE><<<s.t.pipe_grid, 256, tiles_lds(s), st>>>(s, x, pa);
         return;
     }
+    if (e0)
+        (void)hipEventRecord(e0, st);
     if (s.t.geo)
         launch_tiles_g<ISO, SAN, MODE, true>(s, x, pa, nt, st);
     else
         launch_tiles_g<ISO, SAN, MODE, false>(s, x, pa, nt, st);
+    if (e1)
+        (void)hipEventRecord(e1, st);
 }
 }  // namespace
 
@@ -1236,7 +1249,7 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
 }
 
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
-void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
+void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
     const DevSys &s = h->ds;
     if (!s.t.ntiles)
@@ -1245,21 +1258,26 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
         const char *e = getenv("CWF_ABLATE");
         return e ? (unsigned)atoi(e) : 0u;
     }();
-    // beta / convergence from the folded per-rank {r.r, r.z} pairs (one pair on a single GPU)
-    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it,
-               h->hist, abl};
+    // beta / convergence: a single handle folds the update kernel's per-workgroup {r.r, r.z} shares
+    // directly; a shard reads the all-gathered per-rank pairs
+    PcgArgs pa = fast_direct_fold(h)
+                     ? PcgArgs{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->part1, h->part2,
+                               fast_update_blocks(s), 1u, it, h->hist, abl}
+                     : PcgArgs{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
+                               (unsigned)h->nranks, 2u, it, h->hist, abl};
     if (s.iso)
-        launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
+        launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st, e0, e1);
     else
-        launch_tiles<false, false, 1>(s, h->p, pa, tile_threads(), st);
+        launch_tiles<false, false, 1>(s, h->p, pa, tile_threads(), st, e0, e1);
 }
 
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(s, rhs, h->inv6, h->x, h->r, h->z, h->p, h->ctl,
-                                                                      h->g_pap, (unsigned)h->nranks, h->part1,
-                                                                      h->part2, it);
+    const bool direct = fast_direct_fold(h);
+    k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
+        s, rhs, h->inv6, h->x, h->r, h->z, h->p, h->ctl, direct ? h->part0 : h->g_pap,
+        direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it);
 }
 
 // diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
@@ -1274,7 +1292,10 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
 
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
-    k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
+    if (fast_direct_fold(h))
+        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->part1, h->part2, fast_update_blocks(h->ds), 1u, it, h->hist);
+    else
+        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
 }
 
 void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
@@ -1289,13 +1310,29 @@ void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStr
     k_fold_pair<<<1, 1024, 0, st>>>(a, b, n, out);
 }
 
+// a single (unsharded) handle skips the per-rank fold kernels: every consumer workgroup refolds the
+// producer's per-workgroup shares itself (<= 2048 doubles, L2-served), two launches fewer per iteration.
+// CWF_FOLD=kernel keeps the fold kernels (A/B diagnostic).
+bool fast_direct_fold(const cwf_hip_system *h)
+{
+    static const bool kernel_fold = [] {
+        const char *e = getenv("CWF_FOLD");
+        return e && std::string(e) == "kernel";
+    }();
+    return !h->sharded() && !kernel_fold;
+}
+
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st)
 {
+    if (fast_direct_fold(h))
+        return;
     fold_pair(h->part0, nullptr, fast_tile_blocks(h->ds), h->g_pap + h->rank, st);
 }
 
 void fast_fold_rrz(cwf_hip_system *h, hipStream_t st)
 {
+    if (fast_direct_fold(h))
+        return;
     fold_pair(h->part1, h->part2, fast_update_blocks(h->ds), h->g_rrz + 2 * h->rank, st);
 }
 

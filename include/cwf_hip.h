@@ -136,7 +136,8 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
 /* Live kernel timing (measurement support, not a reference interface): when enabled, every
  * K_eff launch inside solve_pcg / stepper_step is bracketed by hipEvents on the handle's stream;
  * cwf_hip_system_timing returns the summed device time (ms) and launch count of the launches that
- * did work, and resets the accumulators. */
+ * did work, and resets the accumulators. `enabled` > 1 samples every enabled-th launch (iteration
+ * index multiple of it), so the event markers do not sit between every pair of kernels. */
 int cwf_hip_system_set_timing(cwf_hip_system *h, int enabled);
 int cwf_hip_system_timing(cwf_hip_system *h, double *keff_ms, uint64_t *keff_launches);
 /* Standalone timed K_eff: `reps` launches of the PCG-loop SpMV (no sanitize) on device x -> y,
