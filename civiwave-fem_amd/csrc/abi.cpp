@@ -476,24 +476,26 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     if (E)
     {
         HostTiles ht;
-        try
-        {
-            build_tiles(d, ht);
-        }
-        catch (const std::bad_alloc &)
-        {
-            return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
-        }
         DevTiles &t = s.t;
         // GEO: stream 8-B corner ids + tile-node coordinates and recompute gradients/volume on the fly,
         // when the desc carries coordinates that reproduce its gradients (CWF_GEO=0 forces the records)
         const char *ge = getenv("CWF_GEO");
-        t.geo = (!ge || ge[0] != '0') && !ht.tcoord[0].empty() && geometry_matches(d) ? 1 : 0;
+        t.geo = (!ge || ge[0] != '0') && d->node_coords && N && geometry_matches(d) ? 1 : 0;
         {
             const char *fo = getenv("CWF_TILE_FOLD");
             t.acc = fo && fo[0] == 'a' ? 1 : 0;
             const char *pp = getenv("CWF_TILE_PIPE");
             t.pipe = t.geo && !t.acc && !(pp && pp[0] == '0') ? 1 : 0;
+        }
+        try
+        {
+            build_tiles(d, ht, t.pipe ? 256u : (uint32_t)kMaxTileNodes);
+        }
+        catch (const std::bad_alloc &)
+        {
+            return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
+        }
+        {
             uint32_t deg = 1;
             for (size_t q = 0; q + 1 < ht.csr_off.size(); ++q)
                 deg = std::max(deg, ht.csr_off[q + 1] - ht.csr_off[q]);
@@ -564,7 +566,15 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (int st = upload(h, &ps, ht.node_part_slot.data(), ht.node_part_slot.size()))
             return bail(st);
         t.part_slot = ps;
-        if (int st = dalloc(h, &part, 3 * ht.tile_nodes.size()))
+        if (t.pipe)
+        {
+            uint32_t *tsl;
+            if (int st = upload(h, &tsl, ht.tile_slot.data(), ht.tile_slot.size()))
+                return bail(st);
+            t.tslot = tsl;
+            t.node_major = 1;
+        }
+        if (int st = dalloc(h, &part, 3 * (ht.tile_nodes.size() + 2)))  // + 2 padding slots (update pass)
             return bail(st);
         t.ntiles = ht.ntiles;
         t.max_tile_nodes = ht.max_tile_nodes;

@@ -48,6 +48,10 @@ struct DevTiles
     const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
     const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile)
     const uint32_t *part_slot = nullptr;      // [total] partial index of each of those slots
+    // pipelined kernel: partials stored node-major (tile node q -> part[3 tslot[q]]), so a node's partials
+    // are the contiguous run part[3 node_part_off[n] .. 3 node_part_off[n+1]) and part_slot is not read
+    const uint32_t *tslot = nullptr;
+    int node_major = 0;
     float *part = nullptr;                    // [3*total] tile-node partial sums, node-major (scratch)
 };
 
@@ -63,7 +67,8 @@ struct HostTiles
     std::vector<float> tcoord[3];  // [total] tile-relative coordinates (when node_coords are given)
 };
 
-int build_tiles(const cwf_system_desc *d, HostTiles &out);
+// max_nodes: distinct nodes per tile (kMaxTileNodes; the pipelined kernel keeps one node per lane: 256)
+int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes = kMaxTileNodes);
 // true when the supplied gradients / volumes are those of the supplied node coordinates (so FAST may
 // recompute them on the fly instead of streaming them)
 bool geometry_matches(const cwf_system_desc *d);

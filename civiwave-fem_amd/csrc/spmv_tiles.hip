@@ -29,8 +29,8 @@ namespace cwf
 namespace
 {
 constexpr int kMaxM = 16;
-constexpr int kUpdThreads = 1024;
-constexpr unsigned kMaxUpdateBlocks = 2048;  // 2 resident per CU; shares folded once by k_fold_pair
+constexpr int kUpdThreads = 256;
+constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -321,6 +321,85 @@ struct PcgArgs
     double *hist;
     unsigned abl;  // diagnostic ablation bits (CWF_ABLATE), 0 in normal runs
 };
+
+// Pipelined-kernel element body (GEO). With edge columns c_k = x_k - x_0 and r_k their cofactor rows
+// (r_1 = c_2 x c_3, ...), the gradients are g_a = r_a / det and V = |det| / 6, so
+//   f_a = V B(g_a)^T D B(g) u = B(r_a)^T D (sum_b B(r_b) u_b) * s_K / (6 |det|):
+// the strain is built from the unscaled r_a and ONE scale lands on the 6 stresses (no per-gradient
+// division, no per-force volume multiply). FAST arithmetic: FMA contractions and the hardware
+// reciprocal (1 ulp), tolerance-checked against the oracle.
+template <bool ISO>
+__device__ __forceinline__ void geo_element_forces(const DevSys &s, uint2 id, const float4 *sxp, const float2 *sq,
+                                                   float sK6, uint32_t mi, const float *dtab, float f[12])
+{
+    constexpr int kTab = ISO ? 12 : 36;
+    const uint32_t li[4] = {id.x & 0xffffu, id.x >> 16, id.y & 0xffffu, id.y >> 16};
+    // one ds_read_b128 {x, y, z, p_x} + one ds_read_b64 {p_y, p_z} per corner
+    float4 X[4];
+    float2 Q[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        X[a] = sxp[li[a]];
+        Q[a] = sq[li[a]];
+    }
+    float c[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        c[k][0] = X[k + 1].x - X[0].x;
+        c[k][1] = X[k + 1].y - X[0].y;
+        c[k][2] = X[k + 1].z - X[0].z;
+    }
+    float g[4][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        const float *u = c[(k + 1) % 3], *v = c[(k + 2) % 3];
+        g[k + 1][0] = fmaf(u[1], v[2], -u[2] * v[1]);
+        g[k + 1][1] = fmaf(u[2], v[0], -u[0] * v[2]);
+        g[k + 1][2] = fmaf(u[0], v[1], -u[1] * v[0]);
+    }
+    const float det = fmaf(c[0][0], g[1][0], fmaf(c[0][1], g[1][1], c[0][2] * g[1][2]));
+    const float scale = sK6 * __builtin_amdgcn_rcpf(fabsf(det));
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+        g[0][q] = -(g[1][q] + g[2][q] + g[3][q]);
+    float eps[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        const float u0 = X[a].w, u1 = Q[a].x, u2 = Q[a].y;
+        const float gx = g[a][0], gy = g[a][1], gz = g[a][2];
+        eps[0] = fmaf(gx, u0, eps[0]);
+        eps[1] = fmaf(gy, u1, eps[1]);
+        eps[2] = fmaf(gz, u2, eps[2]);
+        eps[3] = fmaf(gx, u1, fmaf(gy, u0, eps[3]));
+        eps[4] = fmaf(gy, u2, fmaf(gz, u1, eps[4]));
+        eps[5] = fmaf(gx, u2, fmaf(gz, u0, eps[5]));
+    }
+    float sig[6];
+    if (mi < (uint32_t)kMaxM)
+        stress_f32<ISO>(dtab + kTab * mi, eps, sig);
+    else
+    {
+        float tab[36];
+        for (int t = 0; t < kTab; ++t)
+            tab[t] = (float)s.dmat[36u * mi + dsrc(ISO, t)];
+        stress_f32<ISO>(tab, eps, sig);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+        sig[r] *= scale;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        const float ax = g[a][0], ay = g[a][1], az = g[a][2];
+        f[3 * a + 0] = fmaf(az, sig[5], fmaf(ay, sig[3], ax * sig[0]));
+        f[3 * a + 1] = fmaf(az, sig[4], fmaf(ax, sig[3], ay * sig[1]));
+        f[3 * a + 2] = fmaf(ax, sig[5], fmaf(ay, sig[4], az * sig[2]));
+    }
+}
 
 // MODE 0: apply (gather x, optional sanitize); MODE 1: PCG (gather z, p_old -> p_new).
 // GEO: 8-B element records + per-tile-node coordinates (geometry recomputed); else 48-B records.
@@ -736,8 +815,11 @@ struct PipeNext
     uint2 tn;          // record of tile node threadIdx.x
     float c[3];        // its coordinates
     float v[3], w[3];  // x / p_old and z (MODE 1) at that node
+    float m;           // its lumped mass (MODE 1: the owner slot's m s_M |p|^2 share of p.Ap)
     uint2 id[2];       // corner ids of elements threadIdx.x, threadIdx.x + 256
     uint4 csr;         // 8 local-CSR entries (16 B) of the tile
+    uint32_t slot;     // node-major partial slot of tile node threadIdx.x
+    uint32_t mat[2];   // material of elements threadIdx.x, threadIdx.x + 256 (0 when M == 1)
 };
 
 template <bool SANITIZE, int MODE>
@@ -747,6 +829,7 @@ __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, Pi
     const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
     const uint32_t i = threadIdx.x;
     n.tn = i < nn ? T.tnode[nb + i] : uint2{0u, 0u};
+    n.slot = i < nn ? T.tslot[nb + i] : 0u;
     const uint32_t T3 = T.total_tile_nodes;
     const uint32_t q = nb + (i < nn ? i : 0u);
     n.c[0] = T.tcoord[q];
@@ -757,6 +840,9 @@ __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, Pi
     {
         const uint32_t j = i + k * 256u;
         n.id[k] = T.eid[e0 + (j < ne ? j : 0u)];
+        // prefetched with the records: a load inside the element phase would make its wait drain
+        // every record load in flight for the next tile
+        n.mat[k] = T.mat ? T.mat[e0 + (j < ne ? j : 0u)] : 0u;
     }
     const uint4 *src = reinterpret_cast<const uint4 *>(T.csr_ent + 4ull * e0);  // 4 ne u16 = ne / 2 uint4
     n.csr = i < (ne + 1) / 2 ? src[i] : uint4{0u, 0u, 0u, 0u};
@@ -767,6 +853,7 @@ __device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *
                                                   const float *__restrict__ z, uint32_t nn, PipeNext &n)
 {
     const uint32_t g = n.tn.x & 0x7fffffffu;  // node 0 for idle lanes (harmless, in range)
+    n.m = 0.f;
     (void)nn;
     n.v[0] = x[3u * g + 0];
     n.v[1] = x[3u * g + 1];
@@ -776,6 +863,7 @@ __device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *
         n.w[0] = z[3u * g + 0];
         n.w[1] = z[3u * g + 1];
         n.w[2] = z[3u * g + 2];
+        n.m = s.mass[g];
     }
     else if constexpr (SANITIZE)
     {
@@ -787,7 +875,8 @@ __device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *
 }
 
 template <bool ISO, bool SANITIZE, int MODE>
-__global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa)
+__global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
+                                                         const uint4 *__restrict__ hdr)
 {
     constexpr int NT = 256;
     constexpr int kTab = ISO ? 12 : 36;
@@ -796,8 +885,8 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
     const uint32_t ms = T.max_tile_nodes;
     float *sf = lds;                                                     // [12][kTileElems]
     uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * kTileElems);  // [4*kTileElems] local CSR
-    float *sp = lds + 14 * kTileElems;                                   // [3][ms] node values
-    float *sx = sp + 3 * ms;                                             // [3][ms] node coordinates
+    float4 *sxp = reinterpret_cast<float4 *>(lds + 14 * kTileElems);     // [ms] {x, y, z, v_x}
+    float2 *sq = reinterpret_cast<float2 *>(sxp + ms);                   // [ms] {v_y, v_z}
     __shared__ float dtab[kMaxM * kTab];
     __shared__ double red[NT / 64];
     if constexpr (MODE == 1)
@@ -810,7 +899,9 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
     const uint32_t t_end = (uint32_t)(((uint64_t)(xcd + 1) * T.ntiles) / nxcd);
     uint32_t t = (uint32_t)(((uint64_t)xcd * T.ntiles) / nxcd) + lb;
     PipeNext cur;
-    uint4 hd = t < t_end ? T.hdr[t] : uint4{0u, 0u, 0u, 0u};
+    uint4 hd = t < t_end ? hdr[t] : uint4{0u, 0u, 0u, 0u};
+    // header of the tile after next, loaded one tile early so phase (b) never waits on it
+    uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
     if (t < t_end)
     {
         pipe_issue_records<SANITIZE, MODE>(s, hd, cur);
@@ -826,11 +917,11 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
         if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta, pa.abl & 32u))
             return;
     }
-    const float sK = (float)s.sK, sM = (float)s.sM;
+    const float sK6 = (float)(s.sK / 6.0), sM = (float)s.sM;
     double pap = 0.0;
     for (; t < t_end; t += nbx)
     {
-        const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
+        const uint32_t ne = hd.y, nn = hd.w;
         // (a) LDS fill of tile t from the prefetched registers (second node slot, if any, loads directly)
         const uint32_t i0 = threadIdx.x;
         if (i0 < nn)
@@ -842,60 +933,46 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
                 v1 = fmaf(beta, v1, cur.w[1]);
                 v2 = fmaf(beta, v2, cur.w[2]);
             }
-            sp[i0] = v0;
-            sp[ms + i0] = v1;
-            sp[2 * ms + i0] = v2;
-            sx[i0] = cur.c[0];
-            sx[ms + i0] = cur.c[1];
-            sx[2 * ms + i0] = cur.c[2];
-        }
-        for (uint32_t i = i0 + NT; i < nn; i += NT)
-        {
-            const uint2 tn = T.tnode[nb + i];
-            float u[3];
-            gather_node<SANITIZE, MODE>(s, x, pa.z, beta, tn.x & 0x7fffffffu, u);
-            sp[i] = u[0];
-            sp[ms + i] = u[1];
-            sp[2 * ms + i] = u[2];
-            const uint32_t T3 = T.total_tile_nodes;
-            sx[i] = T.tcoord[nb + i];
-            sx[ms + i] = T.tcoord[T3 + nb + i];
-            sx[2 * ms + i] = T.tcoord[2 * T3 + nb + i];
+            sxp[i0] = float4{cur.c[0], cur.c[1], cur.c[2], v0};
+            sq[i0] = float2{v1, v2};
         }
         if (i0 < (ne + 1) / 2)
             reinterpret_cast<uint4 *>(sc)[i0] = cur.csr;
-        const uint2 tn_own = cur.tn;
         const uint2 id0 = cur.id[0], id1 = cur.id[1];
+        const uint32_t mat0 = cur.mat[0], mat1 = cur.mat[1];
+        const uint2 tn_own = cur.tn;
+        const uint32_t slot_own = cur.slot;
+        const float m_own = cur.m;
         __syncthreads();
         // (b) next tile's records in flight during this tile's element and fold work
         const uint32_t tn_next = t + nbx;
-        uint4 hdn = uint4{0u, 0u, 0u, 0u};
+        const uint4 hdn = hd2;
         if (tn_next < t_end)
-        {
-            hdn = T.hdr[tn_next];
             pipe_issue_records<SANITIZE, MODE>(s, hdn, cur);
-        }
-        // (c) elements of tile t
+        hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
+        // (c) elements of tile t (ablation bit 64: skipped, diagnostic timing only)
 #pragma unroll
         for (int k = 0; k < 2; ++k)
         {
             const uint32_t j = threadIdx.x + k * NT;
-            if (j < ne)
+            if (j < ne && !(pa.abl & 64u))
             {
-                float g[12], vol;
-                uint32_t li[4];
-                coord_geometry(k ? id1 : id0, sx, ms, g, li, &vol);
-                element_forces<ISO>(s, g, li, vol * sK, T.mat ? T.mat[e0 + j] : 0u, j, sp, ms, dtab, sf);
+                float f[12];
+                geo_element_forces<ISO>(s, k ? id1 : id0, sxp, sq, sK6, k ? mat1 : mat0, dtab, f);
+#pragma unroll
+                for (int c = 0; c < 12; ++c)
+                    sf[c * kTileElems + j] = f[c];
             }
         }
         __syncthreads();
-        // (d) next tile's gathers (its node records have arrived by now)
-        if (tn_next < t_end)
+        // (d) next tile's gathers (its node records have arrived by now; ablation bit 256: skipped)
+        if (tn_next < t_end && !(pa.abl & 256u))
             pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hdn.w, cur);
-        // (e) fold per tile node -> tile-major partials (+ p.Ap)
-        for (uint32_t i = threadIdx.x; i < nn; i += NT)
+        // (e) fold per tile node -> node-major partials (+ p.Ap) (ablation bit 128: skipped)
+        if (threadIdx.x < ((pa.abl & 128u) ? 0u : nn))  // nn <= 256: one tile node per lane
         {
-            const uint2 tn = i == threadIdx.x ? tn_own : T.tnode[nb + i];
+            const uint32_t i = threadIdx.x;
+            const uint2 tn = tn_own;
             float a0 = 0.f, a1 = 0.f, a2 = 0.f;
             const uint32_t qe = tn.y >> 16;
             uint32_t q = tn.y & 0xffffu;
@@ -930,17 +1007,21 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
                 a1 += sf[(c + 1) * kTileElems + el];
                 a2 += sf[(c + 2) * kTileElems + el];
             }
-            float *o = T.part + 3ull * (nb + i);
-            o[0] = a0;
-            o[1] = a1;
-            o[2] = a2;
+            // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
+            if (!(pa.abl & 512u))
+            {
+                float *o = T.part + 3ull * ((pa.abl & 1024u) ? hd.z + i : slot_own);
+                o[0] = a0;
+                o[1] = a1;
+                o[2] = a2;
+            }
             if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
             {
-                const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
+                const float p0 = sxp[i].w, p1 = sq[i].x, p2 = sq[i].y;
                 pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
                 if (tn.x & 0x80000000u)  // the node's owner slot adds its mass term m s_M |p|^2 once
                 {
-                    const float m = s.mass[tn.x & 0x7fffffffu] * sM;
+                    const float m = m_own * sM;
                     pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
                            (double)(m * p2) * (double)p2;
                 }
@@ -1028,7 +1109,7 @@ __global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
     {
-        const float *pp = T.part + 3ull * T.part_slot[q];
+        const float *pp = T.part + 3ull * (T.node_major ? q : T.part_slot[q]);
         a0 += pp[0];
         a1 += pp[1];
         a2 += pp[2];
@@ -1086,39 +1167,79 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
                 p[3u * n + k] = fmaf(beta, p[3u * n + k], z[3u * n + k]);
             continue;
         }
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-        for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
-        {
-            const float *pp = T.part + 3ull * T.part_slot[q];
-            a0 += pp[0];
-            a1 += pp[1];
-            a2 += pp[2];
-        }
+        // every independent load first: the partial run [q0, q1) (node-major: contiguous, no slot
+        // indirection) and the node's vectors are in flight together
+        const uint32_t q0 = T.node_part_off[n], q1 = T.node_part_off[n + 1];
         const uint32_t mk = s.mask[n];
         const float m = s.mass[n] * sM;
+        float pv[3], zv[3], xv[3], rv0[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+        {
+            pv[k] = p[3u * n + k];
+            zv[k] = z[3u * n + k];
+            xv[k] = x[3u * n + k];
+            rv0[k] = r[3u * n + k];
+        }
+        const float2 *i2 = reinterpret_cast<const float2 *>(inv + 6ull * n);
+        const float2 u0 = i2[0], u1 = i2[1], u2 = i2[2];
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+        if (T.node_major)
+        {
+            const float *pp = T.part + 3ull * q0;
+            const uint32_t cnt = q1 - q0;
+            // first two partials unconditionally in flight (the part buffer carries 2 padding slots, so
+            // the reads stay in bounds for a node with fewer; unused values are masked below)
+            const float b0 = pp[0], b1 = pp[1], b2 = pp[2];
+            const float c0 = pp[3], c1 = pp[4], c2 = pp[5];
+            if (cnt > 0)
+            {
+                a0 = b0;
+                a1 = b1;
+                a2 = b2;
+            }
+            if (cnt > 1)
+            {
+                a0 += c0;
+                a1 += c1;
+                a2 += c2;
+            }
+            for (uint32_t q = 2; q < cnt; ++q)
+            {
+                a0 += pp[3 * q + 0];
+                a1 += pp[3 * q + 1];
+                a2 += pp[3 * q + 2];
+            }
+        }
+        else
+            for (uint32_t q = q0; q < q1; ++q)
+            {
+                const float *pp = T.part + 3ull * T.part_slot[q];
+                a0 += pp[0];
+                a1 += pp[1];
+                a2 += pp[2];
+            }
         const float av[3] = {a0, a1, a2};
         float rv[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
             const uint32_t d = 3u * n + k;
-            const float pk = fmaf(beta, p[d], z[d]);  // same expression as the tiles gather
+            const float pk = fmaf(beta, pv[k], zv[k]);  // same expression as the tiles gather
             const float apk = (mk & (1u << k)) ? pk : fmaf(m, pk, av[k]);
-            float xv = fmaf(alpha, pk, x[d]);
-            float rw = fmaf(-alpha, apk, r[d]);
+            float xn = fmaf(alpha, pk, xv[k]);
+            float rw = fmaf(-alpha, apk, rv0[k]);
             if (mk & (1u << k))
             {
-                xv = rhs[d];
+                xn = rhs[d];
                 rw = 0.0f;
             }
-            x[d] = xv;
+            x[d] = xn;
             r[d] = rw;
             p[d] = pk;
             rv[k] = rw;
         }
         // symmetric block inverse, 6 floats per node {a00 a01 a02 a11 a12 a22} (three 8-B loads)
-        const float2 *i2 = reinterpret_cast<const float2 *>(inv + 6ull * n);
-        const float2 u0 = i2[0], u1 = i2[1], u2 = i2[2];
         const float iv[9] = {u0.x, u0.y, u1.x, u0.y, u1.y, u2.x, u1.x, u2.x, u2.y};
 #pragma unroll
         for (int k = 0; k < 3; ++k)
@@ -1167,13 +1288,20 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
         k_keff_tiles<ISO, SAN, MODE, 256, GEO><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
 }
 
+// pipelined kernel: element forces + local CSR + per tile node {x y z v_x}{v_y v_z}
+inline size_t pipe_lds(const DevSys &s)
+{
+    const size_t ms = s.t.max_tile_nodes;
+    return sizeof(float) * 14 * kTileElems + ms * (16 + 8);
+}
+
 template <bool ISO>
 unsigned pipe_grid_query(const DevSys &s)
 {
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1>, 256, tiles_lds(s));
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1>, 256, pipe_lds(s));
     unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     g = g < 8u ? 8u : g - g % 8u;  // whole XCD groups
     const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
@@ -1190,9 +1318,9 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
     {
         if (e0 && e1)
             hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE>, dim3(s.t.pipe_grid), dim3(256),
-                                  (uint32_t)tiles_lds(s), st, e0, e1, 0, s, x, pa);
+                                  (uint32_t)pipe_lds(s), st, e0, e1, 0, s, x, pa, s.t.hdr);
         else
-            k_keff_tiles_pipe<ISO, SAN, MODE><<<s.t.pipe_grid, 256, tiles_lds(s), st>>>(s, x, pa);
+            k_keff_tiles_pipe<ISO, SAN, MODE><<<s.t.pipe_grid, 256, pipe_lds(s), st>>>(s, x, pa, s.t.hdr);
         return;
     }
     if (e0)
@@ -1209,10 +1337,20 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
 unsigned fast_tile_blocks(const DevSys &s) { return s.t.pipe ? s.t.pipe_grid : s.t.ntiles; }
 
 unsigned fast_pipe_grid(const DevSys &s) { return s.iso ? pipe_grid_query<true>(s) : pipe_grid_query<false>(s); }
+// the update pass is grid-stride: at most one resident wave of workgroups (occupancy x CUs), so no
+// workgroup waits for a slot behind the others' whole node ranges
 unsigned fast_update_blocks(const DevSys &s)
 {
+    static const unsigned resident = [] {
+        int dev = 0, bpc = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles, kUpdThreads, 0);
+        const unsigned r = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
+        return r < kMaxUpdateBlocks ? r : kMaxUpdateBlocks;
+    }();
     const unsigned g = grid_for(s.N, kUpdThreads);
-    return g < kMaxUpdateBlocks ? (g ? g : 1u) : kMaxUpdateBlocks;
+    return g < resident ? (g ? g : 1u) : resident;
 }
 
 static int tile_threads()

@@ -36,7 +36,7 @@ inline uint64_t spread21(uint64_t v)
 }
 }  // namespace
 
-int build_tiles(const cwf_system_desc *d, HostTiles &out)
+int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes)
 {
     const uint64_t N = d->node_count, E = d->element_count;
     std::vector<uint32_t> order(E);
@@ -95,7 +95,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out)
             uint32_t add = 0;
             for (int a = 0; a < 4; ++a)
                 add += stamp[d->element_connectivity[(uint64_t)src * 8 + a]] != tile ? 1u : 0u;
-            if (nodes.size() + add > (size_t)kMaxTileNodes)
+            if (nodes.size() + add > (size_t)max_nodes)
                 break;
             for (int a = 0; a < 4; ++a)
             {

@@ -1,6 +1,18 @@
+#!/bin/bash
+# Full GPU evidence pass: parity suite, default bench line (C2, with CPU baseline), C3 line, rocprofv3
+# kernel-trace + FETCH/WRITE PMC passes over the C2 bench, summaries under gpurun_out/round/.
+# usage: bash tools/gpu_round.sh TAG
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && tail -3 gpurun_out/gpu_tests.log &&
-timeout -k 10 300 python -u bench.py > gpurun_out/bench_c2.log 2>&1 && tail -1 gpurun_out/bench_c2.log &&
-timeout -k 10 300 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_c3.log 2>&1 && tail -1 gpurun_out/bench_c3.log &&
-NO_PMC= bash tools/profile.sh c2 --steps 5 --warmup 1 --no-cpu-baseline && python tools/pmc_summary.py gpurun_out/prof_c2 --kernel keff_tiles --json gpurun_out/prof_c2/pmc.json > gpurun_out/prof_c2/summary.txt; cat gpurun_out/prof_c2/summary.txt
+TAG=${1:-r01}
+O=gpurun_out/round
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/${TAG}_gpu_tests.log 2>&1; tail -1 $O/${TAG}_gpu_tests.log
+timeout -k 10 300 python -u bench.py > $O/${TAG}_bench_c2.log 2>&1 && tail -1 $O/${TAG}_bench_c2.log > $O/${TAG}_bench_c2_fast.json &&
+timeout -k 10 300 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_c3.log 2>&1 && tail -1 $O/${TAG}_bench_c3.log > $O/${TAG}_bench_c3_fast.json &&
+bash tools/profile.sh c2 --steps 5 --warmup 1 --no-cpu-baseline > $O/${TAG}_profile.log 2>&1 &&
+python3 tools/pmc_summary.py gpurun_out/prof_c2 --kernel "k_keff_tiles_pipe<true, false, 1>" --json $O/${TAG}_c2_fast_pmc.json > $O/${TAG}_c2_fast_summary.txt &&
+cp gpurun_out/prof_c2/kt/kt_kernel_stats.csv $O/${TAG}_c2_fast_kernel_stats.csv && tail -1 gpurun_out/prof_c2/bench_kt.log > $O/${TAG}_c2_bench_under_rocprof.json
+rc=$?
+rm -rf gpurun_out/prof_c2
+cat $O/${TAG}_c2_fast_summary.txt | head -8
+exit $rc
