@@ -11,7 +11,7 @@ timeout -k 10 300 python -u bench.py > $O/${TAG}_bench_c2.log 2>&1 && tail -1 $O
 timeout -k 10 300 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_c3.log 2>&1 && tail -1 $O/${TAG}_bench_c3.log > $O/${TAG}_bench_c3_fast.json &&
 bash tools/profile.sh c2 --steps 5 --warmup 1 --no-cpu-baseline > $O/${TAG}_profile.log 2>&1 &&
 python3 tools/pmc_summary.py gpurun_out/prof_c2 --kernel "k_keff_tiles_pipe<true, false, 1>" --json $O/${TAG}_c2_fast_pmc.json > $O/${TAG}_c2_fast_summary.txt &&
-cp gpurun_out/prof_c2/kt/kt_kernel_stats.csv $O/${TAG}_c2_fast_kernel_stats.csv && tail -1 gpurun_out/prof_c2/bench_kt.log > $O/${TAG}_c2_bench_under_rocprof.json
+cp gpurun_out/prof_c2/kt/kt_kernel_stats.csv $O/${TAG}_c2_fast_kernel_stats.csv && grep "^{\"metric" gpurun_out/prof_c2/bench_kt.log > $O/${TAG}_c2_bench_under_rocprof.json
 rc=$?
 rm -rf gpurun_out/prof_c2
 cat $O/${TAG}_c2_fast_summary.txt | head -8
