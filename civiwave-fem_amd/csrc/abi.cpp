@@ -736,6 +736,46 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
     return 0;
 }
 
+int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_kind, float *elements,
+                           float *nodes, int out_kind)
+{
+    if (int st = check_ready(h))
+        return st;
+    if (!u || (!elements && !nodes))
+        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "displacement span size mismatch",
+                         "input=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+    const float *uin = nullptr;
+    if (int st = stage_in(h, u, h->tmp, n, u_kind, &uin))
+        return st;
+    const uint64_t ne = 13ull * h->ds.E, nn = 13ull * h->ds.N;
+    float *de = elements, *dn = nodes;
+    if (out_kind != CWF_PTR_DEVICE)  // host outputs: stage through one scratch allocation
+    {
+        float *scratch = nullptr;
+        HIPTRY(h, hipMalloc(reinterpret_cast<void **>(&scratch), (ne + nn + 1) * sizeof(float)));
+        de = elements ? scratch : nullptr;
+        dn = nodes ? scratch + ne : nullptr;
+        derived_fields(h, uin, de, dn, h->stream);
+        hipError_t e1 = hipGetLastError();
+        if (e1 == hipSuccess && elements)
+            e1 = hipMemcpyAsync(elements, de, ne * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+        if (e1 == hipSuccess && nodes)
+            e1 = hipMemcpyAsync(nodes, dn, nn * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+        if (e1 == hipSuccess)
+            e1 = hipStreamSynchronize(h->stream);
+        (void)hipFree(scratch);
+        if (e1 != hipSuccess)
+            return hip_fail(h, e1, "derived fields");
+        return 0;
+    }
+    derived_fields(h, uin, de, dn, h->stream);
+    HIPTRY(h, hipGetLastError());
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
 int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, int kind)
 {
     if (int st = check_ready(h))

@@ -210,6 +210,8 @@ unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
 unsigned fast_update_blocks(const DevSys &s);
 // sharded FAST PCG (comm.cpp orchestrates, spmv_tiles.hip / kernels_fast.hip launch)
+// post.hip: derived fields (derived_fields.cpp:139-211) -> f32 [13 E] / [13 N] (either may be NULL)
+void derived_fields(cwf_hip_system *h, const float *u, float *elem_out, float *node_out, hipStream_t st);
 bool fast_direct_fold(const cwf_hip_system *h);  // unsharded: consumers fold per-workgroup shares
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> g_pap[rank]
 void fast_fold_rrz(cwf_hip_system *h, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]

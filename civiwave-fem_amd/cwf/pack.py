@@ -78,6 +78,15 @@ class PackingResult:
     element_indices: np.ndarray  # u32 [4E]
     local_indices: np.ndarray  # u8 [4E]
     position64: np.ndarray | None = None  # f64 [N,3] the preprocess input (FAST tiles: order + geometry)
+    # nodes.displacement / velocity / acceleration (pack.hpp:95-105), f32 [3N]; the post stack reads them
+    displacement: np.ndarray | None = None
+    velocity: np.ndarray | None = None
+    acceleration: np.ndarray | None = None
+
+    def __post_init__(self):
+        for name in ("displacement", "velocity", "acceleration"):
+            if getattr(self, name) is None:
+                setattr(self, name, np.zeros(3 * self.node_count, np.float32))
 
 
 def _group_nodes(mesh: Mesh, gid: int) -> np.ndarray:

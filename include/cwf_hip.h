@@ -43,7 +43,10 @@ typedef enum cwf_status
     CWF_ERR_HIP = -10,           /* HIP runtime error (message holds hipGetErrorString) */
     CWF_ERR_ARGUMENT = -11,      /* NULL handle / pointer */
     CWF_ERR_COMM = -12,          /* RCCL / communicator failure */
-    CWF_ERR_UNSUPPORTED = -13
+    CWF_ERR_UNSUPPORTED = -13,
+    CWF_ERR_IO = -14,            /* vtu_writer.cpp / probe_logger.cpp / config / mesh file errors */
+    CWF_ERR_INDEX = -15,         /* probe_logger.cpp:116-119 "probe index out of range" */
+    CWF_ERR_PARSE = -16          /* config.cpp / mesh.cpp parse and validation errors */
 } cwf_status;
 
 typedef enum cwf_ptr_kind
@@ -278,6 +281,43 @@ int cwf_preprocess_tets(uint64_t node_count, uint64_t element_count, const doubl
                         const uint32_t *material_index, const double *density, uint64_t material_count,
                         float *grads24, float *volume, double *mass64, float *mass32, uint32_t *offsets,
                         uint32_t *adj_elem, uint8_t *adj_local, uint32_t *conn8);
+
+/* ---- post stack ---------------------------------------------------------- */
+
+/* cwf::post::compute_derived_fields (src/post/derived_fields.cpp:139-211), on the device and bit-exact:
+ * u = displacement f32 [3N] node-interleaved (n = dof_count); outputs are 13 floats per element /
+ * node {strain[6] (Voigt, engineering shear), stress[6], von_mises} -- the memory layout of
+ * cwf::post::ElementField / NodeField (derived_fields.hpp:37-55). `elements` [13E] or `nodes` [13N] may
+ * be NULL. */
+int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_kind, float *elements,
+                           float *nodes, int out_kind);
+
+/* One output frame, host memory (the PackingResult node buffers + DerivedFieldSet the reference
+ * writers read). Vectors are node-interleaved f32 [3N]; connectivity is the packed u32 [8E] with
+ * UINT32_MAX padding (4 valid slots = tet4 / VTK 10, otherwise hex8 / VTK 12). */
+typedef struct cwf_frame_view
+{
+    uint64_t node_count;
+    uint64_t element_count;
+    const float *position0;      /* pack.hpp:96 Float3SoA position0 (f32) */
+    const float *displacement;
+    const float *velocity;
+    const float *acceleration;
+    const float *element_fields; /* [13E] */
+    const float *node_fields;    /* [13N] */
+    const uint32_t *connectivity;
+} cwf_frame_view;
+
+/* cwf::post::write_vtu (vtu_writer.cpp:171-297): binary-appended UnstructuredGrid, byte-identical to
+ * the reference writer; parent directories are created. Errors: CWF_ERR_IO "failed to open VTU file"
+ * {path}. cwf_hip_last_error(NULL) holds the message. */
+int cwf_write_vtu(const char *path, const cwf_frame_view *frame, double simulation_time, uint32_t frame_index);
+
+/* cwf::post::ProbeLogger::log_frame (probe_logger.cpp:91-124): appends one CSV row per probe node;
+ * *header_written is the logger's header_written_ flag (0 -> truncate + header first, then set to 1).
+ * Errors: "probe index out of range" {index} (CWF_ERR_INDEX), "failed to open probe CSV" (CWF_ERR_IO). */
+int cwf_probe_log_frame(const char *path, int *header_written, const uint32_t *probes, uint64_t probe_count,
+                        const cwf_frame_view *frame, double simulation_time, uint32_t frame_index);
 
 #ifdef __cplusplus
 }

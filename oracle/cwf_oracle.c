@@ -1012,3 +1012,97 @@ int orc_dense_newmark_step(uint64_t n, const double *K, const double *mass_diag,
     free(diag);
     return 0;
 }
+
+/* ---- derived fields: src/post/derived_fields.cpp:139-211 (scatter form, as the reference loops) ---- */
+
+/* derived_fields.cpp:47-63 */
+static double orc_von_mises(const double s[6])
+{
+    const double dxy = s[0] - s[1], dyz = s[1] - s[2], dzx = s[2] - s[0];
+    const double energy = 0.5 * (dxy * dxy + dyz * dyz + dzx * dzx) + 3.0 * (s[3] * s[3] + s[4] * s[4] + s[5] * s[5]);
+    return sqrt(energy < 0.0 ? 0.0 : energy);
+}
+
+/* u: f32 [3N] node-interleaved displacement; outputs f32 [13E] / [13N] {strain[6], stress[6], vm} */
+int orc_derived_fields(const orc_system *s, const float *u, float *elem_out, float *node_out)
+{
+    const uint64_t N = s->node_count, E = s->element_count;
+    double *acc = (double *)calloc(N * 13, sizeof(double)); /* [strain 6][stress 6][weight] per node */
+    if (!acc)
+        return ORC_ERR_ALLOC;
+    for (uint64_t e = 0; e < E; ++e)
+    {
+        int lc = 0; /* node_count_for_element :27-40 */
+        while (lc < 8 && s->connectivity[e * 8 + lc] != 0xFFFFFFFFu)
+            ++lc;
+        if (lc == 0)
+            continue;
+        const double *D = s->stiffness + 36 * s->material_index[e];
+        double strain[6] = {0, 0, 0, 0, 0, 0};
+        for (int a = 0; a < lc; ++a) /* :164-180 */
+        {
+            const uint32_t n = s->connectivity[e * 8 + a];
+            const double dx = (double)u[3 * (uint64_t)n], dy = (double)u[3 * (uint64_t)n + 1],
+                         dz = (double)u[3 * (uint64_t)n + 2];
+            const double gx = (double)s->gradients[e * 24 + 3 * a], gy = (double)s->gradients[e * 24 + 3 * a + 1],
+                         gz = (double)s->gradients[e * 24 + 3 * a + 2];
+            strain[0] += gx * dx;
+            strain[1] += gy * dy;
+            strain[2] += gz * dz;
+            strain[3] += gy * dx + gx * dy;
+            strain[4] += gz * dy + gy * dz;
+            strain[5] += gz * dx + gx * dz;
+        }
+        double stress[6]; /* stiffness_mul :66-80 */
+        for (int r = 0; r < 6; ++r)
+        {
+            double t = 0.0;
+            for (int c = 0; c < 6; ++c)
+                t += D[r * 6 + c] * strain[c];
+            stress[r] = t;
+        }
+        if (elem_out) /* store_element :97-108 */
+        {
+            for (int c = 0; c < 6; ++c)
+            {
+                elem_out[13 * e + c] = (float)strain[c];
+                elem_out[13 * e + 6 + c] = (float)stress[c];
+            }
+            elem_out[13 * e + 12] = (float)orc_von_mises(stress);
+        }
+        const double vol = (double)s->volume[e];
+        for (int a = 0; a < lc; ++a) /* accumulate_node :82-95 */
+        {
+            double *q = acc + 13 * (uint64_t)s->connectivity[e * 8 + a];
+            q[12] += vol;
+            for (int c = 0; c < 6; ++c)
+            {
+                q[c] += strain[c] * vol;
+                q[6 + c] += stress[c] * vol;
+            }
+        }
+    }
+    if (node_out)
+        for (uint64_t n = 0; n < N; ++n) /* finalize_node :110-134 */
+        {
+            const double *q = acc + 13 * n;
+            float *o = node_out + 13 * n;
+            if (q[12] <= 0.0)
+            {
+                for (int c = 0; c < 13; ++c)
+                    o[c] = 0.0f;
+                continue;
+            }
+            const double inv = 1.0 / q[12];
+            double avg[6];
+            for (int c = 0; c < 6; ++c)
+            {
+                o[c] = (float)(q[c] * inv);
+                avg[c] = q[6 + c] * inv;
+                o[6 + c] = (float)avg[c];
+            }
+            o[12] = (float)orc_von_mises(avg);
+        }
+    free(acc);
+    return ORC_OK;
+}

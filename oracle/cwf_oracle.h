@@ -107,6 +107,8 @@ int orc_solve_pcg(const orc_system *s, const float *rhs, uint64_t max_iterations
                   int warm_start, float *x, float *r, float *p, float *z, float *Ap, double *partials,
                   orc_telemetry *tel, double *residual_history);
 int orc_stepper_step(orc_stepper *t, double sim_time, int paused, orc_step_telemetry *out);
+/* src/post/derived_fields.cpp:139-211; outputs 13 floats per element / node (either may be NULL) */
+int orc_derived_fields(const orc_system *s, const float *u, float *elem_out, float *node_out);
 
 int orc_dense_assemble(uint64_t node_count, uint64_t element_count, const uint32_t *tets, const double *grads64,
                        const double *volume64, const uint32_t *material_index, const double *stiffness, double *K);

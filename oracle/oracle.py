@@ -71,6 +71,8 @@ def lib():
         L.orc_dense_assemble.restype = i32
         L.orc_dense_newmark_step.argtypes = [u64, P, P, P, P, P, f64, f64, P, P, P, P, f64, u64, P, P, P, P]
         L.orc_dense_newmark_step.restype = i32
+        L.orc_derived_fields.argtypes = [P, P, P, P]
+        L.orc_derived_fields.restype = i32
         _lib = L
     return _lib
 
@@ -252,6 +254,16 @@ class System:
         if st:
             raise OracleError(st)
         return y
+
+    def derived_fields(self, u: np.ndarray):
+        """derived_fields.cpp:139-211 -> (f32 [E,13], f32 [N,13]) {strain[6], stress[6], von_mises}."""
+        u = np.ascontiguousarray(u, np.float32)
+        el = np.zeros((self.packed.element_count, 13), np.float32)
+        nd = np.zeros((self.packed.node_count, 13), np.float32)
+        st = lib().orc_derived_fields(self.ptr, _p(u), _p(el), _p(nd))
+        if st:
+            raise OracleError(st)
+        return el, nd
 
     def block_jacobi(self) -> np.ndarray:
         inv = np.zeros(self.packed.node_count * 9, np.float32)
