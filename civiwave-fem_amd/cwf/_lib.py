@@ -78,6 +78,11 @@ class ShardInfoC(C.Structure):
     ]
 
 
+class MeshInfoC(C.Structure):
+    _fields_ = [("node_count", C.c_uint64), ("element_count", C.c_uint64), ("surface_count", C.c_uint64),
+                ("group_count", C.c_uint64)]
+
+
 class FrameViewC(C.Structure):
     _fields_ = [
         ("node_count", C.c_uint64), ("element_count", C.c_uint64), ("position0", C.c_void_p),
@@ -153,6 +158,19 @@ def load() -> C.CDLL:
         "cwf_hip_derived_fields": ([P, P, u64, i32, P, P, i32], i32),
         "cwf_write_vtu": ([C.c_char_p, P, f64, C.c_uint32], i32),
         "cwf_probe_log_frame": ([C.c_char_p, P, P, u64, P, f64, C.c_uint32], i32),
+        "cwf_config_load_file": ([C.c_char_p, P], i32),
+        "cwf_config_load_string": ([C.c_char_p, P], i32),
+        "cwf_config_json": ([P], C.c_char_p),
+        "cwf_config_destroy": ([P], None),
+        "cwf_mesh_load_file": ([C.c_char_p, P], i32),
+        "cwf_mesh_load_string": ([C.c_char_p, P], i32),
+        "cwf_mesh_destroy": ([P], None),
+        "cwf_mesh_get_info": ([P, P], i32),
+        "cwf_mesh_nodes": ([P, P, P], i32),
+        "cwf_mesh_elements": ([P, P, P, P, P], i32),
+        "cwf_mesh_surfaces": ([P, P, P, P], i32),
+        "cwf_mesh_group": ([P, u64, P, P, P], i32),
+        "cwf_mesh_node_group": ([P, C.c_uint32, P, P], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -175,4 +193,4 @@ def last_error(handle=None) -> tuple[str, list[str]]:
     L = load()
     msg = L.cwf_hip_last_error(handle).decode()
     ctx = L.cwf_hip_last_context(handle).decode()
-    return msg, ([ctx] if ctx else [])
+    return msg, (ctx.split("\n") if ctx else [])  # breadcrumb vectors are joined with '\n' 

@@ -111,3 +111,73 @@ CONFIGS = {
     "c5": dict(name="slab 800x400x50 hex (Kuhn tets), 49.1M DOF", shape=(800, 400, 50), h=0.1, xi=0.02,
                w=(5.0, 50.0), tol=3e-4),
 }
+
+
+def boundary_faces(tets: np.ndarray, nodes) -> np.ndarray:
+    """Boundary triangles (faces of exactly one tet) whose three nodes all lie in `nodes` -> u32 [F,3]."""
+    t = np.asarray(tets, np.int64)
+    faces = np.concatenate([t[:, [0, 1, 2]], t[:, [0, 1, 3]], t[:, [0, 2, 3]], t[:, [1, 2, 3]]])
+    key = np.sort(faces, 1)
+    _, inv, cnt = np.unique(key, axis=0, return_inverse=True, return_counts=True)
+    inv = inv.reshape(-1)
+    member = np.zeros(int(t.max()) + 1, bool)
+    member[np.asarray(nodes, np.int64)] = True
+    keep = (cnt[inv] == 1) & member[faces].all(1)
+    return faces[keep].astype(np.uint32)
+
+
+def write_gmsh(tm: TetMesh, path: str, solid: str = "SOLID", surface_groups=("FIXED", "TIP"),
+               node_groups=None) -> None:
+    """Gmsh MSH 4.1 ASCII of a TetMesh that cwf.mesh.load_gmsh_file reads back in the same node and
+    element order: physical volume `solid` (id 1) holds the tets; every name in `surface_groups` becomes
+    a physical surface of its boundary triangles; every name in `node_groups` (default: all of
+    tm.node_groups) tags its nodes through $Entities (Mesh::node_groups). Node blocks follow the node
+    order (one block per run of nodes of the same entity), so node i of the mesh is node i of the file."""
+    names = list(tm.node_groups) if node_groups is None else list(node_groups)
+    phys = {solid: (3, 1)}
+    for i, n in enumerate(names):
+        phys[n] = (2, i + 2)
+    N = tm.node_count
+    owner = np.zeros(N, np.int64)  # entity per node: 0 = volume entity, k = surface entity of names[k-1]
+    for k, n in enumerate(names, start=1):
+        sel = np.asarray(tm.node_groups[n], np.int64)
+        free = sel[owner[sel] == 0]
+        owner[free] = k
+    lines = ["$MeshFormat", "4.1 0 8", "$EndMeshFormat", "$PhysicalNames", str(len(phys))]
+    lines += [f'{d} {i} "{n}"' for n, (d, i) in phys.items()]
+    lines += ["$EndPhysicalNames", "$Entities", f"0 0 {len(names)} 1"]
+    lines += [f"{k} 0 0 0 1 1 1 1 {phys[n][1]} 0" for k, n in enumerate(names, start=1)]
+    lines += [f"1 0 0 0 1 1 1 1 {phys[solid][1]} 0", "$EndEntities"]
+    # node blocks: runs of equal owner
+    runs = []
+    start = 0
+    for i in range(1, N + 1):
+        if i == N or owner[i] != owner[start]:
+            runs.append((start, i))
+            start = i
+    lines += ["$Nodes", f"{len(runs)} {N} 1 {N}"]
+    for a, b in runs:
+        dim, tag = (3, 1) if owner[a] == 0 else (2, int(owner[a]))
+        lines.append(f"{dim} {tag} 0 {b - a}")
+        lines += [str(i + 1) for i in range(a, b)]
+        lines += [f"{x!r} {y!r} {z!r}" for x, y, z in tm.coords[a:b].tolist()]
+    lines.append("$EndNodes")
+    surf = [(k, boundary_faces(tm.tets, tm.node_groups[n])) for k, n in enumerate(names, start=1)
+            if n in surface_groups]
+    surf = [(k, f) for k, f in surf if len(f)]
+    E = tm.element_count
+    total = E + sum(len(f) for _, f in surf)
+    lines += ["$Elements", f"{1 + len(surf)} {total} 1 {total}"]
+    tag = 1
+    for k, f in surf:
+        lines.append(f"2 {k} 2 {len(f)}")
+        for tri in f.tolist():
+            lines.append(f"{tag} {tri[0] + 1} {tri[1] + 1} {tri[2] + 1}")
+            tag += 1
+    lines.append(f"3 1 4 {E}")
+    for t in tm.tets.tolist():
+        lines.append(f"{tag} {t[0] + 1} {t[1] + 1} {t[2] + 1} {t[3] + 1}")
+        tag += 1
+    lines.append("$EndElements")
+    with open(path, "w") as fh:
+        fh.write("\n".join(lines) + "\n")

@@ -319,6 +319,44 @@ int cwf_write_vtu(const char *path, const cwf_frame_view *frame, double simulati
 int cwf_probe_log_frame(const char *path, int *header_written, const uint32_t *probes, uint64_t probe_count,
                         const cwf_frame_view *frame, double simulation_time, uint32_t frame_index);
 
+/* ---- scenario front-end ------------------------------------------------------- */
+/* Error contexts of these calls are the reference's breadcrumb vectors joined with '\n'. */
+
+/* cwf::config::load_config_from_file / load_config_from_string (src/config/config.cpp:118-146) with
+ * parse_config_node's validation (:148-605): same messages and breadcrumbs, e.g. "material.E must be
+ * > 0" {"materials", "[0]", "E"} (CWF_ERR_PARSE). The YAML subset is parsed natively (no yaml-cpp). */
+typedef struct cwf_config cwf_config;
+int cwf_config_load_file(const char *path, cwf_config **out);
+int cwf_config_load_string(const char *yaml_text, cwf_config **out);
+/* the validated Config as canonical JSON (field names of config.hpp:41-237, doubles %.17g) */
+const char *cwf_config_json(const cwf_config *cfg);
+void cwf_config_destroy(cwf_config *cfg);
+
+/* cwf::mesh::load_gmsh_file / load_gmsh_from_string (src/mesh/mesh.cpp:459-566): Gmsh MSH 4.1 ASCII. */
+typedef struct cwf_mesh cwf_mesh;
+typedef struct cwf_mesh_info
+{
+    uint64_t node_count;
+    uint64_t element_count; /* volume elements (tet4 / hex8) */
+    uint64_t surface_count; /* tri3 / quad4 boundary faces */
+    uint64_t group_count;   /* physical groups */
+} cwf_mesh_info;
+int cwf_mesh_load_file(const char *path, cwf_mesh **out);
+int cwf_mesh_load_string(const char *text, cwf_mesh **out);
+void cwf_mesh_destroy(cwf_mesh *mesh);
+int cwf_mesh_get_info(const cwf_mesh *mesh, cwf_mesh_info *info);
+/* coords f64 [3N] (xyz per node, file order), original_ids u32 [N]; either may be NULL */
+int cwf_mesh_nodes(const cwf_mesh *mesh, double *coords, uint32_t *original_ids);
+/* nodes8 u32 [8E] (UINT32_MAX padded), geometry u8 [E] (4 = tet4, 8 = hex8), physical_group u32 [E] */
+int cwf_mesh_elements(const cwf_mesh *mesh, uint32_t *nodes8, uint8_t *geometry, uint32_t *physical_group,
+                      uint32_t *original_ids);
+/* nodes4 u32 [4S] (UINT32_MAX padded), geometry u8 [S] (3 = tri3, 4 = quad4), physical_group u32 [S] */
+int cwf_mesh_surfaces(const cwf_mesh *mesh, uint32_t *nodes4, uint8_t *geometry, uint32_t *physical_group);
+/* physical group `index` (0 .. group_count-1, ascending id); *name stays valid until destroy */
+int cwf_mesh_group(const cwf_mesh *mesh, uint64_t index, uint32_t *dimension, uint32_t *id, const char **name);
+/* node indices tagged with physical group `group_id` through $Entities (Mesh::node_groups) */
+int cwf_mesh_node_group(const cwf_mesh *mesh, uint32_t group_id, const uint32_t **nodes, uint64_t *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,7 +18,9 @@ def oracle_system(P, materials, sK, sM, reduction_block=256):
 
 def bits(a):
     a = np.ascontiguousarray(a)
-    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64)
+    if a.dtype.kind != "f":  # integer words compare as they are
+        return a.reshape(-1)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64).reshape(-1)
 
 
 def assert_bitwise(a, b, what=""):
