@@ -489,7 +489,15 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         }
         try
         {
-            build_tiles(d, ht, t.pipe ? 256u : (uint32_t)kMaxTileNodes);
+            // pipelined tiles: 256-thread workgroups over 512-element tiles, or 128 over 256 (CWF_PIPE_NT, or
+            // automatically for meshes whose 512-element tiles would give each resident workgroup < 8 tiles)
+            if (t.pipe)
+            {
+                const char *pn = getenv("CWF_PIPE_NT");
+                t.pipe_nt = pn ? (atoi(pn) == 128 ? 128 : 256) : (E < 4000000ull ? 128 : 256);
+            }
+            build_tiles(d, ht, t.pipe ? (uint32_t)t.pipe_nt : (uint32_t)kMaxTileNodes,
+                        t.pipe ? 2u * (uint32_t)t.pipe_nt : (uint32_t)kTileElems);
         }
         catch (const std::bad_alloc &)
         {

@@ -35,6 +35,7 @@ struct DevTiles
     int acc = 0;  // 1: fixed-point LDS accumulation (no local CSR fold)
     int pipe = 0; // 1: persistent software-pipelined tiles kernel (GEO, CSR fold)
     uint32_t pipe_grid = 0;  // its resident grid (occupancy x CUs, whole XCD groups)
+    int pipe_nt = 256;       // its workgroup size; tiles hold <= 2 pipe_nt elements and <= pipe_nt nodes
     uint32_t deg_log2 = 0;  // ceil(log2(largest number of (element, corner) pairs of one tile node))
     // [3][E] 48-B records: {idx01, idx23, g0x, g0y} {g0z, g1x, g1y, g1z} {g2x, g2y, g2z, vol};
     // g3 = -(g0 + g1 + g2) (partition of unity of the linear tet)
@@ -68,7 +69,8 @@ struct HostTiles
 };
 
 // max_nodes: distinct nodes per tile (kMaxTileNodes; the pipelined kernel keeps one node per lane: 256)
-int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes = kMaxTileNodes);
+int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes = kMaxTileNodes,
+                uint32_t max_elems = kTileElems);
 // true when the supplied gradients / volumes are those of the supplied node coordinates (so FAST may
 // recompute them on the fly instead of streaming them)
 bool geometry_matches(const cwf_system_desc *d);

@@ -822,7 +822,7 @@ struct PipeNext
     uint32_t mat[2];   // material of elements threadIdx.x, threadIdx.x + 256 (0 when M == 1)
 };
 
-template <bool SANITIZE, int MODE>
+template <int NT, bool SANITIZE, int MODE>
 __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, PipeNext &n)
 {
     const DevTiles &T = s.t;
@@ -838,7 +838,7 @@ __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, Pi
 #pragma unroll
     for (int k = 0; k < 2; ++k)
     {
-        const uint32_t j = i + k * 256u;
+        const uint32_t j = i + k * (uint32_t)NT;
         n.id[k] = T.eid[e0 + (j < ne ? j : 0u)];
         // prefetched with the records: a load inside the element phase would make its wait drain
         // every record load in flight for the next tile
@@ -874,18 +874,19 @@ __device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *
     }
 }
 
-template <bool ISO, bool SANITIZE, int MODE>
-__global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
-                                                         const uint4 *__restrict__ hdr)
+// NT threads per workgroup, tiles of <= TE = 2 NT elements and <= NT nodes (one node per lane)
+template <bool ISO, bool SANITIZE, int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
+                                                        const uint4 *__restrict__ hdr)
 {
-    constexpr int NT = 256;
+    constexpr int TE = 2 * NT;
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
     const uint32_t ms = T.max_tile_nodes;
-    float *sf = lds;                                                     // [12][kTileElems]
-    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * kTileElems);  // [4*kTileElems] local CSR
-    float4 *sxp = reinterpret_cast<float4 *>(lds + 14 * kTileElems);     // [ms] {x, y, z, v_x}
+    float *sf = lds;                                                     // [12][TE]
+    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * TE);  // [4*TE] local CSR
+    float4 *sxp = reinterpret_cast<float4 *>(lds + 14 * TE);     // [ms] {x, y, z, v_x}
     float2 *sq = reinterpret_cast<float2 *>(sxp + ms);                   // [ms] {v_y, v_z}
     __shared__ float dtab[kMaxM * kTab];
     __shared__ double red[NT / 64];
@@ -904,7 +905,7 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
     uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
     if (t < t_end)
     {
-        pipe_issue_records<SANITIZE, MODE>(s, hd, cur);
+        pipe_issue_records<NT, SANITIZE, MODE>(s, hd, cur);
         pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hd.w, cur);
     }
     const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
@@ -948,7 +949,7 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
         const uint32_t tn_next = t + nbx;
         const uint4 hdn = hd2;
         if (tn_next < t_end)
-            pipe_issue_records<SANITIZE, MODE>(s, hdn, cur);
+            pipe_issue_records<NT, SANITIZE, MODE>(s, hdn, cur);
         hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
         // (c) elements of tile t (ablation bit 64: skipped, diagnostic timing only)
 #pragma unroll
@@ -961,7 +962,7 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
                 geo_element_forces<ISO>(s, k ? id1 : id0, sxp, sq, sK6, k ? mat1 : mat0, dtab, f);
 #pragma unroll
                 for (int c = 0; c < 12; ++c)
-                    sf[c * kTileElems + j] = f[c];
+                    sf[c * TE + j] = f[c];
             }
         }
         __syncthreads();
@@ -987,9 +988,9 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
                 for (int u = 0; u < 4; ++u)
                 {
                     const uint32_t el = ent[u] >> 2, c = 3u * (ent[u] & 3u);
-                    f[u][0] = sf[(c + 0) * kTileElems + el];
-                    f[u][1] = sf[(c + 1) * kTileElems + el];
-                    f[u][2] = sf[(c + 2) * kTileElems + el];
+                    f[u][0] = sf[(c + 0) * TE + el];
+                    f[u][1] = sf[(c + 1) * TE + el];
+                    f[u][2] = sf[(c + 2) * TE + el];
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
@@ -1003,9 +1004,9 @@ __global__ __launch_bounds__(256) void k_keff_tiles_pipe(DevSys s, const float *
             {
                 const uint32_t ent = sc[q];
                 const uint32_t el = ent >> 2, c = 3u * (ent & 3u);
-                a0 += sf[(c + 0) * kTileElems + el];
-                a1 += sf[(c + 1) * kTileElems + el];
-                a2 += sf[(c + 2) * kTileElems + el];
+                a0 += sf[(c + 0) * TE + el];
+                a1 += sf[(c + 1) * TE + el];
+                a2 += sf[(c + 2) * TE + el];
             }
             // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
             if (!(pa.abl & 512u))
@@ -1291,17 +1292,17 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 // pipelined kernel: element forces + local CSR + per tile node {x y z v_x}{v_y v_z}
 inline size_t pipe_lds(const DevSys &s)
 {
-    const size_t ms = s.t.max_tile_nodes;
-    return sizeof(float) * 14 * kTileElems + ms * (16 + 8);
+    const size_t ms = s.t.max_tile_nodes, te = 2 * (size_t)s.t.pipe_nt;
+    return sizeof(float) * 14 * te + ms * (16 + 8);
 }
 
-template <bool ISO>
+template <bool ISO, int NT>
 unsigned pipe_grid_query(const DevSys &s)
 {
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1>, 256, pipe_lds(s));
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1, NT>, NT, pipe_lds(s));
     unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     g = g < 8u ? 8u : g - g % 8u;  // whole XCD groups
     const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
@@ -1316,11 +1317,23 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
 {
     if (s.t.pipe)
     {
-        if (e0 && e1)
-            hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE>, dim3(s.t.pipe_grid), dim3(256),
-                                  (uint32_t)pipe_lds(s), st, e0, e1, 0, s, x, pa, s.t.hdr);
+        const size_t lds = pipe_lds(s);
+        if (s.t.pipe_nt == 128)
+        {
+            if (e0 && e1)
+                hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, 128>, dim3(s.t.pipe_grid), dim3(128),
+                                      (uint32_t)lds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+            else
+                k_keff_tiles_pipe<ISO, SAN, MODE, 128><<<s.t.pipe_grid, 128, lds, st>>>(s, x, pa, s.t.hdr);
+        }
         else
-            k_keff_tiles_pipe<ISO, SAN, MODE><<<s.t.pipe_grid, 256, pipe_lds(s), st>>>(s, x, pa, s.t.hdr);
+        {
+            if (e0 && e1)
+                hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, 256>, dim3(s.t.pipe_grid), dim3(256),
+                                      (uint32_t)lds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+            else
+                k_keff_tiles_pipe<ISO, SAN, MODE, 256><<<s.t.pipe_grid, 256, lds, st>>>(s, x, pa, s.t.hdr);
+        }
         return;
     }
     if (e0)
@@ -1336,7 +1349,12 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
 
 unsigned fast_tile_blocks(const DevSys &s) { return s.t.pipe ? s.t.pipe_grid : s.t.ntiles; }
 
-unsigned fast_pipe_grid(const DevSys &s) { return s.iso ? pipe_grid_query<true>(s) : pipe_grid_query<false>(s); }
+unsigned fast_pipe_grid(const DevSys &s)
+{
+    if (s.t.pipe_nt == 128)
+        return s.iso ? pipe_grid_query<true, 128>(s) : pipe_grid_query<false, 128>(s);
+    return s.iso ? pipe_grid_query<true, 256>(s) : pipe_grid_query<false, 256>(s);
+}
 // the update pass is grid-stride: at most one resident wave of workgroups (occupancy x CUs), so no
 // workgroup waits for a slot behind the others' whole node ranges
 unsigned fast_update_blocks(const DevSys &s)

@@ -36,7 +36,7 @@ inline uint64_t spread21(uint64_t v)
 }
 }  // namespace
 
-int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes)
+int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems)
 {
     const uint64_t N = d->node_count, E = d->element_count;
     std::vector<uint32_t> order(E);
@@ -89,7 +89,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes)
         // greedy: up to kTileElems elements while the tile's node list fits kMaxTileNodes
         nodes.clear();
         const uint64_t e0 = e;
-        while (e < E && e - e0 < (uint64_t)kTileElems)
+        while (e < E && e - e0 < (uint64_t)max_elems)
         {
             const uint32_t src = order[e];
             uint32_t add = 0;
