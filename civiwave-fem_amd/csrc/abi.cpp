@@ -495,6 +495,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             {
                 const char *pn = getenv("CWF_PIPE_NT");
                 t.pipe_nt = pn ? (atoi(pn) == 128 ? 128 : 256) : (E < 4000000ull ? 128 : 256);
+                const char *pf = getenv("CWF_PIPE_FOLD");
+                t.push = pf && pf[0] == 'c' ? 0 : 1;  // CWF_PIPE_FOLD=csr: the local-CSR entry fold
             }
             build_tiles(d, ht, t.pipe ? (uint32_t)t.pipe_nt : (uint32_t)kMaxTileNodes,
                         t.pipe ? 2u * (uint32_t)t.pipe_nt : (uint32_t)kTileElems);
@@ -566,14 +568,23 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (int st = upload(h, &dtn, tnode.data(), tnode.size()))
             return bail(st);
         ht.csr_ent.resize(ht.csr_ent.size() + 8, 0);  // the pipelined kernel reads a tile's entries as 16-B words
-        if (int st = upload(h, &ce, ht.csr_ent.data(), ht.csr_ent.size()))
-            return bail(st);
+        ce = nullptr;
+        if (!t.push)  // PUSH streams the per-element positions (epos) instead
+            if (int st = upload(h, &ce, ht.csr_ent.data(), ht.csr_ent.size()))
+                return bail(st);
         if (int st = upload(h, &npo, ht.node_part_off.data(), ht.node_part_off.size()))
             return bail(st);
         uint32_t *ps;
         if (int st = upload(h, &ps, ht.node_part_slot.data(), ht.node_part_slot.size()))
             return bail(st);
         t.part_slot = ps;
+        if (t.push)
+        {
+            uint2 *ep;
+            if (int st = upload(h, &ep, ht.epos.data(), ht.epos.size()))
+                return bail(st);
+            t.epos = ep;
+        }
         if (t.pipe)
         {
             uint32_t *tsl;
@@ -733,7 +744,7 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
     if (h->mode == CWF_MODE_FAST && s.t.ntiles)
     {
         // per tile: 16-B header; per tet: corner ids (8 B GEO, 48-B records otherwise) + 4 u16 local-CSR
-        // entries (+ material id when M > 1); per tile node: {node, csr range} 8 B, coordinates 12 B (GEO),
+        // entries or (PUSH) positions (+ material id when M > 1); per tile node: {node, csr range} 8 B, coordinates 12 B (GEO),
         // partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B
         const uint64_t rec = s.t.geo ? 8 : 48;
         *layout_bytes = 16ull * s.t.ntiles + E * (rec + 8 + (s.t.mat ? 4 : 0)) + T * (8 + (s.t.geo ? 12 : 0) + 12) +

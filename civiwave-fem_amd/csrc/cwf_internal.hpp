@@ -36,6 +36,7 @@ struct DevTiles
     int pipe = 0; // 1: persistent software-pipelined tiles kernel (GEO, CSR fold)
     uint32_t pipe_grid = 0;  // its resident grid (occupancy x CUs, whole XCD groups)
     int pipe_nt = 256;       // its workgroup size; tiles hold <= 2 pipe_nt elements and <= pipe_nt nodes
+    int push = 0;            // 1: elements store forces at their local-CSR positions; nodes fold contiguous runs
     uint32_t deg_log2 = 0;  // ceil(log2(largest number of (element, corner) pairs of one tile node))
     // [3][E] 48-B records: {idx01, idx23, g0x, g0y} {g0z, g1x, g1y, g1z} {g2x, g2y, g2z, vol};
     // g3 = -(g0 + g1 + g2) (partition of unity of the linear tet)
@@ -47,6 +48,7 @@ struct DevTiles
     const uint2 *tnode = nullptr;             // [total] {local node | owner bit 31, csr begin | csr end << 16}
                                               // (csr range relative to the tile's first entry 4*e0)
     const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
+    const uint2 *epos = nullptr;              // [E] (PUSH) each corner's position in the tile's local CSR
     const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile)
     const uint32_t *part_slot = nullptr;      // [total] partial index of each of those slots
     // pipelined kernel: partials stored node-major (tile node q -> part[3 tslot[q]]), so a node's partials
@@ -65,6 +67,7 @@ struct HostTiles
         tile_slot;
     std::vector<uint16_t> csr_ent;
     std::vector<uint2> eid;        // [E] local corner ids
+    std::vector<uint2> epos;       // [E] tile-relative local-CSR positions of the 4 (element, corner) pairs
     std::vector<float> tcoord[3];  // [total] tile-relative coordinates (when node_coords are given)
 };
 

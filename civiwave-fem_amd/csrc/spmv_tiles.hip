@@ -818,11 +818,12 @@ struct PipeNext
     float m;           // its lumped mass (MODE 1: the owner slot's m s_M |p|^2 share of p.Ap)
     uint2 id[2];       // corner ids of elements threadIdx.x, threadIdx.x + 256
     uint4 csr;         // 8 local-CSR entries (16 B) of the tile
+    uint2 pos[2];      // (PUSH) local-CSR positions of the corners of elements threadIdx.x, + NT
     uint32_t slot;     // node-major partial slot of tile node threadIdx.x
     uint32_t mat[2];   // material of elements threadIdx.x, threadIdx.x + 256 (0 when M == 1)
 };
 
-template <int NT, bool SANITIZE, int MODE>
+template <int NT, bool SANITIZE, int MODE, bool PUSH = false>
 __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, PipeNext &n)
 {
     const DevTiles &T = s.t;
@@ -843,9 +844,14 @@ __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, Pi
         // prefetched with the records: a load inside the element phase would make its wait drain
         // every record load in flight for the next tile
         n.mat[k] = T.mat ? T.mat[e0 + (j < ne ? j : 0u)] : 0u;
+        if constexpr (PUSH)
+            n.pos[k] = T.epos[e0 + (j < ne ? j : 0u)];
     }
-    const uint4 *src = reinterpret_cast<const uint4 *>(T.csr_ent + 4ull * e0);  // 4 ne u16 = ne / 2 uint4
-    n.csr = i < (ne + 1) / 2 ? src[i] : uint4{0u, 0u, 0u, 0u};
+    if constexpr (!PUSH)
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(T.csr_ent + 4ull * e0);  // 4 ne u16 = ne / 2 uint4
+        n.csr = i < (ne + 1) / 2 ? src[i] : uint4{0u, 0u, 0u, 0u};
+    }
 }
 
 template <bool SANITIZE, int MODE>
@@ -875,18 +881,22 @@ __device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *
 }
 
 // NT threads per workgroup, tiles of <= TE = 2 NT elements and <= NT nodes (one node per lane)
-template <bool ISO, bool SANITIZE, int MODE, int NT>
+// PUSH: each element stores its 4 corner forces at their tile-relative local-CSR positions (epos), so a
+// node's forces sit contiguously in ascending element order and the fold reads them without the
+// dependent CSR-entry lookup (same summation order, bitwise the same result as the CSR fold).
+template <bool ISO, bool SANITIZE, int MODE, int NT, bool PUSH>
 __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
                                                         const uint4 *__restrict__ hdr)
 {
     constexpr int TE = 2 * NT;
+    constexpr int SP = 4 * TE;  // PUSH: slots per component plane (one per (element, corner) pair)
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
     const uint32_t ms = T.max_tile_nodes;
-    float *sf = lds;                                                     // [12][TE]
-    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * TE);  // [4*TE] local CSR
-    float4 *sxp = reinterpret_cast<float4 *>(lds + 14 * TE);     // [ms] {x, y, z, v_x}
+    float *sf = lds;                                                     // [12][TE]; PUSH: [3][SP]
+    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * TE);  // [4*TE] local CSR (unused with PUSH)
+    float4 *sxp = reinterpret_cast<float4 *>(lds + (PUSH ? 3 * SP : 14 * TE));  // [ms] {x, y, z, v_x}
     float2 *sq = reinterpret_cast<float2 *>(sxp + ms);                   // [ms] {v_y, v_z}
     __shared__ float dtab[kMaxM * kTab];
     __shared__ double red[NT / 64];
@@ -905,7 +915,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
     uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
     if (t < t_end)
     {
-        pipe_issue_records<NT, SANITIZE, MODE>(s, hd, cur);
+        pipe_issue_records<NT, SANITIZE, MODE, PUSH>(s, hd, cur);
         pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hd.w, cur);
     }
     const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
@@ -937,9 +947,10 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             sxp[i0] = float4{cur.c[0], cur.c[1], cur.c[2], v0};
             sq[i0] = float2{v1, v2};
         }
-        if (i0 < (ne + 1) / 2)
+        if (!PUSH && i0 < (ne + 1) / 2)
             reinterpret_cast<uint4 *>(sc)[i0] = cur.csr;
         const uint2 id0 = cur.id[0], id1 = cur.id[1];
+        const uint2 pos0 = cur.pos[0], pos1 = cur.pos[1];
         const uint32_t mat0 = cur.mat[0], mat1 = cur.mat[1];
         const uint2 tn_own = cur.tn;
         const uint32_t slot_own = cur.slot;
@@ -949,7 +960,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
         const uint32_t tn_next = t + nbx;
         const uint4 hdn = hd2;
         if (tn_next < t_end)
-            pipe_issue_records<NT, SANITIZE, MODE>(s, hdn, cur);
+            pipe_issue_records<NT, SANITIZE, MODE, PUSH>(s, hdn, cur);
         hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
         // (c) elements of tile t (ablation bit 64: skipped, diagnostic timing only)
 #pragma unroll
@@ -960,9 +971,22 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             {
                 float f[12];
                 geo_element_forces<ISO>(s, k ? id1 : id0, sxp, sq, sK6, k ? mat1 : mat0, dtab, f);
+                if constexpr (PUSH)
+                {
+                    const uint2 ps = k ? pos1 : pos0;
+                    const uint32_t pq[4] = {ps.x & 0xffffu, ps.x >> 16, ps.y & 0xffffu, ps.y >> 16};
 #pragma unroll
-                for (int c = 0; c < 12; ++c)
-                    sf[c * TE + j] = f[c];
+                    for (int a = 0; a < 4; ++a)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            sf[c * SP + pq[a]] = f[3 * a + c];
+                }
+                else
+                {
+#pragma unroll
+                    for (int c = 0; c < 12; ++c)
+                        sf[c * TE + j] = f[c];
+                }
             }
         }
         __syncthreads();
@@ -977,6 +1001,32 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             float a0 = 0.f, a1 = 0.f, a2 = 0.f;
             const uint32_t qe = tn.y >> 16;
             uint32_t q = tn.y & 0xffffu;
+            if constexpr (PUSH)
+            {
+                // the node's forces are the contiguous run [q, qe) of each component plane
+                for (; q + 4 <= qe; q += 4)
+                {
+                    float f[4][3];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            f[u][c] = sf[c * SP + q + u];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                    {
+                        a0 += f[u][0];
+                        a1 += f[u][1];
+                        a2 += f[u][2];
+                    }
+                }
+                for (; q < qe; ++q)
+                {
+                    a0 += sf[q];
+                    a1 += sf[SP + q];
+                    a2 += sf[2 * SP + q];
+                }
+            }
             for (; q + 4 <= qe; q += 4)
             {
                 uint32_t ent[4];
@@ -1293,20 +1343,33 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 inline size_t pipe_lds(const DevSys &s)
 {
     const size_t ms = s.t.max_tile_nodes, te = 2 * (size_t)s.t.pipe_nt;
-    return sizeof(float) * 14 * te + ms * (16 + 8);
+    // PUSH: 3 component planes of 4 te (element, corner) slots; CSR fold: 12 te forces + 4 te u16 entries
+    return sizeof(float) * (s.t.push ? 12 * te : 14 * te) + ms * (16 + 8);
 }
 
-template <bool ISO, int NT>
+template <bool ISO, int NT, bool PUSH>
 unsigned pipe_grid_query(const DevSys &s)
 {
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1, NT>, NT, pipe_lds(s));
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1, NT, PUSH>, NT,
+                                                       pipe_lds(s));
     unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     g = g < 8u ? 8u : g - g % 8u;  // whole XCD groups
     const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
     return g < need ? g : (need ? need : 8u);
+}
+
+template <bool ISO, bool SAN, int MODE, int NT, bool PUSH>
+void launch_pipe(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
+{
+    const size_t lds = pipe_lds(s);
+    if (e0 && e1)
+        hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, NT, PUSH>, dim3(s.t.pipe_grid), dim3(NT),
+                              (uint32_t)lds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+    else
+        k_keff_tiles_pipe<ISO, SAN, MODE, NT, PUSH><<<s.t.pipe_grid, NT, lds, st>>>(s, x, pa, s.t.hdr);
 }
 
 // e0/e1 (optional): hipExtLaunchKernel stamps them from the dispatch packet itself, so the timed
@@ -1317,23 +1380,12 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
 {
     if (s.t.pipe)
     {
-        const size_t lds = pipe_lds(s);
         if (s.t.pipe_nt == 128)
-        {
-            if (e0 && e1)
-                hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, 128>, dim3(s.t.pipe_grid), dim3(128),
-                                      (uint32_t)lds, st, e0, e1, 0, s, x, pa, s.t.hdr);
-            else
-                k_keff_tiles_pipe<ISO, SAN, MODE, 128><<<s.t.pipe_grid, 128, lds, st>>>(s, x, pa, s.t.hdr);
-        }
+            s.t.push ? launch_pipe<ISO, SAN, MODE, 128, true>(s, x, pa, st, e0, e1)
+                     : launch_pipe<ISO, SAN, MODE, 128, false>(s, x, pa, st, e0, e1);
         else
-        {
-            if (e0 && e1)
-                hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, 256>, dim3(s.t.pipe_grid), dim3(256),
-                                      (uint32_t)lds, st, e0, e1, 0, s, x, pa, s.t.hdr);
-            else
-                k_keff_tiles_pipe<ISO, SAN, MODE, 256><<<s.t.pipe_grid, 256, lds, st>>>(s, x, pa, s.t.hdr);
-        }
+            s.t.push ? launch_pipe<ISO, SAN, MODE, 256, true>(s, x, pa, st, e0, e1)
+                     : launch_pipe<ISO, SAN, MODE, 256, false>(s, x, pa, st, e0, e1);
         return;
     }
     if (e0)
@@ -1351,9 +1403,15 @@ unsigned fast_tile_blocks(const DevSys &s) { return s.t.pipe ? s.t.pipe_grid : s
 
 unsigned fast_pipe_grid(const DevSys &s)
 {
+    if (s.t.push)
+    {
+        if (s.t.pipe_nt == 128)
+            return s.iso ? pipe_grid_query<true, 128, true>(s) : pipe_grid_query<false, 128, true>(s);
+        return s.iso ? pipe_grid_query<true, 256, true>(s) : pipe_grid_query<false, 256, true>(s);
+    }
     if (s.t.pipe_nt == 128)
-        return s.iso ? pipe_grid_query<true, 128>(s) : pipe_grid_query<false, 128>(s);
-    return s.iso ? pipe_grid_query<true, 256>(s) : pipe_grid_query<false, 256>(s);
+        return s.iso ? pipe_grid_query<true, 128, false>(s) : pipe_grid_query<false, 128, false>(s);
+    return s.iso ? pipe_grid_query<true, 256, false>(s) : pipe_grid_query<false, 256, false>(s);
 }
 // the update pass is grid-stride: at most one resident wave of workgroups (occupancy x CUs), so no
 // workgroup waits for a slot behind the others' whole node ranges

@@ -78,6 +78,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
     if (d->material_count > 1)
         out.mat.resize(E);
     out.eid.resize(E);
+    out.epos.resize(E);
     out.csr_ent.reserve(E * 4);
     std::vector<uint32_t> stamp(N, 0xFFFFFFFFu), local(N, 0);
     std::vector<uint32_t> nodes;
@@ -146,11 +147,14 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
         for (uint32_t j = 0; j < ne; ++j)
         {
             const uint32_t src = order[e0 + j];
+            uint32_t epos[4];
             for (int a = 0; a < 4; ++a)
             {
                 const uint32_t l = local[d->element_connectivity[(uint64_t)src * 8 + a]];
+                epos[a] = cur[l];  // the corner's tile-relative local-CSR position (PUSH)
                 out.csr_ent[base + cur[l]++] = (uint16_t)(j * 4 + a);
             }
+            out.epos[e0 + j] = uint2{epos[0] | (epos[1] << 16), epos[2] | (epos[3] << 16)};
         }
         for (uint32_t i = 0; i < nn; ++i)
         {
