@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", help="BASELINE config key (c1..c5)")
     ap.add_argument("--mode", default="fast", choices=["fast", "parity"])
+    ap.add_argument("--element", default="tet4", choices=["tet4", "hex8"],
+                    help="tet4: the Kuhn expansion the reference runs (the headline); hex8: native hexes "
+                         "(SURVEY 8f4, FAST only, parity unpinned)")
     ap.add_argument("--max-iterations", type=int, default=2000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--keff-sample", type=int, default=4,
@@ -94,15 +97,15 @@ def main():
     mode = _lib.MODE_FAST if args.mode == "fast" else _lib.MODE_PARITY
     comm = None
     if world == 1:
-        case = scenarios.config_case(args.config, max_iterations=args.max_iterations)
+        case = scenarios.config_case(args.config, max_iterations=args.max_iterations, element=args.element)
         P = case.packing
         sK, sM = case.scalars()
         stepper = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode,
                           device=device)
         owned_dofs, local_nodes, local_tets = P.dof_count, P.node_count, P.element_count
     else:
-        if mode != _lib.MODE_FAST:
-            raise SystemExit("multi-GPU runs the FAST path only")
+        if mode != _lib.MODE_FAST or args.element != "tet4":
+            raise SystemExit("multi-GPU runs the FAST tet4 path only")
         case, node_global, begin = scenarios.slab_case(args.config, world, rank, max_iterations=args.max_iterations)
         P = case.packing
         sK, sM = case.scalars()
@@ -179,7 +182,7 @@ def main():
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
+        if not args.no_cpu_baseline and world == 1 and args.element == "tet4":  # rank 0 at N=1 only
             cpu = cpu_baseline(case, sK, sM, args.cpu_iterations)
         result = {
             "metric": "PCG DOF-iterations/sec per Newmark step (PCG-it/s x DOFs); DOF-updates/s and "
@@ -194,8 +197,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.mode == "fast" else "f64",
-            "data": "synthetic (structured hex block -> Kuhn tets, gravity + tip load)",
-            "config": {"workload": case.name, "nodes_per_gpu": local_nodes, "tets_per_gpu": local_tets,
+            "data": "synthetic (structured hex block -> Kuhn tets, gravity + tip load)" if args.element == "tet4"
+                    else "synthetic (structured native hex8 block, gravity + tip load)",
+            "config": {"workload": case.name, "nodes_per_gpu": local_nodes,
+                       ("hexes_per_gpu" if args.element == "hex8" else "tets_per_gpu"): local_tets,
                        "dofs": int(dofs_sum), "mode": args.mode,
                        "parallelism": f"node-range shards x{world} (RCCL halo + all-gather)" if world > 1
                        else "single"},
@@ -205,7 +210,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "k_keff_tiles_pipe" if args.mode == "fast" else "k_keff_parity",
+                         "kernel": ("k_keff_hex_tiles" if args.element == "hex8" else "k_keff_tiles_pipe")
+                                   if args.mode == "fast" else "k_keff_parity",
                          "avg_launch_ms": avg_keff_ms, "launches": int(keff_n.value),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "reference_layout_bytes_per_launch": ref_bytes,

@@ -331,13 +331,24 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     if (N * 3 >= (1ull << 32) || E >= (1ull << 30))
         return set_error(nullptr, CWF_ERR_UNSUPPORTED, "mesh too large for one handle (shard it)",
                          "nodes=" + std::to_string(N) + " elements=" + std::to_string(E));
+    // hex8: all 8 connectivity slots used; tet4 pads slots 4..7 with UINT32_MAX
+    const bool hex = E && d->element_connectivity[4] != 0xFFFFFFFFu;
+    const int K = hex ? 8 : 4;
+    if (hex && d->mode != CWF_MODE_FAST)
+        return set_error(nullptr, CWF_ERR_UNSUPPORTED, "hex8 elements run in CWF_MODE_FAST only",
+                         "the reference has no hex8 arithmetic to reproduce (preprocess.cpp:326-330)");
+    if (hex && !d->node_coords)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "hex8 systems need node_coords");
     for (uint64_t e = 0; e < E; ++e)
     {
         if (d->element_material_index[e] >= d->material_count)
             return set_error(nullptr, CWF_ERR_MATERIAL_RANGE, "element references material out of range",
                              "element=" + std::to_string(e) +
                                  " material_index=" + std::to_string(d->element_material_index[e]));
-        for (int a = 0; a < 4; ++a)
+        if ((d->element_connectivity[e * 8 + 4] != 0xFFFFFFFFu) != hex)
+            return set_error(nullptr, CWF_ERR_UNSUPPORTED, "mixed tet4/hex8 meshes are not supported",
+                             "element=" + std::to_string(e));
+        for (int a = 0; a < K; ++a)
             if (d->element_connectivity[e * 8 + a] >= N)
                 return set_error(nullptr, CWF_ERR_NODE_RANGE, "element connectivity references node out of range",
                                  "element=" + std::to_string(e) +
@@ -377,8 +388,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     s.iso = 1;
     for (uint64_t m = 0; m < d->material_count; ++m)
         s.iso &= iso_pattern(d->material_stiffness + 36 * m) ? 1 : 0;
+    s.hex = hex ? 1 : 0;
 
-    // element records (64 B/tet)
+    // element records (64 B/tet; the PARITY kernels only, so none for hex8)
+    if (!hex)
     {
         std::vector<uint32_t> rec;
         try
@@ -426,9 +439,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     // node -> element CSR, ascending element per node (preprocess.cpp:380-403)
     {
         std::vector<uint32_t> off(N + 1, 0), inc;
+        const uint32_t sh = hex ? 3u : 2u;  // inc = element << sh | corner
         try
         {
-            inc.resize(E * 4);
+            inc.resize(E * K);
         }
         catch (const std::bad_alloc &)
         {
@@ -437,17 +451,17 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (d->adjacency_offsets && d->adjacency_elements && d->adjacency_local)
         {
             std::memcpy(off.data(), d->adjacency_offsets, (N + 1) * sizeof(uint32_t));
-            if (off[N] != E * 4)
+            if (off[N] != E * K)
                 return bail(set_error(h, CWF_ERR_SIZE, "adjacency size mismatch",
-                                      "expected=" + std::to_string(E * 4) + " actual=" + std::to_string(off[N])));
-            for (uint64_t j = 0; j < E * 4; ++j)
-                inc[j] = (d->adjacency_elements[j] << 2) | (d->adjacency_local[j] & 3u);
+                                      "expected=" + std::to_string(E * K) + " actual=" + std::to_string(off[N])));
+            for (uint64_t j = 0; j < E * K; ++j)
+                inc[j] = (d->adjacency_elements[j] << sh) | (d->adjacency_local[j] & (uint32_t)(K - 1));
         }
         else
         {
             std::vector<uint32_t> cnt(N, 0);
             for (uint64_t e = 0; e < E; ++e)
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < K; ++a)
                     ++cnt[d->element_connectivity[e * 8 + a]];
             uint32_t acc = 0;
             for (uint64_t n = 0; n < N; ++n)
@@ -458,16 +472,16 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             }
             off[N] = acc;
             for (uint64_t e = 0; e < E; ++e)
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < K; ++a)
                 {
                     const uint32_t n = d->element_connectivity[e * 8 + a];
-                    inc[off[n] + cnt[n]++] = ((uint32_t)e << 2) | (uint32_t)a;
+                    inc[off[n] + cnt[n]++] = ((uint32_t)e << sh) | (uint32_t)a;
                 }
         }
         uint32_t *doff, *dinc;
         if (int st = upload(h, &doff, off.data(), N + 1))
             return bail(st);
-        if (int st = upload(h, &dinc, inc.data(), E * 4))
+        if (int st = upload(h, &dinc, inc.data(), E * K))
             return bail(st);
         s.off = doff;
         s.inc = dinc;
@@ -480,7 +494,13 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         // GEO: stream 8-B corner ids + tile-node coordinates and recompute gradients/volume on the fly,
         // when the desc carries coordinates that reproduce its gradients (CWF_GEO=0 forces the records)
         const char *ge = getenv("CWF_GEO");
-        t.geo = (!ge || ge[0] != '0') && d->node_coords && N && geometry_matches(d) ? 1 : 0;
+        t.geo = hex || ((!ge || ge[0] != '0') && d->node_coords && N && geometry_matches(d)) ? 1 : 0;
+        if (hex)  // k_keff_hex_tiles: kHexTileThreads lanes, one hex and two tile nodes per lane, push fold
+        {
+            t.hex = 1;
+            t.push = 1;
+        }
+        else
         {
             const char *fo = getenv("CWF_TILE_FOLD");
             t.acc = fo && fo[0] == 'a' ? 1 : 0;
@@ -498,8 +518,11 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 const char *pf = getenv("CWF_PIPE_FOLD");
                 t.push = pf && pf[0] == 'c' ? 0 : 1;  // CWF_PIPE_FOLD=csr: the local-CSR entry fold
             }
-            build_tiles(d, ht, t.pipe ? (uint32_t)t.pipe_nt : (uint32_t)kMaxTileNodes,
-                        t.pipe ? 2u * (uint32_t)t.pipe_nt : (uint32_t)kTileElems);
+            if (hex)
+                build_tiles(d, ht, 2u * kHexTileThreads, kHexTileThreads, 8);
+            else
+                build_tiles(d, ht, t.pipe ? (uint32_t)t.pipe_nt : (uint32_t)kMaxTileNodes,
+                            t.pipe ? 2u * (uint32_t)t.pipe_nt : (uint32_t)kTileElems);
         }
         catch (const std::bad_alloc &)
         {
@@ -518,9 +541,16 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     ht.max_tile_nodes, t.geo ? "8-B geometric" : "48-B gradient");
         if (t.geo)
         {
-            uint2 *eid;
+            uint2 *eid = nullptr;
             float *tc;
-            if (int st = upload(h, &eid, ht.eid.data(), E))
+            if (hex)
+            {
+                uint4 *e8;
+                if (int st = upload(h, &e8, ht.eid8.data(), E))
+                    return bail(st);
+                t.eid8 = e8;
+            }
+            else if (int st = upload(h, &eid, ht.eid.data(), E))
                 return bail(st);
             const size_t T3 = ht.tile_nodes.size();
             if (int st = dalloc(h, &tc, 3 * T3))
@@ -556,7 +586,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             const uint32_t e0 = ht.tile_elem_off[k], nb = ht.tile_node_off[k], nb1 = ht.tile_node_off[k + 1];
             hdr[k] = uint4{e0, ht.tile_elem_off[k + 1] - e0, nb, nb1 - nb};
             for (uint32_t q = nb; q < nb1; ++q)
-                tnode[q] = uint2{ht.tile_nodes[q], (ht.csr_off[q] - 4u * e0) | ((ht.csr_off[q + 1] - 4u * e0) << 16)};
+                tnode[q] = uint2{ht.tile_nodes[q], (ht.csr_off[q] - (uint32_t)K * e0) |
+                                                       ((ht.csr_off[q + 1] - (uint32_t)K * e0) << 16)};
         }
         uint4 *dh;
         uint2 *dtn;
@@ -578,14 +609,21 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (int st = upload(h, &ps, ht.node_part_slot.data(), ht.node_part_slot.size()))
             return bail(st);
         t.part_slot = ps;
-        if (t.push)
+        if (t.push && hex)
+        {
+            uint4 *ep;
+            if (int st = upload(h, &ep, ht.epos8.data(), ht.epos8.size()))
+                return bail(st);
+            t.epos8 = ep;
+        }
+        else if (t.push)
         {
             uint2 *ep;
             if (int st = upload(h, &ep, ht.epos.data(), ht.epos.size()))
                 return bail(st);
             t.epos = ep;
         }
-        if (t.pipe)
+        if (t.pipe || t.hex)
         {
             uint32_t *tsl;
             if (int st = upload(h, &tsl, ht.tile_slot.data(), ht.tile_slot.size()))
@@ -604,8 +642,25 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.csr_ent = ce;
         t.node_part_off = npo;
         t.part = part;
-        if (t.pipe)
+        if (t.pipe || t.hex)
             t.pipe_grid = fast_pipe_grid(s);
+    }
+    if (hex)  // the hex block-Jacobi setup integrates from the global corners (fp64)
+    {
+        uint32_t *hc;
+        double *hx;
+        std::vector<uint32_t> conn(E * 8);
+        std::memcpy(conn.data(), d->element_connectivity, E * 8 * sizeof(uint32_t));
+        if (int st = upload(h, &hc, conn.data(), E * 8))
+            return bail(st);
+        if (int st = upload(h, &hx, d->node_coords, 3 * N))
+            return bail(st);
+        float *hg;
+        if (int st = upload(h, &hg, d->element_gradients, 24 * E))
+            return bail(st);
+        s.hconn = hc;
+        s.hcoord = hx;
+        s.hgrad = hg;
     }
     // solver scratch
     const uint64_t D = 3 * N;
@@ -657,6 +712,9 @@ int cwf_hip_system_set_mode(cwf_hip_system *h, int mode)
 {
     if (int st = check_ready(h))
         return st;
+    if (h->ds.hex && mode != CWF_MODE_FAST)
+        return set_error(h, CWF_ERR_UNSUPPORTED, "hex8 elements run in CWF_MODE_FAST only",
+                         "the reference has no hex8 arithmetic to reproduce (preprocess.cpp:326-330)");
     h->mode = mode == CWF_MODE_FAST ? CWF_MODE_FAST : CWF_MODE_PARITY;
     return 0;
 }
@@ -746,7 +804,8 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // per tile: 16-B header; per tet: corner ids (8 B GEO, 48-B records otherwise) + 4 u16 local-CSR
         // entries or (PUSH) positions (+ material id when M > 1); per tile node: {node, csr range} 8 B, coordinates 12 B (GEO),
         // partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B
-        const uint64_t rec = s.t.geo ? 8 : 48;
+        // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
+        const uint64_t rec = s.t.hex ? 24 : s.t.geo ? 8 : 48;
         *layout_bytes = 16ull * s.t.ntiles + E * (rec + 8 + (s.t.mat ? 4 : 0)) + T * (8 + (s.t.geo ? 12 : 0) + 12) +
                         N * (24 + 4);
     }
@@ -826,7 +885,10 @@ int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64
         return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
                          "required=" + std::to_string(req) + " available=" + std::to_string(n));
     float *dst = kind == CWF_PTR_DEVICE ? inv_out : h->inv;
-    parity_block_jacobi(h, dst, h->stream);
+    if (h->ds.hex)
+        hex_block_jacobi(h, dst, h->stream);
+    else
+        parity_block_jacobi(h, dst, h->stream);
     HIPTRY(h, hipGetLastError());
     if (kind != CWF_PTR_DEVICE)
         HIPTRY(h, hipMemcpyAsync(inv_out, dst, req * sizeof(float), hipMemcpyDeviceToHost, h->stream));

@@ -24,6 +24,7 @@ namespace cwf
 // FAST-mode element tiles (tiles.cpp): element-centric K_eff with deterministic LDS folds
 constexpr int kTileElems = 512;      // elements per tile (= per 256-thread workgroup)
 constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two node slots per thread)
+constexpr uint32_t kHexTileThreads = 128;  // hex8 tiles: <= 128 hexes and <= 256 nodes per 128-lane workgroup
 
 struct DevTiles
 {
@@ -49,6 +50,10 @@ struct DevTiles
                                               // (csr range relative to the tile's first entry 4*e0)
     const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
     const uint2 *epos = nullptr;              // [E] (PUSH) each corner's position in the tile's local CSR
+    // native hex8: k_keff_hex_tiles, 128-thread persistent grid (pipe_grid), push fold
+    int hex = 0;
+    const uint4 *eid8 = nullptr;   // [E] 8 u16 local corner ids (Gmsh corner order)
+    const uint4 *epos8 = nullptr;  // [E] 8 u16 local-CSR positions
     const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile)
     const uint32_t *part_slot = nullptr;      // [total] partial index of each of those slots
     // pipelined kernel: partials stored node-major (tile node q -> part[3 tslot[q]]), so a node's partials
@@ -68,12 +73,14 @@ struct HostTiles
     std::vector<uint16_t> csr_ent;
     std::vector<uint2> eid;        // [E] local corner ids
     std::vector<uint2> epos;       // [E] tile-relative local-CSR positions of the 4 (element, corner) pairs
+    std::vector<uint4> eid8, epos8;  // hex8: [E] the 8 corners' local ids / local-CSR positions (u16 pairs)
     std::vector<float> tcoord[3];  // [total] tile-relative coordinates (when node_coords are given)
 };
 
 // max_nodes: distinct nodes per tile (kMaxTileNodes; the pipelined kernel keeps one node per lane: 256)
+// corners: 4 (tet4) or 8 (hex8: eid8/epos8 records, local-CSR entries element_local * 8 + corner)
 int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes = kMaxTileNodes,
-                uint32_t max_elems = kTileElems);
+                uint32_t max_elems = kTileElems, int corners = 4);
 // true when the supplied gradients / volumes are those of the supplied node coordinates (so FAST may
 // recompute them on the fly instead of streaming them)
 bool geometry_matches(const cwf_system_desc *d);
@@ -96,6 +103,10 @@ struct DevSys
     double sK = 1.0;  // stiffness_scale
     double sM = 0.0;  // mass_factor
     int iso = 0;      // every material has the isotropic Voigt zero pattern
+    int hex = 0;      // elements are hex8 (FAST only): hconn / hcoord feed the hex block-Jacobi setup
+    const uint32_t *hconn = nullptr;  // [8E] hex corner nodes (Gmsh order)
+    const double *hcoord = nullptr;   // [3N] node coordinates
+    const float *hgrad = nullptr;     // [24E] element-centre dN_a/dx (the post stack's centroid strain)
     DevTiles t{};     // FAST-mode tiles (empty in a PARITY-only handle)
 };
 
@@ -187,6 +198,7 @@ uint32_t parity_chunk_count(const cwf_hip_system *h);
 void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st);
 void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st);
 void parity_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st);
+void hex_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st);  // hex8 diagonal blocks -> inverse
 void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b, const float *c, double *pab,
                          double *pac, const Ctl *ctl, hipStream_t st);
 void parity_fold(const double *part, uint32_t count, double *out, hipStream_t st);

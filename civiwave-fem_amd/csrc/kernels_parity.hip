@@ -322,6 +322,104 @@ __global__ __launch_bounds__(kBlock) void k_block_jacobi_parity(DevSys s, float 
         inv_out[9u * n + i] = (float)iv[i];
 }
 
+// Native hex8 block-Jacobi (FAST only; parity unpinned: the reference rejects hex8). One
+// thread per node, incident hexes in ascending element order (inc = element << 3 | corner): the
+// corner's diagonal 3x3 block of K_e = sum_gp |det J| B_a^T D B_a s_K in fp64 (2x2x2 Gauss), then the
+// same m s_M diagonal, regularised fp64 inverse and constrained-row identity as the tet path.
+__global__ __launch_bounds__(kBlock) void k_block_jacobi_hex(DevSys s, float *__restrict__ inv_out)
+{
+    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if (n >= s.N)
+        return;
+    const double sg[8][3] = {{-1, -1, -1}, {1, -1, -1}, {1, 1, -1}, {-1, 1, -1},
+                             {-1, -1, 1},  {1, -1, 1},  {1, 1, 1},  {-1, 1, 1}};
+    const double r3 = 0.57735026918962576;  // 1 / sqrt(3)
+    double blk[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t j = s.off[n]; j < s.off[n + 1]; ++j)
+    {
+        const uint32_t inc = s.inc[j];
+        const uint32_t e = inc >> 3, a = inc & 7u;
+        double X[8][3];
+        for (int c = 0; c < 8; ++c)
+        {
+            const uint32_t v = s.hconn[8ull * e + c];
+            X[c][0] = s.hcoord[3ull * v + 0];
+            X[c][1] = s.hcoord[3ull * v + 1];
+            X[c][2] = s.hcoord[3ull * v + 2];
+        }
+        const double *Dm = s.dmat + 36u * s.mat[e];
+        for (int p = 0; p < 8; ++p)
+        {
+            const double q[3] = {(p & 1) ? r3 : -r3, (p & 2) ? r3 : -r3, (p & 4) ? r3 : -r3};
+            double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, dNa[3] = {0, 0, 0};
+            for (int c = 0; c < 8; ++c)
+            {
+                const double f0 = 1.0 + sg[c][0] * q[0], f1 = 1.0 + sg[c][1] * q[1], f2 = 1.0 + sg[c][2] * q[2];
+                const double d0 = 0.125 * sg[c][0] * f1 * f2, d1 = 0.125 * f0 * sg[c][1] * f2,
+                             d2 = 0.125 * f0 * f1 * sg[c][2];
+                for (int m = 0; m < 3; ++m)
+                {
+                    J[m][0] += X[c][m] * d0;
+                    J[m][1] += X[c][m] * d1;
+                    J[m][2] += X[c][m] * d2;
+                }
+                if ((uint32_t)c == a)
+                {
+                    dNa[0] = d0;
+                    dNa[1] = d1;
+                    dNa[2] = d2;
+                }
+            }
+            double A[3][3];
+            A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+            A[0][1] = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+            A[0][2] = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+            A[1][0] = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+            A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+            A[1][2] = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+            A[2][0] = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+            A[2][1] = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+            A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+            const double det = J[0][0] * A[0][0] + J[0][1] * A[1][0] + J[0][2] * A[2][0];
+            double g[3];
+            for (int m = 0; m < 3; ++m)
+                g[m] = (dNa[0] * A[0][m] + dNa[1] * A[1][m] + dNa[2] * A[2][m]) / det;
+            // B_a (6x3), rows xx yy zz xy yz xz
+            const double B[6][3] = {{g[0], 0, 0}, {0, g[1], 0}, {0, 0, g[2]},
+                                    {g[1], g[0], 0}, {0, g[2], g[1]}, {g[2], 0, g[0]}};
+            const double w = fabs(det) * s.sK;
+            for (int i = 0; i < 3; ++i)
+                for (int k = 0; k < 3; ++k)
+                {
+                    double sum = 0.0;
+                    for (int r = 0; r < 6; ++r)
+                    {
+                        double db = 0.0;
+                        for (int c = 0; c < 6; ++c)
+                            db += Dm[6 * r + c] * B[c][k];
+                        sum += B[r][i] * db;
+                    }
+                    blk[3 * i + k] += sum * w;
+                }
+        }
+    }
+    const double m = (double)s.mass[n] * s.sM;
+    blk[0] += m;
+    blk[4] += m;
+    blk[8] += m;
+    double iv[9];
+    invert_spd_3x3(blk, iv);
+    const uint32_t mk = s.mask[n];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (mk & (1u << k))
+            for (int c = 0; c < 3; ++c)
+                iv[3 * k + c] = (k == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        inv_out[9u * n + i] = (float)iv[i];
+}
+
 // ---- reductions (pcg.cpp:170-207): sequential fp64 fold inside each reduction_block chunk ----
 
 // generic chunk size: one thread per chunk, sequential loads
@@ -696,6 +794,13 @@ void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, co
 void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
 {
     parity_keff_ds(h->ds, x, y, sanitize, ctl, st);
+}
+
+void hex_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st)
+{
+    if (h->ds.N == 0)
+        return;
+    k_block_jacobi_hex<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, inv);
 }
 
 void parity_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st)

@@ -25,20 +25,44 @@ struct ElemTensors
     double stress[6];
 };
 
-// derived_fields.cpp:164-180 + stiffness_mul :66-80 for element e (tet4: 4 local nodes)
-template <bool ISO>
+// derived_fields.cpp:164-180 + stiffness_mul :66-80 for element e (tet4: 4 local nodes). HEX (native
+// hex8, SURVEY 8f4, parity unpinned): the same statement order over 8 corners with the element-centre
+// gradients cwf_preprocess_hex8 stores in the 24 gradient slots, i.e. the centroid strain.
+template <bool ISO, bool HEX = false>
 __device__ __forceinline__ void element_tensors(const DevSys &s, const float *__restrict__ u, uint32_t e,
                                                 ElemTensors &t)
 {
-    const uint4 q0 = s.erec[4u * e + 0u];
-    const uint4 g0 = s.erec[4u * e + 1u], g1 = s.erec[4u * e + 2u], g2 = s.erec[4u * e + 3u];
-    const uint32_t c[4] = {q0.x, q0.y, q0.z, q0.w};
-    const float g[12] = {__uint_as_float(g0.x), __uint_as_float(g0.y), __uint_as_float(g0.z), __uint_as_float(g0.w),
-                         __uint_as_float(g1.x), __uint_as_float(g1.y), __uint_as_float(g1.z), __uint_as_float(g1.w),
-                         __uint_as_float(g2.x), __uint_as_float(g2.y), __uint_as_float(g2.z), __uint_as_float(g2.w)};
+    constexpr int K = HEX ? 8 : 4;
+    uint32_t c[K];
+    float g[3 * K];
+    if constexpr (HEX)
+    {
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+            c[a] = s.hconn[8ull * e + a];
+#pragma unroll
+        for (int i = 0; i < 24; ++i)
+            g[i] = s.hgrad[24ull * e + i];
+    }
+    else
+    {
+        const uint4 q0 = s.erec[4u * e + 0u];
+        const uint4 g0 = s.erec[4u * e + 1u], g1 = s.erec[4u * e + 2u], g2 = s.erec[4u * e + 3u];
+        const uint32_t cc[4] = {q0.x, q0.y, q0.z, q0.w};
+        const float gg[12] = {__uint_as_float(g0.x), __uint_as_float(g0.y), __uint_as_float(g0.z),
+                              __uint_as_float(g0.w), __uint_as_float(g1.x), __uint_as_float(g1.y),
+                              __uint_as_float(g1.z), __uint_as_float(g1.w), __uint_as_float(g2.x),
+                              __uint_as_float(g2.y), __uint_as_float(g2.z), __uint_as_float(g2.w)};
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+            c[a] = cc[a];
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+            g[i] = gg[i];
+    }
     double e6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < K; ++a)
     {
         const double ux = (double)u[3ull * c[a] + 0], uy = (double)u[3ull * c[a] + 1], uz = (double)u[3ull * c[a] + 2];
         const double gx = (double)g[3 * a], gy = (double)g[3 * a + 1], gz = (double)g[3 * a + 2];
@@ -84,7 +108,7 @@ __device__ __forceinline__ double von_mises(const double s[6])
     return sqrt(energy < 0.0 ? 0.0 : energy);  // std::max(energy, 0.0), NaN passes through
 }
 
-template <bool ISO>
+template <bool ISO, bool HEX>
 __global__ __launch_bounds__(kBlock) void k_derived_elements(DevSys s, const float *__restrict__ u,
                                                              float *__restrict__ out)
 {
@@ -92,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void k_derived_elements(DevSys s, const flo
     if (e >= s.E)
         return;
     ElemTensors t;
-    element_tensors<ISO>(s, u, e, t);
+    element_tensors<ISO, HEX>(s, u, e, t);
     float *o = out + 13ull * e;
 #pragma unroll
     for (int c = 0; c < 6; ++c)
@@ -103,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void k_derived_elements(DevSys s, const flo
     o[12] = (float)von_mises(t.stress);
 }
 
-template <bool ISO>
+template <bool ISO, bool HEX>
 __global__ __launch_bounds__(kBlock) void k_derived_nodes(DevSys s, const float *__restrict__ u, float *__restrict__ out)
 {
     const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
@@ -112,9 +136,9 @@ __global__ __launch_bounds__(kBlock) void k_derived_nodes(DevSys s, const float 
     double ws = 0.0, as[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, at[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     for (uint32_t q = s.off[n]; q < s.off[n + 1]; ++q)
     {
-        const uint32_t e = s.inc[q] >> 2;
+        const uint32_t e = s.inc[q] >> (HEX ? 3 : 2);
         ElemTensors t;
-        element_tensors<ISO>(s, u, e, t);
+        element_tensors<ISO, HEX>(s, u, e, t);
         const double vol = (double)s.vol[e];
         ws += vol;  // accumulate_node (derived_fields.cpp:82-95)
 #pragma unroll
@@ -146,25 +170,32 @@ __global__ __launch_bounds__(kBlock) void k_derived_nodes(DevSys s, const float 
 
 inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-}  // namespace
-
-void derived_fields(cwf_hip_system *h, const float *u, float *elem_out, float *node_out, hipStream_t st)
+template <bool HEX>
+void derived_fields_k(const DevSys &s, const float *u, float *elem_out, float *node_out, hipStream_t st)
 {
-    const DevSys &s = h->ds;
     if (s.E && elem_out)
     {
         if (s.iso)
-            k_derived_elements<true><<<grid_for(s.E), kBlock, 0, st>>>(s, u, elem_out);
+            k_derived_elements<true, HEX><<<grid_for(s.E), kBlock, 0, st>>>(s, u, elem_out);
         else
-            k_derived_elements<false><<<grid_for(s.E), kBlock, 0, st>>>(s, u, elem_out);
+            k_derived_elements<false, HEX><<<grid_for(s.E), kBlock, 0, st>>>(s, u, elem_out);
     }
     if (s.N && node_out)
     {
         if (s.iso)
-            k_derived_nodes<true><<<grid_for(s.N), kBlock, 0, st>>>(s, u, node_out);
+            k_derived_nodes<true, HEX><<<grid_for(s.N), kBlock, 0, st>>>(s, u, node_out);
         else
-            k_derived_nodes<false><<<grid_for(s.N), kBlock, 0, st>>>(s, u, node_out);
+            k_derived_nodes<false, HEX><<<grid_for(s.N), kBlock, 0, st>>>(s, u, node_out);
     }
+}
+}  // namespace
+
+void derived_fields(cwf_hip_system *h, const float *u, float *elem_out, float *node_out, hipStream_t st)
+{
+    if (h->ds.hex)
+        derived_fields_k<true>(h->ds, u, elem_out, node_out, st);
+    else
+        derived_fields_k<false>(h->ds, u, elem_out, node_out, st);
 }
 
 }  // namespace cwf

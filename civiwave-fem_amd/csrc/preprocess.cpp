@@ -128,3 +128,124 @@ extern "C" int cwf_preprocess_tets(uint64_t N, uint64_t E, const double *coords,
         }
     return 0;
 }
+
+// ---- native hex8 ---------------------------------------------------------------
+// The reference stops here ("only tetrahedron elements supported in Phase 3", preprocess.cpp:326-330);
+// this is the trilinear isoparametric element (Gmsh/VTK corner order, 2x2x2 Gauss) the FAST hex8
+// kernels integrate: V = sum_gp det J, lumped mass rho V / 8 per corner, grads24 = dN_a/dx at the
+// element centre (the 8 x 3 gradient slots the packed layout reserves, pcg.hpp:67-86; the post
+// stack's centroid strain reads them). Parity unpinned (no reference arithmetic exists).
+namespace
+{
+const double kHexSign[8][3] = {{-1, -1, -1}, {1, -1, -1}, {1, 1, -1}, {-1, 1, -1},
+                               {-1, -1, 1},  {1, -1, 1},  {1, 1, 1},  {-1, 1, 1}};
+
+// dN_a/dx at reference point q of the hex with corners X; returns det J
+double hex_grads(const double X[8][3], const double q[3], double g[8][3])
+{
+    double dN[8][3], J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int a = 0; a < 8; ++a)
+    {
+        const double *s = kHexSign[a];
+        const double f0 = 1.0 + s[0] * q[0], f1 = 1.0 + s[1] * q[1], f2 = 1.0 + s[2] * q[2];
+        dN[a][0] = 0.125 * s[0] * f1 * f2;
+        dN[a][1] = 0.125 * f0 * s[1] * f2;
+        dN[a][2] = 0.125 * f0 * f1 * s[2];
+        for (int m = 0; m < 3; ++m)
+            for (int l = 0; l < 3; ++l)
+                J[m][l] += X[a][m] * dN[a][l];
+    }
+    double A[3][3];
+    A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+    A[0][1] = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+    A[0][2] = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+    A[1][0] = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+    A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+    A[1][2] = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+    A[2][0] = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+    A[2][1] = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+    A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    const double det = J[0][0] * A[0][0] + J[0][1] * A[1][0] + J[0][2] * A[2][0];
+    for (int a = 0; a < 8; ++a)
+        for (int m = 0; m < 3; ++m)
+            g[a][m] = (dN[a][0] * A[0][m] + dN[a][1] * A[1][m] + dN[a][2] * A[2][m]) / det;
+    return det;
+}
+}  // namespace
+
+extern "C" int cwf_preprocess_hex8(uint64_t N, uint64_t E, const double *coords, const uint32_t *hexes,
+                                   const uint32_t *material_index, const double *density, uint64_t material_count,
+                                   float *grads24, float *volume, double *mass64, float *mass32, uint32_t *offsets,
+                                   uint32_t *adj_elem, uint8_t *adj_local, uint32_t *conn8)
+{
+    using cwf::set_error;
+    if ((N && (!coords || !mass64 || !mass32 || !offsets)) ||
+        (E && (!hexes || !material_index || !density || !grads24 || !volume || !adj_elem || !adj_local)))
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    if (N == 0)
+        return set_error(nullptr, CWF_ERR_SIZE, "mesh has zero nodes", "mesh");
+    if (E == 0)
+        return set_error(nullptr, CWF_ERR_SIZE, "mesh has zero elements", "mesh");
+    const double r = 1.0 / std::sqrt(3.0);
+    std::vector<uint32_t> counts(N, 0);
+    for (uint64_t n = 0; n < N; ++n)
+        mass64[n] = 0.0;
+    for (uint64_t e = 0; e < E; ++e)
+    {
+        double X[8][3], g[8][3];
+        for (int a = 0; a < 8; ++a)
+        {
+            const uint32_t n = hexes[e * 8 + a];
+            if (n >= N)
+                return set_error(nullptr, CWF_ERR_NODE_RANGE, "element references node out of range",
+                                 "elements [" + std::to_string(e) + "]");
+            for (int m = 0; m < 3; ++m)
+                X[a][m] = coords[3 * (uint64_t)n + m];
+            ++counts[n];
+        }
+        if (material_index[e] >= material_count)
+            return set_error(nullptr, CWF_ERR_MATERIAL_RANGE, "element physical group missing assignment",
+                             "elements [" + std::to_string(e) + "]");
+        double vol = 0.0;
+        for (int p = 0; p < 8; ++p)
+        {
+            const double q[3] = {(p & 1) ? r : -r, (p & 2) ? r : -r, (p & 4) ? r : -r};
+            const double det = hex_grads(X, q, g);
+            if (!(det > 0.0))
+                return set_error(nullptr, CWF_ERR_SIZE, "hexahedron Jacobian non-positive (inverted or degenerate)",
+                                 "elements [" + std::to_string(e) + "]");
+            vol += det;
+        }
+        const double q0[3] = {0.0, 0.0, 0.0};
+        (void)hex_grads(X, q0, g);
+        float *gr = grads24 + e * 24;
+        for (int a = 0; a < 8; ++a)
+            for (int m = 0; m < 3; ++m)
+                gr[3 * a + m] = safe_f32(g[a][m]);
+        volume[e] = safe_f32(vol);
+        const double lump = density[material_index[e]] * vol / 8.0;
+        for (int a = 0; a < 8; ++a)
+            mass64[hexes[e * 8 + a]] += lump;
+        if (conn8)
+            for (int a = 0; a < 8; ++a)
+                conn8[e * 8 + a] = hexes[e * 8 + a];
+    }
+    uint32_t acc = 0;
+    for (uint64_t n = 0; n < N; ++n)
+    {
+        offsets[n] = acc;
+        acc += counts[n];
+        counts[n] = 0;
+        mass32[n] = safe_f32(mass64[n]);
+    }
+    offsets[N] = acc;
+    for (uint64_t e = 0; e < E; ++e)
+        for (int a = 0; a < 8; ++a)
+        {
+            const uint32_t n = hexes[e * 8 + a];
+            const uint32_t w = offsets[n] + counts[n]++;
+            adj_elem[w] = (uint32_t)e;
+            adj_local[w] = (uint8_t)a;
+        }
+    return 0;
+}

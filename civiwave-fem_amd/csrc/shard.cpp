@@ -45,6 +45,9 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
     if (!d || !rank_node_begin || !out)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
     *out = nullptr;
+    if (d->element_count && d->element_connectivity && d->element_connectivity[4] != 0xFFFFFFFFu)
+        return set_error(nullptr, CWF_ERR_UNSUPPORTED, "sharding supports tet4 systems only",
+                         "hex8 (SURVEY 8f4) runs on one handle");
     if (nranks < 1 || rank < 0 || rank >= nranks)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "rank out of range",
                          "nranks=" + std::to_string(nranks) + " rank=" + std::to_string(rank));

@@ -1339,6 +1339,8 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
         k_keff_tiles<ISO, SAN, MODE, 256, GEO><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
 }
 
+#include "hex8_tiles.inc"
+
 // pipelined kernel: element forces + local CSR + per tile node {x y z v_x}{v_y v_z}
 inline size_t pipe_lds(const DevSys &s)
 {
@@ -1378,6 +1380,11 @@ template <bool ISO, bool SAN, int MODE>
 void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st,
                   hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
+    if (s.t.hex)
+    {
+        launch_hex<ISO, SAN, MODE>(s, x, pa, st, e0, e1);
+        return;
+    }
     if (s.t.pipe)
     {
         if (s.t.pipe_nt == 128)
@@ -1399,10 +1406,12 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
 }
 }  // namespace
 
-unsigned fast_tile_blocks(const DevSys &s) { return s.t.pipe ? s.t.pipe_grid : s.t.ntiles; }
+unsigned fast_tile_blocks(const DevSys &s) { return (s.t.pipe || s.t.hex) ? s.t.pipe_grid : s.t.ntiles; }
 
 unsigned fast_pipe_grid(const DevSys &s)
 {
+    if (s.t.hex)
+        return s.iso ? hex_grid_query<true>(s) : hex_grid_query<false>(s);
     if (s.t.push)
     {
         if (s.t.pipe_nt == 128)
@@ -1514,7 +1523,10 @@ void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 
 void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
 {
-    parity_block_jacobi(h, h->inv, st);
+    if (h->ds.hex)
+        hex_block_jacobi(h, h->inv, st);
+    else
+        parity_block_jacobi(h, h->inv, st);
     if (h->ds.N)
         k_sym_inverse<<<grid_for(h->ds.N, 256), 256, 0, st>>>(h->ds.N, h->inv, h->inv6);
 }

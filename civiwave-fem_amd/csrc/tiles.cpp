@@ -36,9 +36,10 @@ inline uint64_t spread21(uint64_t v)
 }
 }  // namespace
 
-int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems)
+int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems, int corners)
 {
     const uint64_t N = d->node_count, E = d->element_count;
+    const int K = corners == 8 ? 8 : 4;  // tet4 or hex8 (slots 0..K-1 of the 8-slot connectivity)
     std::vector<uint32_t> order(E);
     std::iota(order.begin(), order.end(), 0u);
     if (d->node_coords && E)
@@ -58,12 +59,12 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
         for (uint64_t e = 0; e < E; ++e)
         {
             double c[3] = {0, 0, 0};
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < K; ++a)
                 for (int k = 0; k < 3; ++k)
                     c[k] += d->node_coords[3 * (uint64_t)d->element_connectivity[e * 8 + a] + k];
             uint64_t q[3];
             for (int k = 0; k < 3; ++k)
-                q[k] = (uint64_t)std::llround((c[k] * 0.25 - lo[k]) * scale);
+                q[k] = (uint64_t)std::llround((c[k] / K - lo[k]) * scale);
             key[e] = spread21(q[0]) | spread21(q[1]) << 1 | spread21(q[2]) << 2;
         }
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
@@ -73,13 +74,21 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
     out.tile_elem_off.push_back(0);
     out.tile_node_off.push_back(0);
     out.csr_off.push_back(0);
-    for (int q = 0; q < 3; ++q)
-        out.planes[q].resize(E);
+    if (K == 4)
+    {
+        for (int q = 0; q < 3; ++q)
+            out.planes[q].resize(E);
+        out.eid.resize(E);
+        out.epos.resize(E);
+    }
+    else
+    {
+        out.eid8.resize(E);
+        out.epos8.resize(E);
+    }
     if (d->material_count > 1)
         out.mat.resize(E);
-    out.eid.resize(E);
-    out.epos.resize(E);
-    out.csr_ent.reserve(E * 4);
+    out.csr_ent.reserve(E * K);
     std::vector<uint32_t> stamp(N, 0xFFFFFFFFu), local(N, 0);
     std::vector<uint32_t> nodes;
     std::vector<uint32_t> cnt;
@@ -94,11 +103,11 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
         {
             const uint32_t src = order[e];
             uint32_t add = 0;
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < K; ++a)
                 add += stamp[d->element_connectivity[(uint64_t)src * 8 + a]] != tile ? 1u : 0u;
             if (nodes.size() + add > (size_t)max_nodes)
                 break;
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < K; ++a)
             {
                 const uint32_t g = d->element_connectivity[(uint64_t)src * 8 + a];
                 if (stamp[g] != tile)
@@ -118,11 +127,19 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
         for (uint32_t j = 0; j < ne; ++j)
         {
             const uint32_t src = order[e0 + j];
-            uint32_t li[4];
-            for (int a = 0; a < 4; ++a)
+            uint32_t li[8];
+            for (int a = 0; a < K; ++a)
             {
                 li[a] = local[d->element_connectivity[(uint64_t)src * 8 + a]];
                 ++cnt[li[a] + 1];
+            }
+            if (!out.mat.empty())
+                out.mat[e0 + j] = d->element_material_index[src];
+            if (K == 8)
+            {
+                out.eid8[e0 + j] = uint4{li[0] | (li[1] << 16), li[2] | (li[3] << 16), li[4] | (li[5] << 16),
+                                         li[6] | (li[7] << 16)};
+                continue;
             }
             const float *g = d->element_gradients + (uint64_t)src * 24;
             uint4 q0, q1, q2;
@@ -136,25 +153,27 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
             out.planes[0][e0 + j] = q0;
             out.planes[1][e0 + j] = q1;
             out.planes[2][e0 + j] = q2;
-            if (!out.mat.empty())
-                out.mat[e0 + j] = d->element_material_index[src];
         }
         for (uint32_t i = 0; i < nn; ++i)
             cnt[i + 1] += cnt[i];
         const uint64_t base = out.csr_ent.size();
-        out.csr_ent.resize(base + 4ull * ne);
+        out.csr_ent.resize(base + (uint64_t)K * ne);
         std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
         for (uint32_t j = 0; j < ne; ++j)
         {
             const uint32_t src = order[e0 + j];
-            uint32_t epos[4];
-            for (int a = 0; a < 4; ++a)
+            uint32_t epos[8];
+            for (int a = 0; a < K; ++a)
             {
                 const uint32_t l = local[d->element_connectivity[(uint64_t)src * 8 + a]];
                 epos[a] = cur[l];  // the corner's tile-relative local-CSR position (PUSH)
-                out.csr_ent[base + cur[l]++] = (uint16_t)(j * 4 + a);
+                out.csr_ent[base + cur[l]++] = (uint16_t)(j * K + a);
             }
-            out.epos[e0 + j] = uint2{epos[0] | (epos[1] << 16), epos[2] | (epos[3] << 16)};
+            if (K == 8)
+                out.epos8[e0 + j] = uint4{epos[0] | (epos[1] << 16), epos[2] | (epos[3] << 16),
+                                          epos[4] | (epos[5] << 16), epos[6] | (epos[7] << 16)};
+            else
+                out.epos[e0 + j] = uint2{epos[0] | (epos[1] << 16), epos[2] | (epos[3] << 16)};
         }
         for (uint32_t i = 0; i < nn; ++i)
         {

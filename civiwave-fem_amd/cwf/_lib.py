@@ -155,6 +155,7 @@ def load() -> C.CDLL:
         "cwf_hip_system_attach": ([P, P, i32, P], i32),
         "cwf_hip_solve_pcg_group": ([P, i32, P, P, P, i32, P], i32),
         "cwf_preprocess_tets": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),
+        "cwf_preprocess_hex8": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),
         "cwf_hip_derived_fields": ([P, P, u64, i32, P, P, i32], i32),
         "cwf_write_vtu": ([C.c_char_p, P, f64, C.c_uint32], i32),
         "cwf_probe_log_frame": ([C.c_char_p, P, P, u64, P, f64, C.c_uint32], i32),

@@ -55,12 +55,15 @@ class GmshMesh:
             out.setdefault(g, []).append(i)
         return out
 
-    def to_tet_mesh(self) -> pack.Mesh:
+    def to_tet_mesh(self, allow_hex8: bool = False) -> pack.Mesh:
+        """The reference's preprocess input (tet4 only, preprocess.cpp:326-330). allow_hex8: an all-hex8
+        mesh is passed on as native hex8 elements (FAST mode only)."""
         if len(self.coords) == 0:
             raise pack.PackError("mesh has zero nodes", ["mesh"])
         if len(self.geometry) == 0:
             raise pack.PackError("mesh has zero elements", ["mesh"])
-        bad = np.nonzero(self.geometry != 4)[0]
+        K = 8 if allow_hex8 and np.all(self.geometry == 8) else 4
+        bad = np.nonzero(self.geometry != K)[0]
         if bad.size:
             raise pack.PackError("only tetrahedron elements supported in Phase 3", ["elements", f"[{int(bad[0])}]"])
         names = {}
@@ -68,7 +71,7 @@ class GmshMesh:
             names.setdefault(g.name, g.id)
         surf = [(int(g), tuple(int(n) for n in s[: int(k)]))
                 for g, s, k in zip(self.surface_group, self.surfaces, self.surface_geometry)]
-        return pack.Mesh(np.ascontiguousarray(self.coords), np.ascontiguousarray(self.elements[:, :4]),
+        return pack.Mesh(np.ascontiguousarray(self.coords), np.ascontiguousarray(self.elements[:, :K]),
                          np.ascontiguousarray(self.element_group), names, dict(self.node_groups), surf)
 
 

@@ -54,6 +54,33 @@ def kuhn_block(nx: int, ny: int, nz: int, h: float = 1.0) -> TetMesh:
                                   "CORNER": np.array([(nz * B + ny) * A + nx], np.uint32)}, (nx, ny, nz))
 
 
+# hex corner bit pattern (i, j, k) -> Gmsh/VTK hexahedron order 0(-,-,-) 1(+,-,-) 2(+,+,-) 3(-,+,-) 4..7 (z+)
+HEX_GMSH = np.array([0, 1, 3, 2, 4, 5, 7, 6], np.int64)
+
+
+def hex_block(nx: int, ny: int, nz: int, h: float = 1.0) -> TetMesh:
+    """The same structured block as native hex8 elements: nx*ny*nz hexes, [E, 8]
+    connectivity in Gmsh/VTK corner order, the node numbering and groups of kuhn_block."""
+    A, B, Cn = nx + 1, ny + 1, nz + 1
+    k, j, i = np.meshgrid(np.arange(Cn), np.arange(B), np.arange(A), indexing="ij")
+    if h == 1.0:
+        coords = np.stack([i, j, k], -1).reshape(-1, 3).astype(np.float64)
+    else:
+        coords = np.stack([h * i.astype(np.float64), h * j.astype(np.float64), h * k.astype(np.float64)],
+                          -1).reshape(-1, 3)
+    hk, hj, hi = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    hk, hj, hi = hk.reshape(-1), hj.reshape(-1), hi.reshape(-1)
+    corners = np.empty((hk.size, 8), np.int64)
+    for b in range(8):
+        corners[:, b] = ((hk + ((b >> 2) & 1)) * B + (hj + ((b >> 1) & 1))) * A + (hi + (b & 1))
+    hexes = corners[:, HEX_GMSH].astype(np.uint32)
+    kk, jj = np.meshgrid(np.arange(Cn), np.arange(B), indexing="ij")
+    fixed = ((kk * B + jj) * A).reshape(-1).astype(np.uint32)
+    tip = ((kk * B + jj) * A + nx).reshape(-1).astype(np.uint32)
+    return TetMesh(coords, hexes, {"FIXED": fixed, "TIP": tip,
+                                   "CORNER": np.array([(nz * B + ny) * A + nx], np.uint32)}, (nx, ny, nz))
+
+
 def kuhn_slab(nx: int, ny: int, nz: int, kc0: int, kc1: int, h: float = 1.0):
     """Cells k in [kc0, kc1) of the nx*ny*nz Kuhn block (nodes on planes kc0..kc1), numbered
     compactly but in the global order -> (TetMesh, global node id per sub-mesh node). Elements keep
@@ -113,10 +140,18 @@ CONFIGS = {
 }
 
 
+# hex8 faces (Gmsh corner order), each counter-clockwise seen from outside
+HEX_FACES = [[0, 3, 2, 1], [4, 5, 6, 7], [0, 1, 5, 4], [1, 2, 6, 5], [2, 3, 7, 6], [3, 0, 4, 7]]
+
+
 def boundary_faces(tets: np.ndarray, nodes) -> np.ndarray:
-    """Boundary triangles (faces of exactly one tet) whose three nodes all lie in `nodes` -> u32 [F,3]."""
+    """Boundary faces (faces of exactly one element) whose nodes all lie in `nodes`: triangles u32 [F,3]
+    of a tet4 mesh, quads u32 [F,4] of a hex8 mesh."""
     t = np.asarray(tets, np.int64)
-    faces = np.concatenate([t[:, [0, 1, 2]], t[:, [0, 1, 3]], t[:, [0, 2, 3]], t[:, [1, 2, 3]]])
+    if t.shape[1] == 8:
+        faces = np.concatenate([t[:, f] for f in HEX_FACES])
+    else:
+        faces = np.concatenate([t[:, [0, 1, 2]], t[:, [0, 1, 3]], t[:, [0, 2, 3]], t[:, [1, 2, 3]]])
     key = np.sort(faces, 1)
     _, inv, cnt = np.unique(key, axis=0, return_inverse=True, return_counts=True)
     inv = inv.reshape(-1)
@@ -169,14 +204,15 @@ def write_gmsh(tm: TetMesh, path: str, solid: str = "SOLID", surface_groups=("FI
     total = E + sum(len(f) for _, f in surf)
     lines += ["$Elements", f"{1 + len(surf)} {total} 1 {total}"]
     tag = 1
+    hexes = tm.tets.shape[1] == 8  # Gmsh type 5 volumes with type 3 (quad) faces, else type 4 / type 2
     for k, f in surf:
-        lines.append(f"2 {k} 2 {len(f)}")
-        for tri in f.tolist():
-            lines.append(f"{tag} {tri[0] + 1} {tri[1] + 1} {tri[2] + 1}")
+        lines.append(f"2 {k} {3 if hexes else 2} {len(f)}")
+        for face in f.tolist():
+            lines.append(f"{tag} " + " ".join(str(v + 1) for v in face))
             tag += 1
-    lines.append(f"3 1 4 {E}")
+    lines.append(f"3 1 {5 if hexes else 4} {E}")
     for t in tm.tets.tolist():
-        lines.append(f"{tag} {t[0] + 1} {t[1] + 1} {t[2] + 1} {t[3] + 1}")
+        lines.append(f"{tag} " + " ".join(str(v + 1) for v in t))
         tag += 1
     lines.append("$EndElements")
     with open(path, "w") as fh:

@@ -19,10 +19,10 @@ from .physics import Config, evaluate_curve
 
 @dataclass
 class Mesh:
-    """Subset of cwf::mesh::Mesh (include/cwf/mesh/mesh.hpp:120-150) for tet4 meshes."""
+    """Subset of cwf::mesh::Mesh (include/cwf/mesh/mesh.hpp:120-150) for tet4 (or native hex8) meshes."""
 
     coords: np.ndarray  # f64 [N,3]
-    tets: np.ndarray  # u32 [E,4]
+    tets: np.ndarray  # u32 [E,4] (tet4) or [E,8] (hex8, Gmsh corner order; FAST mode only)
     element_group: np.ndarray | None = None  # u32 [E] physical group id per element
     group_names: dict = field(default_factory=dict)  # name -> id
     node_groups: dict = field(default_factory=dict)  # id -> u32 node indices
@@ -122,14 +122,16 @@ def preprocess(mesh: Mesh, cfg: Config):
         raise PackError("element physical group missing assignment", ["elements", f"[{int(bad[0])}]"])
     coords = np.ascontiguousarray(mesh.coords, np.float64)
     tets = np.ascontiguousarray(mesh.tets, np.uint32)
+    K = tets.shape[1] if tets.ndim == 2 else 4  # 4: tet4 (the reference path), 8: native hex8
     out = dict(grads=np.zeros(E * 24, np.float32), volume=np.zeros(E, np.float32), mass64=np.zeros(N, np.float64),
                mass32=np.zeros(N, np.float32), offsets=np.zeros(N + 1, np.uint32),
-               adj_elem=np.zeros(E * 4, np.uint32), adj_local=np.zeros(E * 4, np.uint8),
+               adj_elem=np.zeros(E * K, np.uint32), adj_local=np.zeros(E * K, np.uint8),
                conn8=np.zeros(E * 8, np.uint32), material_index=mat)
     p = _lib.ptr
-    st = L.cwf_preprocess_tets(N, E, p(coords), p(tets), p(mat), p(density), len(cfg.materials), p(out["grads"]),
-                               p(out["volume"]), p(out["mass64"]), p(out["mass32"]), p(out["offsets"]),
-                               p(out["adj_elem"]), p(out["adj_local"]), p(out["conn8"]))
+    fn = L.cwf_preprocess_hex8 if K == 8 else L.cwf_preprocess_tets
+    st = fn(N, E, p(coords), p(tets), p(mat), p(density), len(cfg.materials), p(out["grads"]),
+            p(out["volume"]), p(out["mass64"]), p(out["mass32"]), p(out["offsets"]),
+            p(out["adj_elem"]), p(out["adj_local"]), p(out["conn8"]))
     if st:
         msg, ctx = _lib.last_error(None)
         raise PackError(msg, ctx)

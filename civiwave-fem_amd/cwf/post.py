@@ -56,7 +56,9 @@ def compute_derived_fields(packing, materials=None, system: MatrixFreeSystem | N
     device tensor (e.g. the Stepper's state)."""
     own = system is None
     if own:
-        system = MatrixFreeSystem.from_packing(packing, materials, 1.0, 0.0, _lib.MODE_PARITY)
+        hex8 = packing.element_count and int(packing.connectivity[4]) != 0xFFFFFFFF  # native hex8: FAST only
+        system = MatrixFreeSystem.from_packing(packing, materials, 1.0, 0.0,
+                                               _lib.MODE_FAST if hex8 else _lib.MODE_PARITY)
     try:
         u = packing.displacement if displacement is None else displacement
         ukind = _lib.PTR_HOST if isinstance(u, np.ndarray) else _lib.PTR_DEVICE

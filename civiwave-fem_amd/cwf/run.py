@@ -41,8 +41,9 @@ def resolve_mesh_path(cfg_path: str, mesh_path: str) -> str:
     return mesh_path
 
 
-def load_scenario(cfg_path: str):
-    """-> (config, tet mesh, packing, materials). Raises ScenarioError with the reference's texts."""
+def load_scenario(cfg_path: str, allow_hex8: bool = False):
+    """-> (config, tet mesh, packing, materials). Raises ScenarioError with the reference's texts.
+    allow_hex8: an all-hex8 Gmsh mesh runs as native hex8 (FAST mode only)."""
     rc = config.load_config_from_file(cfg_path)
     if not rc.has_value():
         raise ScenarioError(f"config: {rc.error().message} {rc.error().context}")
@@ -51,7 +52,7 @@ def load_scenario(cfg_path: str):
     if not rm.has_value():
         raise ScenarioError(f"mesh: {rm.error().message} {rm.error().context}")
     try:
-        m = rm.value().to_tet_mesh()
+        m = rm.value().to_tet_mesh(allow_hex8)
         P = pack.build_packed_buffers(m, cfg)
     except pack.PackError as e:
         raise ScenarioError(f"preprocess: {e.message} {e.context}") from None
@@ -60,7 +61,7 @@ def load_scenario(cfg_path: str):
 
 def run_scenario(cfg_path: str, steps: int, out_dir: str | None, mode: int = _lib.MODE_PARITY, device: int = 0,
                  paused: bool = False, time_varying_loads: bool = False, log=print) -> dict:
-    cfg, m, P, materials = load_scenario(cfg_path)
+    cfg, m, P, materials = load_scenario(cfg_path, allow_hex8=mode == _lib.MODE_FAST)
     st = Stepper(P, materials, compute_rayleigh(cfg.damping), cfg.solver, cfg.time, mode=mode, device=device)
     om = post.OutputManager(out_dir, m, P, materials, cfg.output, stepper=st) if out_dir else None
     t_sim, total_iters, wall0 = 0.0, 0, time.perf_counter()

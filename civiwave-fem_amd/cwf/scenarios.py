@@ -48,20 +48,24 @@ def make_config(xi=0.02, w=(5.0, 50.0), tol=3e-4, max_iterations=2000, dt=0.01, 
                   dirichlet=[DirichletFix("FIXED", (True, True, True), (0.0, 0.0, 0.0))])
 
 
-def block_case(nx, ny, nz, h=0.1, jitter=False, **cfg_kw) -> Case:
-    tm = meshgen.kuhn_block(nx, ny, nz, h)
+def block_case(nx, ny, nz, h=0.1, jitter=False, element="tet4", **cfg_kw) -> Case:
+    """element="tet4": the Kuhn expansion (the reference's path); "hex8": native hexes (SURVEY 8f4,
+    FAST mode only)."""
+    tm = meshgen.hex_block(nx, ny, nz, h) if element == "hex8" else meshgen.kuhn_block(nx, ny, nz, h)
     if jitter:
         tm = meshgen.jitter_and_permute(tm, h)
     mesh = pack.from_tetmesh(tm)
     cfg = make_config(**cfg_kw)
-    return Case(f"kuhn{nx}x{ny}x{nz}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
+    tag = "hex" if element == "hex8" else "kuhn"
+    return Case(f"{tag}{nx}x{ny}x{nz}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
 
 
-def config_case(key: str, max_iterations: int = 2000) -> Case:
+def config_case(key: str, max_iterations: int = 2000, element: str = "tet4") -> Case:
     c = meshgen.CONFIGS[key]
     case = block_case(*c["shape"], h=c["h"], jitter=c.get("jitter", False), xi=c["xi"], w=c["w"], tol=c["tol"],
-                      max_iterations=max_iterations)
-    case.name = f"{key}: {c['name']}"
+                      max_iterations=max_iterations, element=element)
+    name = c["name"].replace("(Kuhn tets)", "(native hex8)") if element == "hex8" else c["name"]
+    case.name = f"{key}: {name}"
     return case
 
 

@@ -282,6 +282,17 @@ int cwf_preprocess_tets(uint64_t node_count, uint64_t element_count, const doubl
                         float *grads24, float *volume, double *mass64, float *mass32, uint32_t *offsets,
                         uint32_t *adj_elem, uint8_t *adj_local, uint32_t *conn8);
 
+/* Native hex8 (no reference counterpart: the reference rejects hex8 in
+ * preprocess.cpp:326-330, so parity is unpinned). Trilinear isoparametric element, Gmsh/VTK corner
+ * order, 2x2x2 Gauss: volume = sum_gp det J, lumped mass rho V / 8 per corner, grads24 = dN_a/dx at
+ * the element centre; CSR with 8E incidences (adj_local 0..7); conn8 = hexes. A system_desc whose
+ * connectivity fills all 8 slots is a hex8 system: CWF_MODE_FAST only, node_coords required.
+ * Errors: "hexahedron Jacobian non-positive (inverted or degenerate)" {"elements [e]"} (CWF_ERR_SIZE). */
+int cwf_preprocess_hex8(uint64_t node_count, uint64_t element_count, const double *coords, const uint32_t *hexes,
+                        const uint32_t *material_index, const double *density, uint64_t material_count,
+                        float *grads24, float *volume, double *mass64, float *mass32, uint32_t *offsets,
+                        uint32_t *adj_elem, uint8_t *adj_local, uint32_t *conn8);
+
 /* ---- post stack ---------------------------------------------------------- */
 
 /* cwf::post::compute_derived_fields (src/post/derived_fields.cpp:139-211), on the device and bit-exact:

@@ -118,6 +118,19 @@ int orc_dense_newmark_step(uint64_t n, const double *K, const double *mass_diag,
                            double tolerance, uint64_t max_iterations, double *u1, double *v1, double *acc1,
                            orc_dense_stats *stats);
 
+/* native hex8 (hex8_oracle.c; parity unpinned: the reference rejects hex8) */
+int orc_hex8_preprocess(uint64_t N, uint64_t E, const double *coords, const uint32_t *conn8,
+                        const uint32_t *material_index, const double *density, uint64_t material_count,
+                        double *volume, double *mass64, float *grads24);
+int orc_hex8_apply(uint64_t N, uint64_t E, const double *coords, const uint32_t *conn8, const uint32_t *material_index,
+                   const double *D36, double sK, double sM, const float *mass, const uint32_t *mask, const float *x,
+                   float *y, double *acc);
+int orc_hex8_apply64(uint64_t N, uint64_t E, const double *coords, const uint32_t *conn8,
+                     const uint32_t *material_index, const double *D36, double sK, double sM, const float *mass,
+                     const uint32_t *mask, const double *x, double *y);
+int orc_hex8_diag_blocks(uint64_t N, uint64_t E, const double *coords, const uint32_t *conn8,
+                         const uint32_t *material_index, const double *D36, double sK, double *blocks);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,8 +39,8 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
-            os.path.join(_HERE, "cwf_oracle.c")
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < max(
+            os.path.getmtime(os.path.join(_HERE, f)) for f in ("cwf_oracle.c", "hex8_oracle.c", "cwf_oracle.h")
         ):
             build()
         L = C.CDLL(_LIB_PATH)
@@ -73,6 +73,14 @@ def lib():
         L.orc_dense_newmark_step.restype = i32
         L.orc_derived_fields.argtypes = [P, P, P, P]
         L.orc_derived_fields.restype = i32
+        L.orc_hex8_preprocess.argtypes = [u64, u64, P, P, P, P, u64, P, P, P]
+        L.orc_hex8_preprocess.restype = i32
+        L.orc_hex8_apply.argtypes = [u64, u64, P, P, P, P, f64, f64, P, P, P, P, P]
+        L.orc_hex8_apply.restype = i32
+        L.orc_hex8_apply64.argtypes = [u64, u64, P, P, P, P, f64, f64, P, P, P, P]
+        L.orc_hex8_apply64.restype = i32
+        L.orc_hex8_diag_blocks.argtypes = [u64, u64, P, P, P, P, f64, P]
+        L.orc_hex8_diag_blocks.restype = i32
         _lib = L
     return _lib
 
@@ -415,3 +423,98 @@ def fnv1a64_words(x: np.ndarray) -> str:
     for w in np.ascontiguousarray(x, np.float32).view(np.uint32).tolist():
         h = ((h ^ w) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
     return f"{h:016x}"
+
+
+# ---- native hex8 (hex8_oracle.c): PARITY UNPINNED -- the reference rejects hex8 elements
+# (src/mesh/preprocess.cpp:326-330); this is the textbook fp64 isoparametric element the GPU
+# hex8 kernels are checked against, plus physics checks in the tests.
+def hex8_preprocess(coords: np.ndarray, hexes: np.ndarray, material_index: np.ndarray, density):
+    """-> (volume f64 [E], lumped mass f64 [N], centroid gradients f32 [E*24])"""
+    coords = np.ascontiguousarray(coords, np.float64)
+    hexes = np.ascontiguousarray(hexes, np.uint32).reshape(-1, 8)
+    mat = np.ascontiguousarray(material_index, np.uint32)
+    dens = np.ascontiguousarray(np.atleast_1d(density), np.float64)
+    N, E = coords.shape[0], hexes.shape[0]
+    vol, mass, grads = np.zeros(E), np.zeros(N), np.zeros(E * 24, np.float32)
+    st = lib().orc_hex8_preprocess(N, E, _p(coords), _p(hexes), _p(mat), _p(dens), dens.size, _p(vol), _p(mass),
+                                   _p(grads))
+    if st:
+        raise OracleError(st)
+    return vol, mass, grads
+
+
+def hex8_apply(coords, hexes, material_index, D36s, sK, sM, mass, mask, x) -> np.ndarray:
+    """y = K_eff x (fp64 accumulation, f32 out) with apply_keff's Dirichlet semantics."""
+    coords = np.ascontiguousarray(coords, np.float64)
+    hexes = np.ascontiguousarray(hexes, np.uint32).reshape(-1, 8)
+    mat = np.ascontiguousarray(material_index, np.uint32)
+    D = np.ascontiguousarray(D36s, np.float64)
+    mass = np.ascontiguousarray(mass, np.float32)
+    mask = np.ascontiguousarray(mask, np.uint32)
+    x = np.ascontiguousarray(x, np.float32)
+    N, E = coords.shape[0], hexes.shape[0]
+    y, acc = np.zeros(3 * N, np.float32), np.zeros(3 * N)
+    st = lib().orc_hex8_apply(N, E, _p(coords), _p(hexes), _p(mat), _p(D), sK, sM, _p(mass), _p(mask), _p(x), _p(y),
+                              _p(acc))
+    if st:
+        raise OracleError(st)
+    return y
+
+
+def hex8_diag_blocks(coords, hexes, material_index, D36s, sK) -> np.ndarray:
+    """node diagonal 3x3 blocks of the assembled stiffness (x sK), f64 [N, 3, 3]"""
+    coords = np.ascontiguousarray(coords, np.float64)
+    hexes = np.ascontiguousarray(hexes, np.uint32).reshape(-1, 8)
+    mat = np.ascontiguousarray(material_index, np.uint32)
+    D = np.ascontiguousarray(D36s, np.float64)
+    N, E = coords.shape[0], hexes.shape[0]
+    out = np.zeros(9 * N)
+    st = lib().orc_hex8_diag_blocks(N, E, _p(coords), _p(hexes), _p(mat), _p(D), sK, _p(out))
+    if st:
+        raise OracleError(st)
+    return out.reshape(N, 3, 3)
+
+
+def hex8_solve64(coords, hexes, material_index, D36s, sK, sM, mass, mask, rhs, tol=1e-11, max_iterations=20000):
+    """fp64 block-Jacobi PCG on the fp64 hex8 operator (the reference solution for the GPU tests)."""
+    coords = np.ascontiguousarray(coords, np.float64)
+    hexes = np.ascontiguousarray(hexes, np.uint32).reshape(-1, 8)
+    mat = np.ascontiguousarray(material_index, np.uint32)
+    D = np.ascontiguousarray(D36s, np.float64)
+    mass = np.ascontiguousarray(mass, np.float32)
+    mask = np.ascontiguousarray(mask, np.uint32)
+    N, E = coords.shape[0], hexes.shape[0]
+    L = lib()
+
+    def A(v):
+        v = np.ascontiguousarray(v, np.float64)
+        out = np.zeros(3 * N)
+        L.orc_hex8_apply64(N, E, _p(coords), _p(hexes), _p(mat), _p(D), sK, sM, _p(mass), _p(mask), _p(v), _p(out))
+        return out
+
+    blk = hex8_diag_blocks(coords, hexes, mat, D, sK) + (mass.astype(np.float64) * sM)[:, None, None] * np.eye(3)
+    fixed = np.repeat(mask, 3) & np.tile(np.array([1, 2, 4], np.uint32), N)
+    for k in range(3):
+        c = (mask & (1 << k)) != 0
+        blk[c, k, :] = 0.0
+        blk[c, :, k] = 0.0
+        blk[c, k, k] = 1.0
+    inv = np.linalg.inv(blk)
+    b = np.asarray(rhs, np.float64).copy()
+    x = np.where(fixed != 0, b, 0.0)
+    r = b - A(x)
+    z = np.einsum("nij,nj->ni", inv, r.reshape(-1, 3)).reshape(-1)
+    p = z.copy()
+    rz = r @ z
+    nb = np.linalg.norm(b)
+    for _ in range(max_iterations):
+        Ap = A(p)
+        al = rz / (p @ Ap)
+        x += al * p
+        r -= al * Ap
+        if np.linalg.norm(r) <= tol * nb:
+            break
+        z = np.einsum("nij,nj->ni", inv, r.reshape(-1, 3)).reshape(-1)
+        rz, rz0 = r @ z, rz
+        p = z + (rz / rz0) * p
+    return x

@@ -45,10 +45,11 @@ output:
 
 
 def write_block_scenario(dirname, nx, ny, nz, h=0.1, xi=0.02, w=(5.0, 50.0), tol=3e-4, maxit=2000, stride=2,
-                         relative=True):
+                         relative=True, element="tet4"):
     """Writes block.msh + block.yaml for the Kuhn block (same mesh, config and loads as
-    scenarios.block_case(nx, ny, nz, h, xi=xi, w=w, tol=tol, max_iterations=maxit)) -> yaml path."""
-    tm = meshgen.kuhn_block(nx, ny, nz, h)
+    scenarios.block_case(nx, ny, nz, h, xi=xi, w=w, tol=tol, max_iterations=maxit)) -> yaml path.
+    element="hex8": the same block as native hex8 elements with quad boundary faces."""
+    tm = meshgen.hex_block(nx, ny, nz, h) if element == "hex8" else meshgen.kuhn_block(nx, ny, nz, h)
     msh = os.path.join(dirname, "block.msh")
     meshgen.write_gmsh(tm, msh, node_groups=["FIXED", "TIP"])
     y = os.path.join(dirname, "block.yaml")
