@@ -174,7 +174,8 @@ def main():
     if tpath == "auto":
         import glob
 
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{args.config}_{args.mode}_pmc.json")))
+        tag = f"{args.config}_{args.mode}" + ("_hex8" if args.element == "hex8" else "")
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc.json")))
         tpath = cands[-1] if cands and world == 1 else None
     if tpath and os.path.exists(tpath):
         traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
