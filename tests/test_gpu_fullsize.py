@@ -1,0 +1,110 @@
+"""BASELINE.json's full sizes on the GPU.
+
+C2 = configs[1] (69^3 hex block -> 1,971,054 Kuhn tets, 1.03M DOF): PARITY is bit-exact against the
+pinned oracle at full size: apply_keff, the block-Jacobi inverse, and 25 PCG iterations (x, r, the fp64
+residual history, the max-iterations stop).
+C3 = configs[2] (149^3 -> 19.8M tets, 10.1M DOF, Rayleigh): PARITY apply_keff bit-exact against the
+oracle over the whole vector, plus size-independent properties of the FAST path: symmetry of the
+constrained operator, rigid translation in the interior, FAST within 2e-5 of PARITY (relative to the
+operator scale), and a FAST Newmark step that converges with the PARITY step's iteration count +-15%.
+"""
+import numpy as np
+import pytest
+
+from cwf import _lib, pcg, scenarios
+from cwf.stepper import Stepper
+from helpers import assert_bitwise, oracle_system
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c2():
+    return scenarios.config_case("c2")
+
+
+@pytest.fixture(scope="module")
+def c3():
+    return scenarios.config_case("c3")
+
+
+def _system(case, mode):
+    return pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, *case.scalars(), mode=mode)
+
+
+def test_c2_parity_apply_and_block_jacobi_bitwise(c2):
+    s = _system(c2, _lib.MODE_PARITY)
+    o = oracle_system(c2.packing, c2.materials, *c2.scalars())
+    x = np.random.Generator(np.random.PCG64(21)).uniform(-1, 1, c2.packing.dof_count).astype(np.float32)
+    y = np.zeros_like(x)
+    pcg.apply_keff(s, x, y).value()
+    assert_bitwise(y, o.apply_keff(x), "C2 apply_keff")
+    inv = np.zeros(9 * c2.packing.node_count, np.float32)
+    pcg.build_block_jacobi_inverse(s, None, inv).value()
+    assert_bitwise(inv, o.block_jacobi(), "C2 block inverse")
+    s.close()
+
+
+def test_c2_parity_pcg_25_iterations_bitwise(c2):
+    s = _system(c2, _lib.MODE_PARITY)
+    o = oracle_system(c2.packing, c2.materials, *c2.scalars())
+    rhs = c2.static_rhs()
+    x, r = np.zeros_like(rhs), np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(25, 1e-12), pcg.PcgVectors(x, r)).value()
+    ref = o.solve_pcg(rhs, 25, 1e-12, history=True)
+    rt = ref["telemetry"]
+    assert (t.iterations, t.converged) == (rt.iterations, bool(rt.converged)) == (25, False)
+    assert (t.residual_norm, t.alpha_last, t.beta_last) == (rt.residual_norm, rt.alpha_last, rt.beta_last)
+    assert_bitwise(x, ref["x"], "C2 x")
+    assert_bitwise(r, ref["r"], "C2 r")
+    assert np.array_equal(pcg.residual_history(s), ref["history"])
+    s.close()
+
+
+def test_c3_parity_apply_bitwise_and_fast_properties(c3):
+    P = c3.packing
+    sp = _system(c3, _lib.MODE_PARITY)
+    sf = _system(c3, _lib.MODE_FAST)
+    o = oracle_system(P, c3.materials, *c3.scalars())
+    rng = np.random.Generator(np.random.PCG64(31))
+    x = rng.uniform(-1, 1, P.dof_count).astype(np.float32)
+    yp, yf = np.zeros_like(x), np.zeros_like(x)
+    pcg.apply_keff(sp, x, yp).value()
+    assert_bitwise(yp, o.apply_keff(x), "C3 apply_keff")
+    pcg.apply_keff(sf, x, yf).value()
+    # FAST (fp32 element math, FMA) vs the bit-exact path, relative to the operator scale
+    assert np.max(np.abs(yf.astype(np.float64) - yp)) <= 2e-5 * np.max(np.abs(yp))
+    # symmetry of the constrained operator: a, b zero on Dirichlet dofs
+    free = (np.repeat(P.bc_mask, 3) & np.tile(np.array([1, 2, 4], np.uint32), P.node_count)) == 0
+    a = np.where(free, rng.standard_normal(P.dof_count), 0.0).astype(np.float32)
+    b = np.where(free, rng.standard_normal(P.dof_count), 0.0).astype(np.float32)
+    Ka, Kb = np.zeros_like(a), np.zeros_like(b)
+    pcg.apply_keff(sf, a, Ka).value()
+    pcg.apply_keff(sf, b, Kb).value()
+    ab, ba = float(b.astype(np.float64) @ Ka), float(a.astype(np.float64) @ Kb)
+    assert abs(ab - ba) <= 1e-5 * abs(float(a.astype(np.float64) @ Ka))
+    sp.close()
+    sf.close()
+    # rigid translation: stiffness-only FAST operator, interior nodes (away from the fixed face) carry ~0
+    sk = pcg.MatrixFreeSystem.from_packing(P, c3.materials, 1.0, 0.0, mode=_lib.MODE_FAST)
+    t = np.tile(np.array([1e-3, -2e-3, 5e-4], np.float32), P.node_count)
+    y = np.zeros_like(t)
+    pcg.apply_keff(sk, t, y).value()
+    xs = c3.mesh.coords[:, 0]
+    far = (xs > xs.min() + 0.25) & (xs < xs.max() - 1e-9)
+    yr = y.reshape(-1, 3)
+    assert np.abs(yr[far]).max() <= 1e-6 * 30.0e9 * 0.1 * 2e-3
+    sk.close()
+
+
+def test_c3_fast_newmark_step_matches_parity_iterations(c3):
+    P = c3.packing
+    its = {}
+    for mode in (_lib.MODE_PARITY, _lib.MODE_FAST):
+        st = Stepper(P, c3.materials, c3.rayleigh, c3.cfg.solver, c3.cfg.time, mode=mode)
+        tel = st.step(0.0).value()
+        assert tel.pcg.converged
+        its[mode] = tel.pcg.iterations
+        st.close()
+        st.system.close()
+    assert abs(its[_lib.MODE_FAST] - its[_lib.MODE_PARITY]) <= 0.15 * its[_lib.MODE_PARITY]
