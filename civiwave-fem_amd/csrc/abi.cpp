@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -107,6 +108,94 @@ int stage_in(cwf_hip_system *h, const float *src, float *scratch, uint64_t n, in
     HIPTRY(h, hipMemcpyAsync(scratch, src, n * sizeof(float), hipMemcpyHostToDevice, h->stream));
     *out = scratch;
     return 0;
+}
+
+// caller-order node vector (w floats per node, host or device) -> internal order. Without renumbering a
+// device input is used in place (*out = src); otherwise it lands in `scratch` (internal order).
+int stage_vec(cwf_hip_system *h, const float *src, float *scratch, int kind, int w, const float **out)
+{
+    const uint64_t n = (uint64_t)w * h->ds.N;
+    if (!h->perm)
+        return stage_in(h, src, scratch, n, kind, out);
+    const float *s = src;
+    if (kind != CWF_PTR_DEVICE)
+    {
+        HIPTRY(h, hipMemcpyAsync(h->pbuf, src, n * sizeof(float), hipMemcpyHostToDevice, h->stream));
+        s = h->pbuf;
+    }
+    perm_gather(h->perm, s, scratch, h->ds.N, w, h->stream);
+    *out = scratch;
+    return 0;
+}
+
+// caller-order input into a fixed internal buffer (always copies)
+int vec_in(cwf_hip_system *h, const float *src, float *dst, int kind, int w)
+{
+    const float *p = nullptr;
+    if (int st = stage_vec(h, src, dst, kind, w, &p))
+        return st;
+    if (p != dst)
+        HIPTRY(h, hipMemcpyAsync(dst, p, (uint64_t)w * h->ds.N * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+    return 0;
+}
+
+// internal-order device vector -> caller order (host or device)
+int vec_out(cwf_hip_system *h, const float *src, float *dst, int kind, int w)
+{
+    const uint64_t n = (uint64_t)w * h->ds.N;
+    if (!h->perm)
+    {
+        if (src != dst)
+            HIPTRY(h, hipMemcpyAsync(dst, src, n * sizeof(float),
+                                     kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                                     h->stream));
+        return 0;
+    }
+    if (kind == CWF_PTR_DEVICE)
+    {
+        perm_scatter(h->perm, src, dst, h->ds.N, w, h->stream);
+        return 0;
+    }
+    perm_scatter(h->perm, src, h->pbuf, h->ds.N, w, h->stream);
+    HIPTRY(h, hipMemcpyAsync(dst, h->pbuf, n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    return 0;
+}
+
+// Morton order of the node coordinates: perm[i] = caller node of internal node i
+std::vector<uint32_t> morton_node_order(const double *X, uint64_t N)
+{
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (uint64_t n = 0; n < N; ++n)
+        for (int k = 0; k < 3; ++k)
+        {
+            lo[k] = std::min(lo[k], X[3 * n + k]);
+            hi[k] = std::max(hi[k], X[3 * n + k]);
+        }
+    double ext = 0.0;
+    for (int k = 0; k < 3; ++k)
+        ext = std::max(ext, hi[k] - lo[k]);
+    const double scale = ext > 0 ? (double)((1u << 21) - 1) / ext : 0.0;
+    auto spread = [](uint64_t v) {
+        v &= 0x1fffff;
+        v = (v | v << 32) & 0x1f00000000ffffull;
+        v = (v | v << 16) & 0x1f0000ff0000ffull;
+        v = (v | v << 8) & 0x100f00f00f00f00full;
+        v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+        v = (v | v << 2) & 0x1249249249249249ull;
+        return v;
+    };
+    std::vector<uint64_t> key(N);
+    for (uint64_t n = 0; n < N; ++n)
+    {
+        uint64_t q[3];
+        for (int k = 0; k < 3; ++k)
+            q[k] = (uint64_t)std::llround((X[3 * n + k] - lo[k]) * scale);
+        key[n] = spread(q[0]) | spread(q[1]) << 1 | spread(q[2]) << 2;
+    }
+    std::vector<uint32_t> perm(N);
+    std::iota(perm.begin(), perm.end(), 0u);
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    return perm;
 }
 
 std::string pcg_error_message(int code, int iter, std::string *ctx)
@@ -353,6 +442,53 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 return set_error(nullptr, CWF_ERR_NODE_RANGE, "element connectivity references node out of range",
                                  "element=" + std::to_string(e) +
                                      " node=" + std::to_string(d->element_connectivity[e * 8 + a]));
+    }
+    // FAST handles renumber their nodes along a Morton curve (cwf_hip.h CWF_DESC_KEEP_NODE_ORDER): the
+    // rest of create then sees a desc in internal order; perm converts at the boundary
+    cwf_system_desc rd{};
+    std::vector<uint32_t> r_perm, r_conn, r_mask;
+    std::vector<float> r_mass;
+    std::vector<double> r_coords;
+    const char *rn = getenv("CWF_RENUMBER");
+    const bool renumber = d->mode == CWF_MODE_FAST && E && N && d->node_coords &&
+                          !(d->reserved & CWF_DESC_KEEP_NODE_ORDER) && !(rn && rn[0] == '0');
+    if (renumber)
+    {
+        try
+        {
+            r_perm = morton_node_order(d->node_coords, N);
+            std::vector<uint32_t> inv(N);
+            for (uint64_t i = 0; i < N; ++i)
+                inv[r_perm[i]] = (uint32_t)i;
+            r_conn.assign(d->element_connectivity, d->element_connectivity + 8 * E);
+            for (auto &c : r_conn)
+                if (c != 0xFFFFFFFFu)
+                    c = inv[c];
+            r_mass.resize(N);
+            r_mask.resize(N);
+            r_coords.resize(3 * N);
+            for (uint64_t i = 0; i < N; ++i)
+            {
+                const uint64_t n = r_perm[i];
+                r_mass[i] = d->lumped_mass[n];
+                r_mask[i] = d->bc_mask[n];
+                for (int k = 0; k < 3; ++k)
+                    r_coords[3 * i + k] = d->node_coords[3 * n + k];
+            }
+        }
+        catch (const std::bad_alloc &)
+        {
+            return set_error(nullptr, CWF_ERR_ALLOC, "host allocation failed");
+        }
+        rd = *d;
+        rd.element_connectivity = r_conn.data();
+        rd.lumped_mass = r_mass.data();
+        rd.bc_mask = r_mask.data();
+        rd.node_coords = r_coords.data();
+        rd.adjacency_offsets = nullptr;  // rebuilt in internal order (ascending element per node)
+        rd.adjacency_elements = nullptr;
+        rd.adjacency_local = nullptr;
+        d = &rd;
     }
     hipError_t he = hipSetDevice(device);
     if (he != hipSuccess)
@@ -691,6 +827,13 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     h->g_rrz = h->g_pap + 1;
     h->g_init = h->g_rrz + 2;
     h->g_rz0 = h->g_init + 2;
+    if (renumber)
+    {
+        if (int st = upload(h, &h->perm, r_perm.data(), N))
+            return bail(st);
+        if (int st = dalloc(h, &h->pbuf, 13 * N))
+            return bail(st);
+    }
     HIPTRY(h, hipMemset(h->x, 0, D * sizeof(float)));
     HIPTRY(h, hipMemset(h->ctl, 0, sizeof(Ctl)));
     HIPTRY(h, hipMemset(h->g_pap, 0, 6 * sizeof(double)));
@@ -715,6 +858,9 @@ int cwf_hip_system_set_mode(cwf_hip_system *h, int mode)
     if (h->ds.hex && mode != CWF_MODE_FAST)
         return set_error(h, CWF_ERR_UNSUPPORTED, "hex8 elements run in CWF_MODE_FAST only",
                          "the reference has no hex8 arithmetic to reproduce (preprocess.cpp:326-330)");
+    if (h->perm && mode != CWF_MODE_FAST)
+        return set_error(h, CWF_ERR_UNSUPPORTED, "a renumbered FAST handle cannot switch to CWF_MODE_PARITY",
+                         "create the PARITY handle separately (or with CWF_DESC_KEEP_NODE_ORDER)");
     h->mode = mode == CWF_MODE_FAST ? CWF_MODE_FAST : CWF_MODE_PARITY;
     return 0;
 }
@@ -825,11 +971,11 @@ int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_
         return set_error(h, CWF_ERR_SIZE, "displacement span size mismatch",
                          "input=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
     const float *uin = nullptr;
-    if (int st = stage_in(h, u, h->tmp, n, u_kind, &uin))
+    if (int st = stage_vec(h, u, h->tmp, u_kind, 3, &uin))
         return st;
     const uint64_t ne = 13ull * h->ds.E, nn = 13ull * h->ds.N;
     float *de = elements, *dn = nodes;
-    if (out_kind != CWF_PTR_DEVICE)  // host outputs: stage through one scratch allocation
+    if (out_kind != CWF_PTR_DEVICE || h->perm)  // stage through one scratch allocation
     {
         float *scratch = nullptr;
         HIPTRY(h, hipMalloc(reinterpret_cast<void **>(&scratch), (ne + nn + 1) * sizeof(float)));
@@ -837,10 +983,16 @@ int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_
         dn = nodes ? scratch + ne : nullptr;
         derived_fields(h, uin, de, dn, h->stream);
         hipError_t e1 = hipGetLastError();
+        const hipMemcpyKind back = out_kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
         if (e1 == hipSuccess && elements)
-            e1 = hipMemcpyAsync(elements, de, ne * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+            e1 = hipMemcpyAsync(elements, de, ne * sizeof(float), back, h->stream);
         if (e1 == hipSuccess && nodes)
-            e1 = hipMemcpyAsync(nodes, dn, nn * sizeof(float), hipMemcpyDeviceToHost, h->stream);
+        {
+            if (h->perm)  // node fields back to the caller's node order
+                e1 = vec_out(h, dn, nodes, out_kind, 13) ? hipErrorUnknown : hipSuccess;
+            else
+                e1 = hipMemcpyAsync(nodes, dn, nn * sizeof(float), back, h->stream);
+        }
         if (e1 == hipSuccess)
             e1 = hipStreamSynchronize(h->stream);
         (void)hipFree(scratch);
@@ -862,16 +1014,16 @@ int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, 
         return set_error(h, CWF_ERR_SIZE, "input/output span size mismatch",
                          "input=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
     const float *xin = nullptr;
-    if (int st = stage_in(h, x, h->tmp, n, kind, &xin))
+    if (int st = stage_vec(h, x, h->tmp, kind, 3, &xin))
         return st;
-    float *yout = kind == CWF_PTR_DEVICE ? y : h->Ap;
+    float *yout = kind == CWF_PTR_DEVICE && !h->perm ? y : h->Ap;
     if (h->mode == CWF_MODE_FAST)
         fast_keff(h, xin, yout, true, nullptr, nullptr, h->stream);
     else
         parity_keff(h, xin, yout, true, nullptr, h->stream);
     HIPTRY(h, hipGetLastError());
-    if (kind != CWF_PTR_DEVICE)
-        HIPTRY(h, hipMemcpyAsync(y, yout, n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    if (int st = vec_out(h, yout, y, kind, 3))
+        return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -884,14 +1036,14 @@ int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64
     if (n < req)
         return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
                          "required=" + std::to_string(req) + " available=" + std::to_string(n));
-    float *dst = kind == CWF_PTR_DEVICE ? inv_out : h->inv;
+    float *dst = kind == CWF_PTR_DEVICE && !h->perm ? inv_out : h->inv;
     if (h->ds.hex)
         hex_block_jacobi(h, dst, h->stream);
     else
         parity_block_jacobi(h, dst, h->stream);
     HIPTRY(h, hipGetLastError());
-    if (kind != CWF_PTR_DEVICE)
-        HIPTRY(h, hipMemcpyAsync(inv_out, dst, req * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    if (int st = vec_out(h, dst, inv_out, kind, 9))
+        return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -965,17 +1117,17 @@ int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_setting
     if (settings->max_iterations == 0)
         return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
     const float *drhs = nullptr;
-    if (int st = stage_in(h, rhs, h->rhs, n, kind, &drhs))
+    if (int st = stage_vec(h, rhs, h->rhs, kind, 3, &drhs))
         return st;
     if (settings->warm_start)
-        HIPTRY(h, hipMemcpyAsync(h->x, x_inout, n * sizeof(float),
-                                 kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                 h->stream));
+        if (int st = vec_in(h, x_inout, h->x, kind, 3))
+            return st;
     int st = run_pcg(h, drhs, *settings, telemetry);
-    const hipMemcpyKind back = kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    HIPTRY(h, hipMemcpyAsync(x_inout, h->x, n * sizeof(float), back, h->stream));
+    if (int e = vec_out(h, h->x, x_inout, kind, 3))
+        return e;
     if (residual_out)
-        HIPTRY(h, hipMemcpyAsync(residual_out, h->r, n * sizeof(float), back, h->stream));
+        if (int e = vec_out(h, h->r, residual_out, kind, 3))
+            return e;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return st;
 }
@@ -1107,9 +1259,9 @@ int cwf_hip_stepper_create(cwf_hip_system *h, const cwf_stepper_desc *desc, cwf_
     for (float *p : {t->u, t->v, t->a, t->up, t->vp, t->f, t->bcv})
         (void)hipMemsetAsync(p, 0, D * sizeof(float), s);
     if (desc->external_force)
-        (void)hipMemcpyAsync(t->f, desc->external_force, D * sizeof(float), hipMemcpyHostToDevice, s);
+        (void)vec_in(h, desc->external_force, t->f, CWF_PTR_HOST, 3);
     if (desc->bc_value)
-        (void)hipMemcpyAsync(t->bcv, desc->bc_value, D * sizeof(float), hipMemcpyHostToDevice, s);
+        (void)vec_in(h, desc->bc_value, t->bcv, CWF_PTR_HOST, 3);
     (void)hipMemsetAsync(h->x, 0, D * sizeof(float), s);  // solver.x starts at 0 (pack.cpp:214)
     hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess)
@@ -1226,8 +1378,8 @@ int cwf_hip_stepper_get_state(cwf_hip_stepper *t, int which, float *out, uint64_
     const float *src = which == 0 ? t->u : which == 1 ? t->v : which == 2 ? t->a : which == 3 ? h->x : nullptr;
     if (!src)
         return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
-    HIPTRY(h, hipMemcpyAsync(out, src, n * sizeof(float),
-                             kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->stream));
+    if (int st = vec_out(h, src, out, kind, 3))
+        return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -1244,8 +1396,8 @@ int cwf_hip_stepper_set_state(cwf_hip_stepper *t, int which, const float *in, ui
     float *dst = which == 0 ? t->u : which == 1 ? t->v : which == 2 ? t->a : which == 3 ? h->x : nullptr;
     if (!dst)
         return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
-    HIPTRY(h, hipMemcpyAsync(dst, in, n * sizeof(float),
-                             kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    if (int st = vec_in(h, in, dst, kind, 3))
+        return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -1259,8 +1411,8 @@ int cwf_hip_stepper_set_external_force(cwf_hip_stepper *t, const float *f, uint6
         return st;
     if (n != h->ds.D)
         return set_error(h, CWF_ERR_SIZE, "external force span size mismatch");
-    HIPTRY(h, hipMemcpyAsync(t->f, f, n * sizeof(float),
-                             kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    if (int st = vec_in(h, f, t->f, kind, 3))
+        return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return 0;
 }

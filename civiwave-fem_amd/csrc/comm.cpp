@@ -350,6 +350,9 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
     if (h->comm)
         return set_error(h, CWF_ERR_ARGUMENT, "handle already attached");
+    if (h->perm)
+        return set_error(h, CWF_ERR_ARGUMENT, "shard handles keep their node order",
+                         "create the handle with CWF_DESC_KEEP_NODE_ORDER (cwf_system_desc.reserved)");
     if (rank < 0 || rank >= cm->nranks || (cm->kind == 0 && cm->members[rank]))
         return set_error(h, CWF_ERR_ARGUMENT, "rank out of range or taken", "rank=" + std::to_string(rank));
     if (cm->device != h->device)

@@ -148,6 +148,10 @@ struct cwf_hip_system
     float *inv6 = nullptr;  // FAST: symmetric block inverse packed [6N]
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
     uint64_t part_cap = 0;
+    // FAST-mode internal node renumbering (Morton order of the coordinates): perm[i] = caller's node of
+    // internal node i; every vector crossing the ABI is gathered / scattered through it (pbuf: 13N staging)
+    uint32_t *perm = nullptr;
+    float *pbuf = nullptr;
     cwf::Ctl *ctl = nullptr;       // device
     cwf::Ctl *ctl_host = nullptr;  // pinned
     double *scal = nullptr;        // device scalar scratch
@@ -210,6 +214,9 @@ void launch_precond(const cwf_hip_system *h, const Ctl *ctl, hipStream_t st);
 void launch_p_init(const cwf_hip_system *h, hipStream_t st);
 
 // ---- kernels_fast.hip ----
+// dst[w i + k] = src[w perm[i] + k] (gather = caller order -> internal) / dst[w perm[i] + k] = src[w i + k]
+void perm_gather(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st);
+void perm_scatter(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st);
 uint32_t fast_block_count(const cwf_hip_system *h);
 uint32_t fast_dot_blocks(uint32_t D);
 void fast_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, double *part,

@@ -136,6 +136,34 @@ void fast_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize,
 }
 
 // dot over D dofs: one partial per 256-dof block (grid = ceil(D/256) capped) then fold
+__global__ __launch_bounds__(kBlock) void k_perm_copy(const uint32_t *__restrict__ perm, const float *__restrict__ src,
+                                                      float *__restrict__ dst, uint32_t N, int w, int scatter)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (uint64_t)N * w)
+        return;
+    const uint32_t i = (uint32_t)(t / w), k = (uint32_t)(t % w);
+    const uint64_t ext = (uint64_t)perm[i] * w + k;
+    if (scatter)
+        dst[ext] = src[t];
+    else
+        dst[t] = src[ext];
+}
+
+void perm_gather(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)N * w;
+    if (n)
+        k_perm_copy<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(perm, src, dst, N, w, 0);
+}
+
+void perm_scatter(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)N * w;
+    if (n)
+        k_perm_copy<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(perm, src, dst, N, w, 1);
+}
+
 uint32_t fast_dot_blocks(uint32_t D) { return grid_for(D, kBlock) < 4096u ? grid_for(D, kBlock) : 4096u; }
 
 void fast_dot(const float *a, const float *b, const float *c, uint32_t D, double *pab, double *pac, hipStream_t st)

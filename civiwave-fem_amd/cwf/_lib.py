@@ -17,6 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "cwf_hip.h")
 
 PTR_HOST, PTR_DEVICE = 0, 1
 MODE_PARITY, MODE_FAST = 0, 1
+DESC_KEEP_NODE_ORDER = 1  # cwf_system_desc.reserved flag (cwf_hip.h)
 
 STATUS = {
     0: "CWF_OK", -1: "CWF_ERR_SIZE", -2: "CWF_ERR_NODE_RANGE", -3: "CWF_ERR_MATERIAL_RANGE",

@@ -118,6 +118,31 @@ def jitter_and_permute(mesh: TetMesh, h: float, jitter: float = 0.15, seed_jitte
     return TetMesh(c[node_perm], tets, groups, None)
 
 
+def morton_renumber(mesh: TetMesh) -> TetMesh:
+    """Nodes renumbered along a Morton curve of their coordinates (elements keep their order); groups
+    remapped. A diagnostic for how much node-order locality is worth to the FAST kernels."""
+    c = mesh.coords
+    lo, hi = c.min(0), c.max(0)
+    q = np.floor((c - lo) / max(float((hi - lo).max()), 1e-300) * ((1 << 20) - 1)).astype(np.uint64)
+
+    def spread(v):
+        v = v & np.uint64(0x1FFFFF)
+        v = (v | v << np.uint64(32)) & np.uint64(0x1F00000000FFFF)
+        v = (v | v << np.uint64(16)) & np.uint64(0x1F0000FF0000FF)
+        v = (v | v << np.uint64(8)) & np.uint64(0x100F00F00F00F00F)
+        v = (v | v << np.uint64(4)) & np.uint64(0x10C30C30C30C30C3)
+        v = (v | v << np.uint64(2)) & np.uint64(0x1249249249249249)
+        return v
+
+    key = spread(q[:, 0]) | spread(q[:, 1]) << np.uint64(1) | spread(q[:, 2]) << np.uint64(2)
+    order = np.argsort(key, kind="stable")  # new -> old
+    old_to_new = np.empty_like(order)
+    old_to_new[order] = np.arange(order.size)
+    tets = old_to_new[mesh.tets.astype(np.int64)].astype(np.uint32)
+    groups = {k: np.sort(old_to_new[v.astype(np.int64)]).astype(np.uint32) for k, v in mesh.node_groups.items()}
+    return TetMesh(c[order], tets, groups, None)
+
+
 def single_tet() -> TetMesh:
     """The reference test fixture (tests/pcg_test.cpp:35-74): unit tet, base face fixed."""
     coords = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], np.float64)

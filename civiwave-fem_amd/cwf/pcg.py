@@ -92,8 +92,10 @@ class MatrixFreeSystem:
     def __init__(self, element_connectivity, element_gradients, element_volume, element_material_index, materials,
                  lumped_mass, bc_mask, node_count, element_count, dof_count, stiffness_scale=1.0, mass_factor=0.0,
                  reduction_block=256, reduction_partials=None, adjacency=None, mode: int = _lib.MODE_PARITY,
-                 device: int = 0, node_coords=None):
-        # node_coords (optional, [N,3]) only orders the FAST-mode element tiles (Morton order)
+                 device: int = 0, node_coords=None, keep_node_order: bool = False):
+        # node_coords (optional, [N,3]) orders the FAST-mode element tiles and (FAST, unless keep_node_order)
+        # the handle's internal node numbering (cwf_hip.h CWF_DESC_KEEP_NODE_ORDER); shards keep their order
+        self.flags = _lib.DESC_KEEP_NODE_ORDER if keep_node_order else 0
         self.node_coords = (None if node_coords is None else
                             np.ascontiguousarray(np.asarray(node_coords, np.float64).reshape(-1)))
         self.element_connectivity = np.ascontiguousarray(element_connectivity, np.uint32)
@@ -140,7 +142,8 @@ class MatrixFreeSystem:
             p(adj[0]) if adj is not None else None,
             p(adj[1]) if adj is not None else None,
             p(adj[2]) if adj is not None else None,
-            self.stiffness_scale, self.mass_factor, self.reduction_block, self.reduction_partials, self.mode, 0,
+            self.stiffness_scale, self.mass_factor, self.reduction_block, self.reduction_partials, self.mode,
+            self.flags,
             p(self.node_coords) if self.node_coords is not None else None)
 
     # -- handle management --------------------------------------------------------------

@@ -3,6 +3,7 @@ blocks, x=0 face fixed, gravity + a -500 N point load per node of the x=max face
 material (E=30 GPa, nu=0.2, rho=2500), Newmark dt=0.01."""
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -54,6 +55,8 @@ def block_case(nx, ny, nz, h=0.1, jitter=False, element="tet4", **cfg_kw) -> Cas
     tm = meshgen.hex_block(nx, ny, nz, h) if element == "hex8" else meshgen.kuhn_block(nx, ny, nz, h)
     if jitter:
         tm = meshgen.jitter_and_permute(tm, h)
+    if os.environ.get("CWF_MORTON_NODES") == "1":  # diagnostic: node-order locality experiment
+        tm = meshgen.morton_renumber(tm)
     mesh = pack.from_tetmesh(tm)
     cfg = make_config(**cfg_kw)
     tag = "hex" if element == "hex8" else "kuhn"

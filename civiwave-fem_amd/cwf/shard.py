@@ -68,7 +68,7 @@ class Shard:
         return MatrixFreeSystem(self.connectivity, self.gradients, self.volume, self.material_index, materials,
                                 self.lumped_mass, self.bc_mask, self.local_nodes, self.local_elements,
                                 3 * self.local_nodes, stiffness_scale, mass_factor, 256, None, None,
-                                _lib.MODE_FAST, device, self.node_coords)
+                                _lib.MODE_FAST, device, self.node_coords, keep_node_order=True)
 
     def close(self):
         if self._c is not None:

@@ -67,6 +67,12 @@ typedef enum cwf_mode
 /* Mirrors cwf::gpu::pcg::MatrixFreeSystem (include/cwf/gpu/pcg.hpp:67-86) plus the packed
  * adjacency of cwf::mesh::pack::AdjacencyBuffers (include/cwf/mesh/pack.hpp:120-125).
  * All pointers are host memory; the handle copies them to HBM at create time. */
+/* cwf_system_desc.reserved flags. A CWF_MODE_FAST handle renumbers its nodes internally along a Morton
+ * curve of node_coords (locality of the tile gathers and partial stores; 1.8x on a permuted mesh), and
+ * converts every vector at the boundary, so callers always see their own node order. KEEP_NODE_ORDER
+ * disables that: required for handles that are attached as shards (local numbering = the halo plan). */
+#define CWF_DESC_KEEP_NODE_ORDER 1
+
 typedef struct cwf_system_desc
 {
     uint64_t node_count;
@@ -88,7 +94,7 @@ typedef struct cwf_system_desc
     uint64_t reduction_block;           /* 256 in the reference (pack.hpp:183) */
     uint64_t reduction_partials;        /* >= ceil(dof_count / reduction_block) */
     int32_t mode;                       /* cwf_mode */
-    int32_t reserved;
+    int32_t reserved;                   /* flags: CWF_DESC_KEEP_NODE_ORDER */
     const double *node_coords;          /* [node_count * 3] or NULL: only used to order FAST-mode tiles */
 } cwf_system_desc;
 
