@@ -721,6 +721,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         {
             const uint32_t e0 = ht.tile_elem_off[k], nb = ht.tile_node_off[k], nb1 = ht.tile_node_off[k + 1];
             hdr[k] = uint4{e0, ht.tile_elem_off[k + 1] - e0, nb, nb1 - nb};
+            if (hex && !ht.tile_affine.empty() && ht.tile_affine[k])
+                hdr[k].x |= 0x80000000u;  // hex8 tile of parallelepipeds (k_keff_hex_tiles: constant J)
             for (uint32_t q = nb; q < nb1; ++q)
                 tnode[q] = uint2{ht.tile_nodes[q], (ht.csr_off[q] - (uint32_t)K * e0) |
                                                        ((ht.csr_off[q + 1] - (uint32_t)K * e0) << 16)};

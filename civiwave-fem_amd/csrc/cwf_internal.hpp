@@ -74,6 +74,7 @@ struct HostTiles
     std::vector<uint2> eid;        // [E] local corner ids
     std::vector<uint2> epos;       // [E] tile-relative local-CSR positions of the 4 (element, corner) pairs
     std::vector<uint4> eid8, epos8;  // hex8: [E] the 8 corners' local ids / local-CSR positions (u16 pairs)
+    std::vector<uint8_t> tile_affine;  // hex8: 1 when every hex of the tile is a parallelepiped (constant J)
     std::vector<float> tcoord[3];  // [total] tile-relative coordinates (when node_coords are given)
 };
 

@@ -188,6 +188,31 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
                 for (int k = 0; k < 3; ++k)
                     out.tcoord[k].push_back((float)(d->node_coords[3ull * nodes[i] + k] - o[k]));
         }
+        if (K == 8)
+        {
+            // parallelepiped test: the trilinear map's bilinear/trilinear ("hourglass") coefficients
+            // x_0 - x_1 + x_2 - x_3 (bottom face), ..., all ~0 -> J is constant over the hex. Tolerance
+            // 1e-7 of the element's extent: below fp32 rounding of the kernel's own J.
+            bool aff = d->node_coords != nullptr;
+            for (uint64_t j = e0; aff && j < e; ++j)
+            {
+                const uint32_t *c = d->element_connectivity + 8ull * order[j];
+                for (int m = 0; m < 3 && aff; ++m)
+                {
+                    double v[8];  // lexicographic corner L = i + 2 j + 4 k (Gmsh order 0 1 3 2 4 5 7 6)
+                    const int lex[8] = {0, 1, 3, 2, 4, 5, 7, 6};
+                    for (int a = 0; a < 8; ++a)
+                        v[lex[a]] = d->node_coords[3ull * c[a] + m];
+                    const double hxy0 = v[0] - v[1] - v[2] + v[3], hxy1 = v[4] - v[5] - v[6] + v[7];
+                    const double hxz = v[0] - v[1] - v[4] + v[5], hyz = v[0] - v[2] - v[4] + v[6];
+                    const double ext = std::fabs(v[1] - v[0]) + std::fabs(v[2] - v[0]) + std::fabs(v[4] - v[0]);
+                    const double tol = 1e-7 * ext;
+                    aff = std::fabs(hxy0) <= tol && std::fabs(hxy1) <= tol && std::fabs(hxz) <= tol &&
+                          std::fabs(hyz) <= tol;
+                }
+            }
+            out.tile_affine.push_back(aff ? 1 : 0);
+        }
         out.max_tile_nodes = std::max(out.max_tile_nodes, nn);
         out.tile_elem_off.push_back((uint32_t)e);
         out.tile_node_off.push_back((uint32_t)out.tile_nodes.size());
