@@ -772,6 +772,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (int st = dalloc(h, &part, 3 * (ht.tile_nodes.size() + 2)))  // + 2 padding slots (update pass)
             return bail(st);
         t.ntiles = ht.ntiles;
+        t.hex_all_affine = hex && !ht.tile_affine.empty() &&
+                           std::all_of(ht.tile_affine.begin(), ht.tile_affine.end(), [](uint8_t a) { return a != 0; });
         t.max_tile_nodes = ht.max_tile_nodes;
         t.total_tile_nodes = (uint32_t)ht.tile_nodes.size();
         t.E = (uint32_t)E;

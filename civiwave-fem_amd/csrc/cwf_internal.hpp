@@ -52,6 +52,7 @@ struct DevTiles
     const uint2 *epos = nullptr;              // [E] (PUSH) each corner's position in the tile's local CSR
     // native hex8: k_keff_hex_tiles, 128-thread persistent grid (pipe_grid), push fold
     int hex = 0;
+    int hex_all_affine = 0;        // every hex tile is a parallelepiped tile (affine-only kernel variant)
     const uint4 *eid8 = nullptr;   // [E] 8 u16 local corner ids (Gmsh corner order)
     const uint4 *epos8 = nullptr;  // [E] 8 u16 local-CSR positions
     const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile)
