@@ -69,22 +69,12 @@ def cpu_baseline(case, sK, sM, iters):
                        f"{dt:.2f} s, 1 thread, {os.cpu_count()} host CPUs visible")
 
 
-def stream_copy_gbs(torch, nbytes=2 << 30, reps=10):
-    """STREAM-like device copy ceiling measured on this GPU: read + write bytes / time."""
-    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
+def stream_copy_gbs(L, device, nbytes=2 << 30, reps=20):
+    """STREAM-like 16-B-lane device copy measured on this GPU: read + write bytes / time."""
+    import ctypes as C
+
+    g = C.c_double()
+    return g.value if L.cwf_hip_bandwidth_probe(device, nbytes, reps, C.byref(g)) == 0 else None
 
 
 def main():
@@ -199,7 +189,7 @@ def main():
         traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
         traffic_src = os.path.relpath(tpath, ROOT)
     result = None
-    copy_gbs = stream_copy_gbs(torch) if rank == 0 else None
+    copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1 and args.element == "tet4":  # rank 0 at N=1 only

@@ -934,6 +934,42 @@ int cwf_hip_keff_timed(cwf_hip_system *h, const float *x, float *y, int reps, do
     return 0;
 }
 
+int cwf_hip_bandwidth_probe(int device, uint64_t bytes, int reps, double *gbs)
+{
+    if (!gbs || bytes < 16 || reps < 1)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "bandwidth probe: bad arguments");
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess)
+        return hip_fail(nullptr, e, "hipSetDevice");
+    bytes &= ~(uint64_t)15;
+    void *a = nullptr, *b = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    float ms = 0.f;
+    if ((e = hipMalloc(&a, bytes)) == hipSuccess && (e = hipMalloc(&b, bytes)) == hipSuccess &&
+        (e = hipMemset(a, 0, bytes)) == hipSuccess && (e = hipEventCreate(&e0)) == hipSuccess &&
+        (e = hipEventCreate(&e1)) == hipSuccess)
+    {
+        copy16(a, b, bytes, nullptr);  // warm
+        (void)hipEventRecord(e0, nullptr);
+        for (int r = 0; r < reps; ++r)
+            copy16(a, b, bytes, nullptr);
+        (void)hipEventRecord(e1, nullptr);
+        e = hipEventSynchronize(e1);
+        if (e == hipSuccess)
+            e = hipEventElapsedTime(&ms, e0, e1);
+    }
+    if (e0)
+        (void)hipEventDestroy(e0);
+    if (e1)
+        (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    if (e != hipSuccess)
+        return hip_fail(nullptr, e, "bandwidth probe");
+    *gbs = 2.0 * (double)bytes * reps / ((double)ms * 1e-3) / 1e9;  // read + write
+    return 0;
+}
+
 int cwf_hip_system_memory(const cwf_hip_system *h, uint64_t *bytes)
 {
     if (!h || !bytes)

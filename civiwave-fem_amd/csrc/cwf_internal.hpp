@@ -217,6 +217,7 @@ void launch_p_init(const cwf_hip_system *h, hipStream_t st);
 
 // ---- kernels_fast.hip ----
 // dst[w i + k] = src[w perm[i] + k] (gather = caller order -> internal) / dst[w perm[i] + k] = src[w i + k]
+void copy16(const void *a, void *b, uint64_t bytes, hipStream_t st);  // bandwidth probe copy
 void perm_gather(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st);
 void perm_scatter(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st);
 uint32_t fast_block_count(const cwf_hip_system *h);

@@ -129,6 +129,7 @@ def load() -> C.CDLL:
         "cwf_hip_system_set_scalars": ([P, f64, f64], i32),
         "cwf_hip_system_set_mode": ([P, i32], i32),
         "cwf_hip_system_memory": ([P, P], i32),
+        "cwf_hip_bandwidth_probe": ([i32, u64, i32, P], i32),
         "cwf_hip_system_keff_traffic": ([P, P, P], i32),
         "cwf_hip_system_set_timing": ([P, i32], i32),
         "cwf_hip_system_timing": ([P, P, P], i32),

@@ -136,6 +136,9 @@ int cwf_hip_system_set_scalars(cwf_hip_system *h, double stiffness_scale, double
 int cwf_hip_system_set_mode(cwf_hip_system *h, int mode);
 /* bytes of HBM held by the handle */
 int cwf_hip_system_memory(const cwf_hip_system *h, uint64_t *bytes);
+/* STREAM-like device copy (16-B lanes, grid-stride) on `device`: *gbs = (read + write bytes) / time. The
+ * measured HBM ceiling bench.py reports beside the 8 TB/s spec. No reference counterpart. */
+int cwf_hip_bandwidth_probe(int device, uint64_t bytes, int reps, double *gbs);
 /* Algorithmic (compulsory) HBM bytes of one PCG-loop K_eff launch (measurement support, not a
  * reference interface): `layout_bytes` = every array the handle's own K_eff kernel touches, counted
  * once (the headline roofline uses the build's own layout when it reads less);
