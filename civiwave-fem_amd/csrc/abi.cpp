@@ -638,10 +638,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         }
         else
         {
-            const char *fo = getenv("CWF_TILE_FOLD");
-            t.acc = fo && fo[0] == 'a' ? 1 : 0;
-            const char *pp = getenv("CWF_TILE_PIPE");
-            t.pipe = t.geo && !t.acc && !(pp && pp[0] == '0') ? 1 : 0;
+            const char *pp = getenv("CWF_TILE_PIPE");  // diagnostic: 0 = the one-tile-per-workgroup kernel
+            t.pipe = t.geo && !(pp && pp[0] == '0') ? 1 : 0;
         }
         try
         {
@@ -651,8 +649,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             {
                 const char *pn = getenv("CWF_PIPE_NT");
                 t.pipe_nt = pn ? (atoi(pn) == 128 ? 128 : 256) : (E < 4000000ull ? 128 : 256);
-                const char *pf = getenv("CWF_PIPE_FOLD");
-                t.push = pf && pf[0] == 'c' ? 0 : 1;  // CWF_PIPE_FOLD=csr: the local-CSR entry fold
+                t.push = 1;  // the pipelined kernel folds pushed forces (epos), not local-CSR entries
             }
             if (hex)
                 build_tiles(d, ht, 2u * kHexTileThreads, kHexTileThreads, 8);
@@ -663,13 +660,6 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         catch (const std::bad_alloc &)
         {
             return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
-        }
-        {
-            uint32_t deg = 1;
-            for (size_t q = 0; q + 1 < ht.csr_off.size(); ++q)
-                deg = std::max(deg, ht.csr_off[q + 1] - ht.csr_off[q]);
-            while ((1u << t.deg_log2) < deg)
-                ++t.deg_log2;
         }
         if (getenv("CWF_VERBOSE"))
             fprintf(stderr, "[cwf] tiles: %u tiles, %zu tile nodes (%.3f per node), max %u nodes/tile, %s records\n",

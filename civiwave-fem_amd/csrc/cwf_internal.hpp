@@ -33,12 +33,10 @@ struct DevTiles
     uint32_t total_tile_nodes = 0;
     uint32_t E = 0;
     int geo = 0;  // 1: geometry recomputed from tile-node coordinates (eid + tcoord), 0: 48-B planes
-    int acc = 0;  // 1: fixed-point LDS accumulation (no local CSR fold)
-    int pipe = 0; // 1: persistent software-pipelined tiles kernel (GEO, CSR fold)
+    int pipe = 0; // 1: persistent software-pipelined tiles kernel (GEO records, push fold)
     uint32_t pipe_grid = 0;  // its resident grid (occupancy x CUs, whole XCD groups)
     int pipe_nt = 256;       // its workgroup size; tiles hold <= 2 pipe_nt elements and <= pipe_nt nodes
     int push = 0;            // 1: elements store forces at their local-CSR positions; nodes fold contiguous runs
-    uint32_t deg_log2 = 0;  // ceil(log2(largest number of (element, corner) pairs of one tile node))
     // [3][E] 48-B records: {idx01, idx23, g0x, g0y} {g0z, g1x, g1y, g1z} {g2x, g2y, g2z, vol};
     // g3 = -(g0 + g1 + g2) (partition of unity of the linear tet)
     const uint4 *planes = nullptr;

@@ -1,19 +1,22 @@
 // spmv_tiles.hip -- FAST-mode K_eff and the fused FAST PCG iteration (2 kernels / iteration).
 //
-// k_keff_tiles (one workgroup per tile of <= 512 Morton-ordered tets):
-//   a) tile-node phase: one 16-B record per tile node {node|owner, partial slot, csr begin, csr end}
-//      and the node's value gathered into LDS: x (apply_keff) or, inside PCG, the new search direction
-//      p = z + beta p_old formed on the fly (the p-update pass of pcg.cpp:897-914 is fused here);
-//   b) element phase: 48-B records from 3 SoA planes (every dwordx4 wave-load is one contiguous 1 KiB
-//      run), corner values from LDS, fp32 strain -> stress -> 12 nodal forces scaled by V*s_K, stored
-//      to LDS as f[12][512] (bank-conflict free);
-//   c) fold phase: every tile node sums its (element, corner) forces in ascending element order through
-//      the tile's local CSR (deterministic, no atomics) and stores a 12-B partial at its node-major
-//      slot; PCG adds the tile's fp64 share of p.Ap.
+// k_keff_tiles_pipe (the default; persistent, XCD-aware, software-pipelined; tiles of <= 2 NT
+// Morton-ordered tets and <= NT nodes):
+//   a) tile-node phase: the node's coordinates and value go to LDS: x (apply_keff) or, inside PCG, the new
+//      search direction p = z + beta p_old formed on the fly (the p-update pass of pcg.cpp:897-914 is
+//      fused here); the next tile's records are already in flight;
+//   b) element phase: 8-B corner-id records, gradients and volume recomputed from the tile-relative
+//      coordinates (cofactor rows, one stress scale), fp32 strain -> stress -> 12 nodal forces, each
+//      corner's 3 forces pushed to its position in the tile's local CSR (epos);
+//   c) fold phase: every tile node sums its contiguous run (ascending element, deterministic, no atomics)
+//      and stores a 12-B partial at its node-major slot; PCG adds the tile's fp64 share of p.Ap.
+// k_keff_tiles: one workgroup per tile, 48-B gradient records and a local-CSR fold; the path for meshes
+//   without coordinates that reproduce their gradients.
+// k_keff_hex_tiles (hex8_tiles.inc): the native hex8 element on the same tile machinery.
 // k_keff_finalize (apply_keff): y = node's partials (ascending tile) + m s_M x, Dirichlet identity rows.
-// k_pcg_update_tiles (PCG, 1024-thread workgroups, grid-stride): Ap from the node-major partials (never
-//   stored), the same p expression, x += alpha p, r -= alpha Ap, Dirichlet, z = M^-1 r, store x r z p,
-//   fp64 r.r / r.z shares.
+// k_pcg_update_tiles (PCG, 256-thread workgroups, resident grid-stride): Ap from the node-major partials
+//   (never stored), the same p expression, x += alpha p, r -= alpha Ap, Dirichlet, z = M^-1 r, store
+//   x r z p, fp64 r.r / r.z shares.
 // Scalars without atomics or fences: every consumer workgroup folds the producer's partials itself in a
 // fixed order (alpha in the update kernel, |r| / convergence / beta in the tiles-kernel preamble,
 // pcg.cpp:840-895); the host passes the iteration index and rho is double-buffered by parity, so no
@@ -605,204 +608,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     }
 }
 
-// Fixed-point variant (CWF_TILE_FOLD=acc): the tile's element forces are accumulated per tile node with
-// 32-bit integer LDS atomics after scaling by a per-tile power of two (block max |f|, headroom for the
-// tile's largest node degree). Integer addition is associative, so the tile sums are exact and
-// independent of atomic order (deterministic) while no force array, local CSR or fold pass is needed:
-// 13 KB of LDS per tile instead of 34 KB, and no CSR stream. The resolution is 2^-24..2^-25 of the
-// tile's largest force, at or below fp32 accumulation's own rounding.
-template <bool ISO, bool SANITIZE, int MODE, int NT, bool GEO>
-__global__ __launch_bounds__(NT) void k_keff_tiles_acc(DevSys s, const float *__restrict__ x, PcgArgs pa)
-{
-    constexpr int kTab = ISO ? 12 : 36;
-    extern __shared__ float lds[];
-    const DevTiles &T = s.t;
-    const uint32_t ms = T.max_tile_nodes;
-    float *sp = lds;                                                        // [3][ms] node values
-    float *sx = sp + 3 * ms;                                                // [3][ms] coordinates (GEO)
-    int *acc = reinterpret_cast<int *>(sx + (GEO ? 3 * ms : 0));            // [3][ms] fixed-point sums
-    __shared__ float dtab[kMaxM * kTab];
-    __shared__ double red[NT / 64];
-    __shared__ float wmax[NT / 64];
-    if constexpr (MODE == 1)
-    {
-        if (!pa.ctl->active)
-            return;
-    }
-    const uint4 hd = T.hdr[blockIdx.x];
-    const uint32_t e0 = hd.x, ne = hd.y, nb = hd.z, nn = hd.w;
-    const float sK = (float)s.sK;
-    const uint32_t i0 = threadIdx.x;
-    uint2 tn0 = uint2{0u, 0u};
-    float v0[3] = {0.f, 0.f, 0.f}, w0[3] = {0.f, 0.f, 0.f};
-    if (i0 < nn)
-    {
-        tn0 = T.tnode[nb + i0];
-        const uint32_t g = tn0.x & 0x7fffffffu;
-        v0[0] = x[3u * g + 0];
-        v0[1] = x[3u * g + 1];
-        v0[2] = x[3u * g + 2];
-        if constexpr (MODE == 1)
-        {
-            w0[0] = pa.z[3u * g + 0];
-            w0[1] = pa.z[3u * g + 1];
-            w0[2] = pa.z[3u * g + 2];
-        }
-        else if constexpr (SANITIZE)
-        {
-            const uint32_t mk = s.mask[g];
-            v0[0] = (mk & 1u) ? 0.f : v0[0];
-            v0[1] = (mk & 2u) ? 0.f : v0[1];
-            v0[2] = (mk & 4u) ? 0.f : v0[2];
-        }
-    }
-    if constexpr (GEO)
-    {
-        const uint32_t T3 = T.total_tile_nodes;
-        for (uint32_t i = threadIdx.x; i < nn; i += NT)
-        {
-            sx[i] = T.tcoord[nb + i];
-            sx[ms + i] = T.tcoord[T3 + nb + i];
-            sx[2 * ms + i] = T.tcoord[2 * T3 + nb + i];
-        }
-    }
-    constexpr int kPer = kTileElems / NT;
-    uint4 pq[kPer][GEO ? 1 : 3];
-    uint2 pid[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-    {
-        const uint32_t j = threadIdx.x + k * NT;
-        const uint32_t e = e0 + (j < ne ? j : 0u);
-        if constexpr (GEO)
-            pid[k] = T.eid[e];
-        else
-        {
-            const uint4 *P = T.planes;
-            pq[k][0] = P[e];
-            pq[k][GEO ? 0 : 1] = P[T.E + e];
-            pq[k][GEO ? 0 : 2] = P[2u * T.E + e];
-        }
-    }
-    for (uint32_t i = threadIdx.x; i < 3 * nn; i += NT)
-        acc[(i / nn) * ms + (i % nn)] = 0;
-    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
-    for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
-        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
-    float beta = 0.f;
-    if constexpr (MODE == 1)
-    {
-        if (pa.abl & 1u)
-            beta = (float)pa.ctl->beta;
-        else if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta,
-                                    pa.abl & 32u))
-            return;
-    }
-    if (i0 < nn)
-    {
-        if constexpr (MODE == 1)
-        {
-            v0[0] = fmaf(beta, v0[0], w0[0]);
-            v0[1] = fmaf(beta, v0[1], w0[1]);
-            v0[2] = fmaf(beta, v0[2], w0[2]);
-        }
-        sp[i0] = v0[0];
-        sp[ms + i0] = v0[1];
-        sp[2 * ms + i0] = v0[2];
-    }
-    for (uint32_t i = i0 + NT; i < nn; i += NT)
-    {
-        const uint2 tn = T.tnode[nb + i];
-        float u[3];
-        gather_node<SANITIZE, MODE>(s, x, pa.z, beta, tn.x & 0x7fffffffu, u);
-        sp[i] = u[0];
-        sp[ms + i] = u[1];
-        sp[2 * ms + i] = u[2];
-    }
-    __syncthreads();
-    // (b) element forces in registers + the tile's largest magnitude
-    float f[kPer][12];
-    uint32_t li[kPer][4];
-    float fmx = 0.f;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-    {
-        const uint32_t j = threadIdx.x + k * NT;
-        float g[12], vol;
-        if constexpr (GEO)
-            coord_geometry(pid[k], sx, ms, g, li[k], &vol);
-        else
-            record_geometry(pq[k][0], pq[k][GEO ? 0 : 1], pq[k][GEO ? 0 : 2], g, li[k], &vol);
-        if (j < ne)
-        {
-            element_force_values<ISO>(s, g, li[k], vol * sK, T.mat ? T.mat[e0 + j] : 0u, sp, ms, dtab, f[k]);
-#pragma unroll
-            for (int c = 0; c < 12; ++c)
-                fmx = fmaxf(fmx, fabsf(f[k][c]));
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        fmx = fmaxf(fmx, __shfl_xor(fmx, o, 64));
-    if ((threadIdx.x & 63) == 0)
-        wmax[threadIdx.x >> 6] = fmx;
-    __syncthreads();
-    float M = 0.f;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w)
-        M = fmaxf(M, wmax[w]);
-    // scale 2^sc with M 2^sc < 2^(30 - ceil(log2 maxdeg)): a node's <= maxdeg terms stay below 2^30
-    int ex = 0;
-    (void)frexpf(M, &ex);
-    const int sc = M > 0.f ? 30 - (int)T.deg_log2 - ex : 0;
-    // (c) exact fixed-point accumulation
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-    {
-        const uint32_t j = threadIdx.x + k * NT;
-        if (j < ne)
-        {
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int c = 0; c < 3; ++c)
-                    atomicAdd(&acc[c * ms + li[k][a]], __float2int_rn(ldexpf(f[k][3 * a + c], sc)));
-        }
-    }
-    __syncthreads();
-    // (d) tile-node partials (tile-major, contiguous) + the p.Ap share
-    double pap = 0.0;
-    const float sM = (float)s.sM;
-    for (uint32_t i = threadIdx.x; i < nn; i += NT)
-    {
-        const uint2 tn = i == threadIdx.x ? tn0 : T.tnode[nb + i];
-        const float a0 = ldexpf((float)acc[i], -sc), a1 = ldexpf((float)acc[ms + i], -sc),
-                    a2 = ldexpf((float)acc[2 * ms + i], -sc);
-        float *o = T.part + 3ull * (nb + i);
-        o[0] = a0;
-        o[1] = a1;
-        o[2] = a2;
-        if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)
-        {
-            const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
-            pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
-            if (tn.x & 0x80000000u)
-            {
-                const float m = s.mass[tn.x & 0x7fffffffu] * sM;
-                pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
-                       (double)(m * p2) * (double)p2;
-            }
-        }
-    }
-    if constexpr (MODE == 1)
-    {
-        const double t = block_sum<NT>(pap, red);
-        if (threadIdx.x == 0)
-            pa.part_dot[blockIdx.x] = t;
-    }
-}
-
-// Persistent, software-pipelined form of k_keff_tiles (GEO records, CSR fold; the default FAST path).
+// Persistent, software-pipelined form of k_keff_tiles (GEO records, push fold; the default FAST path).
 // A resident grid (occupancy x CUs) walks the tiles; while a workgroup computes tile t from LDS, the
 // loads of its next tile t' (tile-node records, coordinates, corner ids, local CSR, then the z/p
 // gathers) are already in flight in registers, so each tile's memory chain overlaps the previous
@@ -817,13 +623,12 @@ struct PipeNext
     float v[3], w[3];  // x / p_old and z (MODE 1) at that node
     float m;           // its lumped mass (MODE 1: the owner slot's m s_M |p|^2 share of p.Ap)
     uint2 id[2];       // corner ids of elements threadIdx.x, threadIdx.x + 256
-    uint4 csr;         // 8 local-CSR entries (16 B) of the tile
-    uint2 pos[2];      // (PUSH) local-CSR positions of the corners of elements threadIdx.x, + NT
+    uint2 pos[2];      // local-CSR positions of the corners of elements threadIdx.x, + NT
     uint32_t slot;     // node-major partial slot of tile node threadIdx.x
     uint32_t mat[2];   // material of elements threadIdx.x, threadIdx.x + 256 (0 when M == 1)
 };
 
-template <int NT, bool SANITIZE, int MODE, bool PUSH = false>
+template <int NT, bool SANITIZE, int MODE>
 __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, PipeNext &n)
 {
     const DevTiles &T = s.t;
@@ -844,13 +649,7 @@ __device__ __forceinline__ void pipe_issue_records(const DevSys &s, uint4 hd, Pi
         // prefetched with the records: a load inside the element phase would make its wait drain
         // every record load in flight for the next tile
         n.mat[k] = T.mat ? T.mat[e0 + (j < ne ? j : 0u)] : 0u;
-        if constexpr (PUSH)
-            n.pos[k] = T.epos[e0 + (j < ne ? j : 0u)];
-    }
-    if constexpr (!PUSH)
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(T.csr_ent + 4ull * e0);  // 4 ne u16 = ne / 2 uint4
-        n.csr = i < (ne + 1) / 2 ? src[i] : uint4{0u, 0u, 0u, 0u};
+        n.pos[k] = T.epos[e0 + (j < ne ? j : 0u)];
     }
 }
 
@@ -881,22 +680,21 @@ __device__ __forceinline__ void pipe_issue_gather(const DevSys &s, const float *
 }
 
 // NT threads per workgroup, tiles of <= TE = 2 NT elements and <= NT nodes (one node per lane)
-// PUSH: each element stores its 4 corner forces at their tile-relative local-CSR positions (epos), so a
-// node's forces sit contiguously in ascending element order and the fold reads them without the
-// dependent CSR-entry lookup (same summation order, bitwise the same result as the CSR fold).
-template <bool ISO, bool SANITIZE, int MODE, int NT, bool PUSH>
+// Push fold: each element stores its 4 corner forces at their tile-relative local-CSR positions (epos),
+// so a node's forces sit contiguously in ascending element order and the fold reads them without a
+// dependent CSR-entry lookup (the order of a local-CSR fold, without its index stream).
+template <bool ISO, bool SANITIZE, int MODE, int NT>
 __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
                                                         const uint4 *__restrict__ hdr)
 {
     constexpr int TE = 2 * NT;
-    constexpr int SP = 4 * TE;  // PUSH: slots per component plane (one per (element, corner) pair)
+    constexpr int SP = 4 * TE;  // slots per component plane (one per (element, corner) pair)
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
     const uint32_t ms = T.max_tile_nodes;
-    float *sf = lds;                                                     // [12][TE]; PUSH: [3][SP]
-    uint16_t *sc = reinterpret_cast<uint16_t *>(lds + 12 * TE);  // [4*TE] local CSR (unused with PUSH)
-    float4 *sxp = reinterpret_cast<float4 *>(lds + (PUSH ? 3 * SP : 14 * TE));  // [ms] {x, y, z, v_x}
+    float *sf = lds;                                          // [3][SP] pushed corner forces
+    float4 *sxp = reinterpret_cast<float4 *>(lds + 3 * SP);  // [ms] {x, y, z, v_x}
     float2 *sq = reinterpret_cast<float2 *>(sxp + ms);                   // [ms] {v_y, v_z}
     __shared__ float dtab[kMaxM * kTab];
     __shared__ double red[NT / 64];
@@ -915,7 +713,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
     uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
     if (t < t_end)
     {
-        pipe_issue_records<NT, SANITIZE, MODE, PUSH>(s, hd, cur);
+        pipe_issue_records<NT, SANITIZE, MODE>(s, hd, cur);
         pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hd.w, cur);
     }
     const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
@@ -947,8 +745,6 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             sxp[i0] = float4{cur.c[0], cur.c[1], cur.c[2], v0};
             sq[i0] = float2{v1, v2};
         }
-        if (!PUSH && i0 < (ne + 1) / 2)
-            reinterpret_cast<uint4 *>(sc)[i0] = cur.csr;
         const uint2 id0 = cur.id[0], id1 = cur.id[1];
         const uint2 pos0 = cur.pos[0], pos1 = cur.pos[1];
         const uint32_t mat0 = cur.mat[0], mat1 = cur.mat[1];
@@ -960,7 +756,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
         const uint32_t tn_next = t + nbx;
         const uint4 hdn = hd2;
         if (tn_next < t_end)
-            pipe_issue_records<NT, SANITIZE, MODE, PUSH>(s, hdn, cur);
+            pipe_issue_records<NT, SANITIZE, MODE>(s, hdn, cur);
         hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
         // (c) elements of tile t (ablation bit 64: skipped, diagnostic timing only)
 #pragma unroll
@@ -971,22 +767,13 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             {
                 float f[12];
                 geo_element_forces<ISO>(s, k ? id1 : id0, sxp, sq, sK6, k ? mat1 : mat0, dtab, f);
-                if constexpr (PUSH)
-                {
-                    const uint2 ps = k ? pos1 : pos0;
-                    const uint32_t pq[4] = {ps.x & 0xffffu, ps.x >> 16, ps.y & 0xffffu, ps.y >> 16};
+                const uint2 ps = k ? pos1 : pos0;
+                const uint32_t pq[4] = {ps.x & 0xffffu, ps.x >> 16, ps.y & 0xffffu, ps.y >> 16};
 #pragma unroll
-                    for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < 4; ++a)
 #pragma unroll
-                        for (int c = 0; c < 3; ++c)
-                            sf[c * SP + pq[a]] = f[3 * a + c];
-                }
-                else
-                {
-#pragma unroll
-                    for (int c = 0; c < 12; ++c)
-                        sf[c * TE + j] = f[c];
-                }
+                    for (int c = 0; c < 3; ++c)
+                        sf[c * SP + pq[a]] = f[3 * a + c];
             }
         }
         __syncthreads();
@@ -1001,47 +788,15 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             float a0 = 0.f, a1 = 0.f, a2 = 0.f;
             const uint32_t qe = tn.y >> 16;
             uint32_t q = tn.y & 0xffffu;
-            if constexpr (PUSH)
-            {
-                // the node's forces are the contiguous run [q, qe) of each component plane
-                for (; q + 4 <= qe; q += 4)
-                {
-                    float f[4][3];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int c = 0; c < 3; ++c)
-                            f[u][c] = sf[c * SP + q + u];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                    {
-                        a0 += f[u][0];
-                        a1 += f[u][1];
-                        a2 += f[u][2];
-                    }
-                }
-                for (; q < qe; ++q)
-                {
-                    a0 += sf[q];
-                    a1 += sf[SP + q];
-                    a2 += sf[2 * SP + q];
-                }
-            }
+            // the node's forces are the contiguous run [q, qe) of each component plane
             for (; q + 4 <= qe; q += 4)
             {
-                uint32_t ent[4];
                 float f[4][3];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    ent[u] = sc[q + u];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                {
-                    const uint32_t el = ent[u] >> 2, c = 3u * (ent[u] & 3u);
-                    f[u][0] = sf[(c + 0) * TE + el];
-                    f[u][1] = sf[(c + 1) * TE + el];
-                    f[u][2] = sf[(c + 2) * TE + el];
-                }
+                    for (int c = 0; c < 3; ++c)
+                        f[u][c] = sf[c * SP + q + u];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                 {
@@ -1052,11 +807,9 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             }
             for (; q < qe; ++q)
             {
-                const uint32_t ent = sc[q];
-                const uint32_t el = ent >> 2, c = 3u * (ent & 3u);
-                a0 += sf[(c + 0) * TE + el];
-                a1 += sf[(c + 1) * TE + el];
-                a2 += sf[(c + 2) * TE + el];
+                a0 += sf[q];
+                a1 += sf[SP + q];
+                a2 += sf[2 * SP + q];
             }
             // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
             if (!(pa.abl & 512u))
@@ -1323,15 +1076,6 @@ inline size_t tiles_lds(const DevSys &s)
 template <bool ISO, bool SAN, int MODE, bool GEO>
 void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st)
 {
-    if (s.t.acc)
-    {
-        const size_t lds = sizeof(float) * (GEO ? 9 : 6) * (size_t)s.t.max_tile_nodes;
-        if (nt == 512)
-            k_keff_tiles_acc<ISO, SAN, MODE, 512, GEO><<<s.t.ntiles, 512, lds, st>>>(s, x, pa);
-        else
-            k_keff_tiles_acc<ISO, SAN, MODE, 256, GEO><<<s.t.ntiles, 256, lds, st>>>(s, x, pa);
-        return;
-    }
     const size_t lds = tiles_lds(s);
     if (nt == 512)
         k_keff_tiles<ISO, SAN, MODE, 512, GEO><<<s.t.ntiles, 512, lds, st>>>(s, x, pa);
@@ -1345,17 +1089,17 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 inline size_t pipe_lds(const DevSys &s)
 {
     const size_t ms = s.t.max_tile_nodes, te = 2 * (size_t)s.t.pipe_nt;
-    // PUSH: 3 component planes of 4 te (element, corner) slots; CSR fold: 12 te forces + 4 te u16 entries
-    return sizeof(float) * (s.t.push ? 12 * te : 14 * te) + ms * (16 + 8);
+    // 3 component planes of 4 te (element, corner) slots, then the tile nodes {x y z v_x}{v_y v_z}
+    return sizeof(float) * 12 * te + ms * (16 + 8);
 }
 
-template <bool ISO, int NT, bool PUSH>
+template <bool ISO, int NT>
 unsigned pipe_grid_query(const DevSys &s)
 {
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1, NT, PUSH>, NT,
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_tiles_pipe<ISO, false, 1, NT>, NT,
                                                        pipe_lds(s));
     unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     g = g < 8u ? 8u : g - g % 8u;  // whole XCD groups
@@ -1363,15 +1107,15 @@ unsigned pipe_grid_query(const DevSys &s)
     return g < need ? g : (need ? need : 8u);
 }
 
-template <bool ISO, bool SAN, int MODE, int NT, bool PUSH>
+template <bool ISO, bool SAN, int MODE, int NT>
 void launch_pipe(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
     const size_t lds = pipe_lds(s);
     if (e0 && e1)
-        hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, NT, PUSH>, dim3(s.t.pipe_grid), dim3(NT),
+        hipExtLaunchKernelGGL(k_keff_tiles_pipe<ISO, SAN, MODE, NT>, dim3(s.t.pipe_grid), dim3(NT),
                               (uint32_t)lds, st, e0, e1, 0, s, x, pa, s.t.hdr);
     else
-        k_keff_tiles_pipe<ISO, SAN, MODE, NT, PUSH><<<s.t.pipe_grid, NT, lds, st>>>(s, x, pa, s.t.hdr);
+        k_keff_tiles_pipe<ISO, SAN, MODE, NT><<<s.t.pipe_grid, NT, lds, st>>>(s, x, pa, s.t.hdr);
 }
 
 // e0/e1 (optional): hipExtLaunchKernel stamps them from the dispatch packet itself, so the timed
@@ -1388,11 +1132,9 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
     if (s.t.pipe)
     {
         if (s.t.pipe_nt == 128)
-            s.t.push ? launch_pipe<ISO, SAN, MODE, 128, true>(s, x, pa, st, e0, e1)
-                     : launch_pipe<ISO, SAN, MODE, 128, false>(s, x, pa, st, e0, e1);
+            launch_pipe<ISO, SAN, MODE, 128>(s, x, pa, st, e0, e1);
         else
-            s.t.push ? launch_pipe<ISO, SAN, MODE, 256, true>(s, x, pa, st, e0, e1)
-                     : launch_pipe<ISO, SAN, MODE, 256, false>(s, x, pa, st, e0, e1);
+            launch_pipe<ISO, SAN, MODE, 256>(s, x, pa, st, e0, e1);
         return;
     }
     if (e0)
@@ -1412,15 +1154,9 @@ unsigned fast_pipe_grid(const DevSys &s)
 {
     if (s.t.hex)
         return s.iso ? hex_grid_query<true>(s) : hex_grid_query<false>(s);
-    if (s.t.push)
-    {
-        if (s.t.pipe_nt == 128)
-            return s.iso ? pipe_grid_query<true, 128, true>(s) : pipe_grid_query<false, 128, true>(s);
-        return s.iso ? pipe_grid_query<true, 256, true>(s) : pipe_grid_query<false, 256, true>(s);
-    }
     if (s.t.pipe_nt == 128)
-        return s.iso ? pipe_grid_query<true, 128, false>(s) : pipe_grid_query<false, 128, false>(s);
-    return s.iso ? pipe_grid_query<true, 256, false>(s) : pipe_grid_query<false, 256, false>(s);
+        return s.iso ? pipe_grid_query<true, 128>(s) : pipe_grid_query<false, 128>(s);
+    return s.iso ? pipe_grid_query<true, 256>(s) : pipe_grid_query<false, 256>(s);
 }
 // the update pass is grid-stride: at most one resident wave of workgroups (occupancy x CUs), so no
 // workgroup waits for a slot behind the others' whole node ranges
