@@ -80,3 +80,26 @@ def test_local_group_requires_group_call():
     e = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, 1e-6), pcg.PcgVectors(np.zeros_like(rhs), None))
     assert not e.has_value() and "solve_pcg_group" in e.error().message
     comm.close()
+
+
+def test_rccl_single_rank_sharded_schedule():
+    """The RCCL transport on one GPU: dlopen + unique id + a 1-rank communicator, a handle attached to it
+    (the sharded schedule: per-rank scalar folds, all-gathers, the halo group call) solving the whole
+    mesh. Multi-rank RCCL needs one GPU per rank and runs in the driver's 8-GPU bench."""
+    glob = scenarios.block_case(8, 5, 6, h=0.1, tol=1e-6)
+    sK, sM = glob.scalars()
+    P = glob.packing
+    comm = shard.Comm.rccl(1, 0, shard.Comm.unique_id(), 0)
+    src = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_FAST)
+    sh = shard.build_shard(src, shard.slab_ranges(P.node_count, 1), 0)
+    s = sh.system(glob.materials, sK, sM)
+    comm.attach(s, sh)
+    x = [np.zeros(3 * sh.local_nodes, np.float32)]
+    tel = shard.solve_pcg_group([s], [sh.local_dofs(glob.static_rhs())], pcg.PcgSettings(800, 1e-6), x).value()
+    ref = oracle_system(P, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 800, 1e-6)
+    xg = np.zeros((P.node_count, 3), np.float32)
+    xg[sh.node_global[: sh.owned_nodes].astype(np.int64)] = x[0].reshape(-1, 3)[: sh.owned_nodes]
+    assert tel.converged
+    assert np.linalg.norm(xg.reshape(-1) - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    s.close()
+    comm.close()
