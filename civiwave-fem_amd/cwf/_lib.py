@@ -18,6 +18,7 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "cwf_hip.h")
 PTR_HOST, PTR_DEVICE = 0, 1
 MODE_PARITY, MODE_FAST = 0, 1
 DESC_KEEP_NODE_ORDER = 1  # cwf_system_desc.reserved flag (cwf_hip.h)
+SCENARIO_TIME_VARYING_LOADS, SCENARIO_PACK_ONLY = 1, 2  # cwf_scenario_create flags
 
 STATUS = {
     0: "CWF_OK", -1: "CWF_ERR_SIZE", -2: "CWF_ERR_NODE_RANGE", -3: "CWF_ERR_MATERIAL_RANGE",
@@ -174,6 +175,13 @@ def load() -> C.CDLL:
         "cwf_mesh_surfaces": ([P, P, P, P], i32),
         "cwf_mesh_group": ([P, u64, P, P, P], i32),
         "cwf_mesh_node_group": ([P, C.c_uint32, P, P], i32),
+        "cwf_scenario_create": ([C.c_char_p, i32, i32, i32, P], i32),
+        "cwf_scenario_info": ([P, P, P, P], i32),
+        "cwf_scenario_step": ([P, i32, P], i32),
+        "cwf_scenario_output_frame": ([P, C.c_char_p], i32),
+        "cwf_scenario_packed": ([P, C.c_char_p, P, P], i32),
+        "cwf_scenario_external_force": ([P, f64, P, u64], i32),
+        "cwf_scenario_destroy": ([P], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -377,6 +377,32 @@ int cwf_mesh_group(const cwf_mesh *mesh, uint64_t index, uint32_t *dimension, ui
 /* node indices tagged with physical group `group_id` through $Entities (Mesh::node_groups) */
 int cwf_mesh_node_group(const cwf_mesh *mesh, uint32_t group_id, const uint32_t **nodes, uint64_t *count);
 
+/* ---- native scenario driver ----------------------------------------------------
+ * The viewer backend's sequence (src/ui/viewer.cpp:200-277) in C++: load_config_from_file ->
+ * load_gmsh_file -> pre::run + pack::build_packed_buffers (loads at t = 0) -> Stepper; per frame
+ * step(simulation_time) with simulation_time = telemetry.simulation_time + time_step, then
+ * OutputManager::handle_frame (output_manager.cpp:49-87). The mesh path is taken as given, else
+ * next to the YAML file. An all-hex8 mesh runs as native hex8 in CWF_MODE_FAST. Errors carry the
+ * reference's texts prefixed "config: ", "mesh: " or "preprocess: "; every call leaves its message in
+ * cwf_hip_last_error(NULL) / cwf_hip_last_context(NULL). */
+typedef struct cwf_scenario cwf_scenario;
+#define CWF_SCENARIO_TIME_VARYING_LOADS 1 /* re-evaluate load curves at each step's start time */
+#define CWF_SCENARIO_PACK_ONLY 2          /* build the packed buffers only, no device handle (host tests) */
+int cwf_scenario_create(const char *yaml_path, int mode, int device, int flags, cwf_scenario **out);
+int cwf_scenario_info(const cwf_scenario *sc, uint64_t *nodes, uint64_t *elements, uint64_t *dofs);
+/* one Newmark frame (Stepper::step errors, e.g. "CG denominator approached zero") */
+int cwf_scenario_step(cwf_scenario *sc, int paused, cwf_step_telemetry *telemetry);
+/* derived fields of the last stepped frame -> <out_root>/vtu/frame_%05u.vtu every vtu_stride frames
+ * and one probe row per probe to <out_root>/probes/probes.csv */
+int cwf_scenario_output_frame(cwf_scenario *sc, const char *out_root);
+/* read-only view of one packed host buffer (pack.hpp:93-183 names): position0, external_force, bc_mask,
+ * bc_value, lumped_mass, lumped_mass64, connectivity, gradients, volume, material_index, offsets,
+ * element_indices, local_indices. Unknown name: CWF_ERR_ARGUMENT. */
+int cwf_scenario_packed(const cwf_scenario *sc, const char *name, const void **data, uint64_t *bytes);
+/* loads.cpp:87-174 assemble_load_vector at `time`, cast like pack.cpp:41-57 -> out f32 [3N] */
+int cwf_scenario_external_force(const cwf_scenario *sc, double time, float *out, uint64_t n);
+void cwf_scenario_destroy(cwf_scenario *sc);
+
 #ifdef __cplusplus
 }
 #endif
