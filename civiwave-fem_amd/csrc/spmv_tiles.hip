@@ -616,6 +616,43 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
 // b runs on XCD b % 8 and walks that XCD's eighth of the Morton-ordered tiles) so neighbouring tiles,
 // which share nodes, share an L2. beta (the residual step) and the material table are set up once
 // per workgroup; the p.Ap share is one per workgroup.
+// Sum of a node's contiguous run [q, qe) of pushed corner forces, in ascending order: {f_x, f_y} pairs
+// accumulate with v_pk_add_f32 straight from ds_read2_b64 (component-wise, so the same order and
+// bits as three scalar sums), f_z from its own plane.
+__device__ __forceinline__ void fold_run(const float2 *sfxy, const float *sfz, uint32_t q, uint32_t qe, float &a0,
+                                         float &a1, float &a2)
+{
+    typedef float pair_t __attribute__((ext_vector_type(2)));
+    const pair_t *pxy = reinterpret_cast<const pair_t *>(sfxy);
+    pair_t axy = {0.f, 0.f};
+    float az = 0.f;
+    for (; q + 4 <= qe; q += 4)
+    {
+        pair_t fxy[4];
+        float fz[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            fxy[u] = pxy[q + u];
+            fz[u] = sfz[q + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            axy += fxy[u];
+            az += fz[u];
+        }
+    }
+    for (; q < qe; ++q)
+    {
+        axy += pxy[q];
+        az += sfz[q];
+    }
+    a0 = axy.x;
+    a1 = axy.y;
+    a2 = az;
+}
+
 struct PipeNext
 {
     uint2 tn;          // record of tile node threadIdx.x
@@ -693,7 +730,10 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
     const uint32_t ms = T.max_tile_nodes;
-    float *sf = lds;                                          // [3][SP] pushed corner forces
+    // pushed corner forces: {f_x, f_y} pairs (one ds_write_b64 / ds_read2_b64 per two, summed with
+    // v_pk_add_f32 without repacking) and an f_z plane
+    float2 *sfxy = reinterpret_cast<float2 *>(lds);           // [SP]
+    float *sfz = lds + 2 * SP;                                // [SP]
     float4 *sxp = reinterpret_cast<float4 *>(lds + 3 * SP);  // [ms] {x, y, z, v_x}
     float2 *sq = reinterpret_cast<float2 *>(sxp + ms);                   // [ms] {v_y, v_z}
     __shared__ float dtab[kMaxM * kTab];
@@ -771,9 +811,10 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                 const uint32_t pq[4] = {ps.x & 0xffffu, ps.x >> 16, ps.y & 0xffffu, ps.y >> 16};
 #pragma unroll
                 for (int a = 0; a < 4; ++a)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        sf[c * SP + pq[a]] = f[3 * a + c];
+                {
+                    sfxy[pq[a]] = float2{f[3 * a], f[3 * a + 1]};
+                    sfz[pq[a]] = f[3 * a + 2];
+                }
             }
         }
         __syncthreads();
@@ -785,32 +826,8 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
         {
             const uint32_t i = threadIdx.x;
             const uint2 tn = tn_own;
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-            const uint32_t qe = tn.y >> 16;
-            uint32_t q = tn.y & 0xffffu;
-            // the node's forces are the contiguous run [q, qe) of each component plane
-            for (; q + 4 <= qe; q += 4)
-            {
-                float f[4][3];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        f[u][c] = sf[c * SP + q + u];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                {
-                    a0 += f[u][0];
-                    a1 += f[u][1];
-                    a2 += f[u][2];
-                }
-            }
-            for (; q < qe; ++q)
-            {
-                a0 += sf[q];
-                a1 += sf[SP + q];
-                a2 += sf[2 * SP + q];
-            }
+            float a0, a1, a2;
+            fold_run(sfxy, sfz, tn.y & 0xffffu, tn.y >> 16, a0, a1, a2);
             // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
             if (!(pa.abl & 512u))
             {

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libcwf_hip.so")
+LIB_PATH = os.environ.get("CWF_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libcwf_hip.so")  # env: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "cwf_hip.h")
 
 PTR_HOST, PTR_DEVICE = 0, 1
