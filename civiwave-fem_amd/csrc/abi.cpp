@@ -524,6 +524,9 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     s.iso = 1;
     for (uint64_t m = 0; m < d->material_count; ++m)
         s.iso &= iso_pattern(d->material_stiffness + 36 * m) ? 1 : 0;
+    if (s.M == 1)  // table order of the FAST kernels (dsrc): iso = 3x3 normal block + 3 shear diagonals
+        for (int t = 0; t < (s.iso ? 12 : 36); ++t)
+            s.d1[t] = (float)d->material_stiffness[s.iso ? (t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7) : t];
     s.hex = hex ? 1 : 0;
 
     // element records (64 B/tet; the PARITY kernels only, so none for hex8)

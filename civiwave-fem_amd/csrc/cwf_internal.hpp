@@ -103,6 +103,8 @@ struct DevSys
     double sK = 1.0;  // stiffness_scale
     double sM = 0.0;  // mass_factor
     int iso = 0;      // every material has the isotropic Voigt zero pattern
+    float d1[36] = {};  // M == 1: the material's D in f32, in the FAST kernels' table order (kernel
+                        // arguments, so the element math reads it from SGPRs)
     int hex = 0;      // elements are hex8 (FAST only): hconn / hcoord feed the hex block-Jacobi setup
     const uint32_t *hconn = nullptr;  // [8E] hex corner nodes (Gmsh order)
     const double *hcoord = nullptr;   // [3N] node coordinates

@@ -382,7 +382,9 @@ __device__ __forceinline__ void geo_element_forces(const DevSys &s, uint2 id, co
         eps[5] = fmaf(gx, u2, fmaf(gz, u0, eps[5]));
     }
     float sig[6];
-    if (mi < (uint32_t)kMaxM)
+    if (s.M == 1)  // uniform branch: D from the kernel arguments (SGPR operands, no LDS reads)
+        stress_f32<ISO>(s.d1, eps, sig);
+    else if (mi < (uint32_t)kMaxM)
         stress_f32<ISO>(dtab + kTab * mi, eps, sig);
     else
     {

@@ -604,4 +604,60 @@ inline auto take(int rc, cwf_mesh *m) -> expected<Mesh, MeshError>
     return detail::take(rc, m);
 }
 }  // namespace mesh
+
+// ---- the viewer backend's scenario sequence (viewer.cpp:200-277) over cwf_scenario_* -------------
+namespace scenario
+{
+struct ScenarioError
+{
+    std::string message;
+    std::vector<std::string> context;
+};
+class Scenario
+{
+  public:
+    [[nodiscard]] static auto create(const std::string &yaml_path, int mode = CWF_MODE_PARITY, int device = 0,
+                                     int flags = 0) -> expected<Scenario, ScenarioError>
+    {
+        cwf_scenario *s = nullptr;
+        if (cwf_scenario_create(yaml_path.c_str(), mode, device, flags, &s) != 0)
+            return unexpected<ScenarioError>{{cwf_hip_last_error(nullptr), pcg::detail::split_context(cwf_hip_last_context(nullptr))}};
+        return Scenario(s);
+    }
+    Scenario(Scenario &&o) noexcept : s_(o.s_) { o.s_ = nullptr; }
+    Scenario &operator=(Scenario &&o) noexcept
+    {
+        std::swap(s_, o.s_);
+        return *this;
+    }
+    Scenario(const Scenario &) = delete;
+    Scenario &operator=(const Scenario &) = delete;
+    ~Scenario() { cwf_scenario_destroy(s_); }
+    // Stepper::step at the scenario clock (simulation_time = telemetry.simulation_time + time_step)
+    [[nodiscard]] auto step(bool paused = false) -> expected<cwf_step_telemetry, ScenarioError>
+    {
+        cwf_step_telemetry t{};
+        if (cwf_scenario_step(s_, paused ? 1 : 0, &t) != 0)
+            return unexpected<ScenarioError>{{cwf_hip_last_error(nullptr), pcg::detail::split_context(cwf_hip_last_context(nullptr))}};
+        return t;
+    }
+    // OutputManager::handle_frame of the last stepped frame under `root` (vtu/, probes/)
+    [[nodiscard]] auto output_frame(const std::string &root) -> expected<void, ScenarioError>
+    {
+        if (cwf_scenario_output_frame(s_, root.c_str()) != 0)
+            return unexpected<ScenarioError>{{cwf_hip_last_error(nullptr), pcg::detail::split_context(cwf_hip_last_context(nullptr))}};
+        return {};
+    }
+    [[nodiscard]] std::uint64_t dof_count() const
+    {
+        std::uint64_t d = 0;
+        cwf_scenario_info(s_, nullptr, nullptr, &d);
+        return d;
+    }
+
+  private:
+    explicit Scenario(cwf_scenario *s) : s_(s) {}
+    cwf_scenario *s_ = nullptr;
+};
+}  // namespace scenario
 }  // namespace cwf::hip

@@ -72,6 +72,18 @@ int main(int argc, char **argv)
     ch::post::ProbeLogger badp(tmp + "/cpp_probes_bad.csv", {9});
     auto r = badp.log_frame(0.0, 0, f, d);
     EXPECT(!r.has_value() && r.error().message == "probe index out of range");
+
+    // the native scenario driver: packing only (no device), then a step is refused
+    auto sc = ch::scenario::Scenario::create(data + "/cantilever.yaml", CWF_MODE_PARITY, 0, CWF_SCENARIO_PACK_ONLY);
+    EXPECT(sc.has_value());
+    if (sc)
+    {
+        EXPECT(sc.value().dof_count() == 12);
+        auto st = sc.value().step();
+        EXPECT(!st.has_value() && st.error().message.find("PACK_ONLY") != std::string::npos);
+    }
+    auto nosc = ch::scenario::Scenario::create(data + "/definitely_missing.yaml");
+    EXPECT(!nosc.has_value() && nosc.error().message.find("config: ") == 0);
     std::printf("%s\n", failures ? "FAILED" : "OK");
     return failures ? 1 : 0;
 }

@@ -1,11 +1,12 @@
-# A/B of the in-tree library against civiwave-fem_amd/lib_base/libcwf_hip.so (CWF_LIB_PATH), same box
+# Same-box A/B of library builds: the in-tree lib ("new") against civiwave-fem_amd/lib_<v>/libcwf_hip.so for
+# each variant v given on the command line (CWF_LIB_PATH). usage: bash tools/ab_lib.sh base [noslp ...]
 source tools/ab.sh
-B=CWF_LIB_PATH=$PWD/civiwave-fem_amd/lib_base/libcwf_hip.so
-run c2_base $B python bench.py --no-cpu-baseline &&
-run c2_new X=1 python bench.py --no-cpu-baseline &&
-run c3_base $B python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline &&
-run c3_new X=1 python bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline &&
-run c2_base2 $B python bench.py --no-cpu-baseline &&
-run c2_new2 X=1 python bench.py --no-cpu-baseline &&
-run hex_base $B python bench.py --element hex8 --no-cpu-baseline &&
-run hex_new X=1 python bench.py --element hex8 --no-cpu-baseline
+for pass in 1 2; do
+  for cfg in c2 c3; do
+    extra=""; [ $cfg = c3 ] && extra="--config c3 --steps 3 --warmup 1"
+    run ${cfg}_new_$pass X=1 python bench.py --no-cpu-baseline $extra || exit 1
+    for v in "$@"; do
+      run ${cfg}_${v}_$pass CWF_LIB_PATH=$PWD/civiwave-fem_amd/lib_$v/libcwf_hip.so python bench.py --no-cpu-baseline $extra || exit 1
+    done
+  done
+done
