@@ -710,15 +710,38 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         // node's slots through part_slot
         std::vector<uint4> hdr(ht.ntiles);
         std::vector<uint2> tnode(ht.tile_nodes.size());
+        // tet push fold: every node's run of pushed forces gets an odd number of slots (one pad slot
+        // after an even-length run), so the runs the fold lanes walk side by side start on spread-out
+        // LDS banks (a uniform even stride such as the 24 tets of an interior Kuhn node would put all
+        // lanes on a few banks); the element corners' positions (epos) shift with their node's run
+        const bool pad_runs = t.push && !hex;
+        std::vector<uint32_t> shift;
         for (uint32_t k = 0; k < ht.ntiles; ++k)
         {
             const uint32_t e0 = ht.tile_elem_off[k], nb = ht.tile_node_off[k], nb1 = ht.tile_node_off[k + 1];
             hdr[k] = uint4{e0, ht.tile_elem_off[k + 1] - e0, nb, nb1 - nb};
             if (hex && !ht.tile_affine.empty() && ht.tile_affine[k])
                 hdr[k].x |= 0x80000000u;  // hex8 tile of parallelepipeds (k_keff_hex_tiles: constant J)
+            uint32_t padded = 0;
+            shift.assign(nb1 - nb, 0);
             for (uint32_t q = nb; q < nb1; ++q)
-                tnode[q] = uint2{ht.tile_nodes[q], (ht.csr_off[q] - (uint32_t)K * e0) |
-                                                       ((ht.csr_off[q + 1] - (uint32_t)K * e0) << 16)};
+            {
+                const uint32_t a = ht.csr_off[q] - (uint32_t)K * e0, b = ht.csr_off[q + 1] - (uint32_t)K * e0;
+                const uint32_t start = pad_runs ? padded : a;
+                tnode[q] = uint2{ht.tile_nodes[q], start | ((start + b - a) << 16)};
+                shift[q - nb] = start - a;
+                padded = start + (b - a) + ((b - a) % 2 == 0 ? 1u : 0u);
+            }
+            if (pad_runs)
+                for (uint32_t j = e0; j < ht.tile_elem_off[k + 1]; ++j)
+                {
+                    const uint2 id = ht.eid[j];
+                    uint2 &ep = ht.epos[j];
+                    const uint32_t li[4] = {id.x & 0xffffu, id.x >> 16, id.y & 0xffffu, id.y >> 16};
+                    const uint32_t p[4] = {(ep.x & 0xffffu) + shift[li[0]], (ep.x >> 16) + shift[li[1]],
+                                           (ep.y & 0xffffu) + shift[li[2]], (ep.y >> 16) + shift[li[3]]};
+                    ep = uint2{p[0] | (p[1] << 16), p[2] | (p[3] << 16)};
+                }
         }
         uint4 *dh;
         uint2 *dtn;

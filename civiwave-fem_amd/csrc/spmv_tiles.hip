@@ -727,7 +727,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                                                         const uint4 *__restrict__ hdr)
 {
     constexpr int TE = 2 * NT;
-    constexpr int SP = 4 * TE;  // slots per component plane (one per (element, corner) pair)
+    constexpr int SP = 4 * TE + NT;  // slots per component plane: (element, corner) pairs + run pads
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
@@ -1108,8 +1108,9 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 inline size_t pipe_lds(const DevSys &s)
 {
     const size_t ms = s.t.max_tile_nodes, te = 2 * (size_t)s.t.pipe_nt;
-    // 3 component planes of 4 te (element, corner) slots, then the tile nodes {x y z v_x}{v_y v_z}
-    return sizeof(float) * 12 * te + ms * (16 + 8);
+    // 3 component planes of 4 te (element, corner) slots + one pad per tile node (odd runs), then the tile
+    // nodes {x y z v_x}{v_y v_z}
+    return sizeof(float) * 3 * (4 * te + (size_t)s.t.pipe_nt) + ms * (16 + 8);
 }
 
 template <bool ISO, int NT>
