@@ -757,6 +757,14 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (!t.push)  // PUSH streams the per-element positions (epos) instead
             if (int st = upload(h, &ce, ht.csr_ent.data(), ht.csr_ent.size()))
                 return bail(st);
+        // the update pass reads each node's partial range anyway: the Dirichlet mask rides in its top bits
+        // (one 4-B stream less per PCG iteration) when the offsets leave them free
+        if (ht.node_part_off.back() <= kPartOffBits)
+        {
+            for (uint64_t n = 0; n < N; ++n)
+                ht.node_part_off[n] |= (d->bc_mask[n] & 7u) << 29;
+            t.off_mask = 1;
+        }
         if (int st = upload(h, &npo, ht.node_part_off.data(), ht.node_part_off.size()))
             return bail(st);
         uint32_t *ps;

@@ -53,7 +53,9 @@ struct DevTiles
     int hex_all_affine = 0;        // every hex tile is a parallelepiped tile (affine-only kernel variant)
     const uint4 *eid8 = nullptr;   // [E] 8 u16 local corner ids (Gmsh corner order)
     const uint4 *epos8 = nullptr;  // [E] 8 u16 local-CSR positions
-    const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile)
+    const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile); with
+                                              // off_mask, bits 29-31 of entry n carry bc_mask[n]
+    int off_mask = 0;
     const uint32_t *part_slot = nullptr;      // [total] partial index of each of those slots
     // pipelined kernel: partials stored node-major (tile node q -> part[3 tslot[q]]), so a node's partials
     // are the contiguous run part[3 node_part_off[n] .. 3 node_part_off[n+1]) and part_slot is not read
@@ -84,6 +86,8 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes = k
 // true when the supplied gradients / volumes are those of the supplied node coordinates (so FAST may
 // recompute them on the fly instead of streaming them)
 bool geometry_matches(const cwf_system_desc *d);
+
+constexpr uint32_t kPartOffBits = 0x1fffffffu;  // node_part_off value bits (the rest: bc_mask, off_mask)
 
 struct DevSys
 {

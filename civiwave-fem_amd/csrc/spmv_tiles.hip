@@ -830,6 +830,20 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
             const uint2 tn = tn_own;
             float a0, a1, a2;
             fold_run(sfxy, sfz, tn.y & 0xffffu, tn.y >> 16, a0, a1, a2);
+            float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+            if constexpr (MODE == 1)
+            {
+                p0 = sxp[i].w;
+                p1 = sq[i].x;
+                p2 = sq[i].y;
+                if (tn.x & 0x80000000u)  // the node's owner slot carries its mass term m s_M p (once)
+                {
+                    const float m = m_own * sM;
+                    a0 = fmaf(m, p0, a0);
+                    a1 = fmaf(m, p1, a1);
+                    a2 = fmaf(m, p2, a2);
+                }
+            }
             // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
             if (!(pa.abl & 512u))
             {
@@ -839,16 +853,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                 o[2] = a2;
             }
             if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
-            {
-                const float p0 = sxp[i].w, p1 = sq[i].x, p2 = sq[i].y;
                 pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
-                if (tn.x & 0x80000000u)  // the node's owner slot adds its mass term m s_M |p|^2 once
-                {
-                    const float m = m_own * sM;
-                    pap += (double)(m * p0) * (double)p0 + (double)(m * p1) * (double)p1 +
-                           (double)(m * p2) * (double)p2;
-                }
-            }
         }
         __syncthreads();  // LDS is refilled by the next tile
         hd = hdn;
@@ -930,7 +935,7 @@ __global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__
     if (n >= s.N)
         return;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (uint32_t q = T.node_part_off[n]; q < T.node_part_off[n + 1]; ++q)
+    for (uint32_t q = T.node_part_off[n] & kPartOffBits; q < (T.node_part_off[n + 1] & kPartOffBits); ++q)
     {
         const float *pp = T.part + 3ull * (T.node_major ? q : T.part_slot[q]);
         a0 += pp[0];
@@ -992,9 +997,10 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         }
         // every independent load first: the partial run [q0, q1) (node-major: contiguous, no slot
         // indirection) and the node's vectors are in flight together
-        const uint32_t q0 = T.node_part_off[n], q1 = T.node_part_off[n + 1];
-        const uint32_t mk = s.mask[n];
-        const float m = s.mass[n] * sM;
+        const uint32_t o0 = T.node_part_off[n], q0 = o0 & kPartOffBits, q1 = T.node_part_off[n + 1] & kPartOffBits;
+        const uint32_t mk = T.off_mask ? o0 >> 29 : s.mask[n];
+        // the tiles kernel folded m s_M p into the node's first partial; a node of no element has none
+        const float m = q0 == q1 ? s.mass[n] * sM : 0.f;
         float pv[3], zv[3], xv[3], rv0[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k)
@@ -1049,7 +1055,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         {
             const uint32_t d = 3u * n + k;
             const float pk = fmaf(beta, pv[k], zv[k]);  // same expression as the tiles gather
-            const float apk = (mk & (1u << k)) ? pk : fmaf(m, pk, av[k]);
+            const float apk = (mk & (1u << k)) ? pk : (q0 == q1 ? m * pk : av[k]);
             float xn = fmaf(alpha, pk, xv[k]);
             float rw = fmaf(-alpha, apk, rv0[k]);
             if (mk & (1u << k))
