@@ -710,11 +710,14 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         // node's slots through part_slot
         std::vector<uint4> hdr(ht.ntiles);
         std::vector<uint2> tnode(ht.tile_nodes.size());
-        // tet push fold: every node's run of pushed forces gets an odd number of slots (one pad slot
-        // after an even-length run), so the runs the fold lanes walk side by side start on spread-out
-        // LDS banks (a uniform even stride such as the 24 tets of an interior Kuhn node would put all
-        // lanes on a few banks); the element corners' positions (epos) shift with their node's run
+        // tet push fold: every node's run of pushed forces starts on an even slot (the fold reads two
+        // {f_x, f_y} pairs with one ds_read_b128 and two f_z with one ds_read_b64) and gets 2 (mod 4)
+        // slots, so the half-start offsets of side-by-side fold lanes are odd multiples apart and spread
+        // over the LDS banks (a uniform stride such as the 24 tets of an interior Kuhn node would put all
+        // lanes on a few banks). A tile whose pads would overflow the kernel's slot budget (4 te + 2 nt)
+        // only rounds to even. The element corners' positions (epos) shift with their node's run.
         const bool pad_runs = t.push && !hex;
+        const uint32_t slot_budget = 8u * (uint32_t)t.pipe_nt + 2u * (uint32_t)t.pipe_nt;
         std::vector<uint32_t> shift;
         for (uint32_t k = 0; k < ht.ntiles; ++k)
         {
@@ -722,15 +725,23 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             hdr[k] = uint4{e0, ht.tile_elem_off[k + 1] - e0, nb, nb1 - nb};
             if (hex && !ht.tile_affine.empty() && ht.tile_affine[k])
                 hdr[k].x |= 0x80000000u;  // hex8 tile of parallelepipeds (k_keff_hex_tiles: constant J)
-            uint32_t padded = 0;
             shift.assign(nb1 - nb, 0);
-            for (uint32_t q = nb; q < nb1; ++q)
+            for (int spread = 1; spread >= 0; --spread)
             {
-                const uint32_t a = ht.csr_off[q] - (uint32_t)K * e0, b = ht.csr_off[q + 1] - (uint32_t)K * e0;
-                const uint32_t start = pad_runs ? padded : a;
-                tnode[q] = uint2{ht.tile_nodes[q], start | ((start + b - a) << 16)};
-                shift[q - nb] = start - a;
-                padded = start + (b - a) + ((b - a) % 2 == 0 ? 1u : 0u);
+                uint32_t padded = 0;
+                for (uint32_t q = nb; q < nb1; ++q)
+                {
+                    const uint32_t a = ht.csr_off[q] - (uint32_t)K * e0, b = ht.csr_off[q + 1] - (uint32_t)K * e0;
+                    const uint32_t start = pad_runs ? padded : a;
+                    tnode[q] = uint2{ht.tile_nodes[q], start | ((start + b - a) << 16)};
+                    shift[q - nb] = start - a;
+                    uint32_t len = (b - a + 1u) & ~1u;  // even
+                    if (spread && (len / 2u) % 2u == 0u)
+                        len += 2u;  // 2 (mod 4)
+                    padded = start + len;
+                }
+                if (!pad_runs || padded <= slot_budget)
+                    break;
             }
             if (pad_runs)
                 for (uint32_t j = e0; j < ht.tile_elem_off[k + 1]; ++j)

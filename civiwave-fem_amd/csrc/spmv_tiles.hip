@@ -626,26 +626,22 @@ __device__ __forceinline__ void fold_run(const float2 *sfxy, const float *sfz, u
 {
     typedef float pair_t __attribute__((ext_vector_type(2)));
     const pair_t *pxy = reinterpret_cast<const pair_t *>(sfxy);
+    // runs start on even slots: two entries per step, {f_x, f_y} x 2 in one ds_read_b128 (4 LDS cycles) and
+    // f_z x 2 in one ds_read_b64 (2 cycles) instead of merged ds_read2_b64 / ds_read2_b32 (8 + 4)
+    typedef float quad_t __attribute__((ext_vector_type(4)));
     pair_t axy = {0.f, 0.f};
     float az = 0.f;
-    for (; q + 4 <= qe; q += 4)
+#pragma unroll 1
+    for (; q + 2 <= qe; q += 2)
     {
-        pair_t fxy[4];
-        float fz[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-        {
-            fxy[u] = pxy[q + u];
-            fz[u] = sfz[q + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-        {
-            axy += fxy[u];
-            az += fz[u];
-        }
+        const quad_t f2 = *reinterpret_cast<const quad_t *>(pxy + q);
+        const pair_t z2 = *reinterpret_cast<const pair_t *>(sfz + q);
+        axy += f2.xy;
+        az += z2.x;
+        axy += f2.zw;
+        az += z2.y;
     }
-    for (; q < qe; ++q)
+    if (q < qe)
     {
         axy += pxy[q];
         az += sfz[q];
@@ -727,7 +723,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                                                         const uint4 *__restrict__ hdr)
 {
     constexpr int TE = 2 * NT;
-    constexpr int SP = 4 * TE + NT;  // slots per component plane: (element, corner) pairs + run pads
+    constexpr int SP = 4 * TE + 2 * NT;  // slots per component plane: (element, corner) pairs + run pads
     constexpr int kTab = ISO ? 12 : 36;
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
@@ -1116,7 +1112,7 @@ inline size_t pipe_lds(const DevSys &s)
     const size_t ms = s.t.max_tile_nodes, te = 2 * (size_t)s.t.pipe_nt;
     // 3 component planes of 4 te (element, corner) slots + one pad per tile node (odd runs), then the tile
     // nodes {x y z v_x}{v_y v_z}
-    return sizeof(float) * 3 * (4 * te + (size_t)s.t.pipe_nt) + ms * (16 + 8);
+    return sizeof(float) * 3 * (4 * te + 2 * (size_t)s.t.pipe_nt) + ms * (16 + 8);
 }
 
 template <bool ISO, int NT>
