@@ -261,7 +261,7 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     {
         h->ev.resize(2 * kMaxBatch);
         for (auto &e : h->ev)
-            HIPTRY(h, hipEventCreate(&e));
+            HIPTRY(h, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // no L2 write-back per timed launch
     }
     uint64_t prev_enq = 0, prev_nb = 0;
     for (;;)
