@@ -84,8 +84,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch  # loaded before libcwf_hip.so so both share one HIP runtime
 
+    # one GPU per rank; ranks beyond the visible GPUs share them round-robin (a 1-GPU rehearsal of the
+    # multi-rank path; device_count() does not initialise the GPU)
+    ngpu = max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(local_rank % ngpu)
 
     dist = None
     if world > 1:
@@ -101,7 +104,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    device = local_rank if world > 1 else 0
+    device = local_rank % ngpu if world > 1 else 0
     mode = _lib.MODE_FAST if args.mode == "fast" else _lib.MODE_PARITY
     comm = None
     if world == 1:
