@@ -844,7 +844,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(st);
     if (int st = dalloc(h, &h->inv, 9 * N))
         return bail(st);
-    if (int st = dalloc(h, &h->inv6, 6 * N))
+    if (int st = dalloc(h, &h->inv6, 4 * N))
         return bail(st);
     const uint64_t chunks = (D + d->reduction_block - 1) / d->reduction_block;
     h->part_cap = std::max<uint64_t>(

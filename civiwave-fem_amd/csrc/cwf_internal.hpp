@@ -151,7 +151,7 @@ struct cwf_hip_system
     // solver scratch (f32 dofs) and partials
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
     float *inv = nullptr;   // block Jacobi [9N]
-    float *inv6 = nullptr;  // FAST: symmetric block inverse packed [6N]
+    float *inv6 = nullptr;  // FAST: symmetric block inverse packed to 16 B per node {fp32 scale, 6 x fp16}
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
     uint64_t part_cap = 0;
     // FAST-mode internal node renumbering (Morton order of the coordinates): perm[i] = caller's node of

@@ -891,24 +891,43 @@ __global__ __launch_bounds__(1024) void k_fold_pair(const double *__restrict__ a
 }
 
 // FAST: symmetrise the block inverse (upper triangle wins, so k_precond and the update agree) and
-// pack it to 6 floats per node for the update pass
+// pack it to 16 B per node for the update pass: one fp32 scale (the largest magnitude of the block) and
+// the six upper-triangle entries as fp16 fractions of it. The dequantised values are written back to the
+// 9-float copy, so the prologue's z (k_precond) and the update's z use the same symmetric operator
+// (≤2^-11 relative per entry: a preconditioner change, the solve still stops at the same tolerance).
 __global__ __launch_bounds__(256) void k_sym_inverse(uint32_t N, float *__restrict__ inv9, float *__restrict__ inv6)
 {
     const uint32_t n = blockIdx.x * 256u + threadIdx.x;
     if (n >= N)
         return;
     float *a = inv9 + 9ull * n;
-    const float a00 = a[0], a01 = a[1], a02 = a[2], a11 = a[4], a12 = a[5], a22 = a[8];
-    a[3] = a01;
-    a[6] = a02;
-    a[7] = a12;
-    float *b = inv6 + 6ull * n;
-    b[0] = a00;
-    b[1] = a01;
-    b[2] = a02;
-    b[3] = a11;
-    b[4] = a12;
-    b[5] = a22;
+    const float v[6] = {a[0], a[1], a[2], a[4], a[5], a[8]};  // a00 a01 a02 a11 a12 a22
+    float sc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        sc = fmaxf(sc, fabsf(v[k]));
+    sc = sc > 0.f ? sc : 1.f;
+    const float rs = 1.f / sc;
+    _Float16 q[6];
+    float d[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+    {
+        q[k] = (_Float16)(v[k] * rs);
+        d[k] = (float)q[k] * sc;  // the update's dequantisation, bit for bit
+    }
+    a[0] = d[0];
+    a[1] = a[3] = d[1];
+    a[2] = a[6] = d[2];
+    a[4] = d[3];
+    a[5] = a[7] = d[4];
+    a[8] = d[5];
+    uint4 w;
+    w.x = __float_as_uint(sc);
+    w.y = (uint32_t)__builtin_bit_cast(uint16_t, q[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, q[1]) << 16);
+    w.z = (uint32_t)__builtin_bit_cast(uint16_t, q[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, q[3]) << 16);
+    w.w = (uint32_t)__builtin_bit_cast(uint16_t, q[4]) | ((uint32_t)__builtin_bit_cast(uint16_t, q[5]) << 16);
+    reinterpret_cast<uint4 *>(inv6)[n] = w;
 }
 
 __global__ __launch_bounds__(256) void k_halo_pack(const uint32_t *__restrict__ idx, uint64_t n,
@@ -1006,8 +1025,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             xv[k] = x[3u * n + k];
             rv0[k] = r[3u * n + k];
         }
-        const float2 *i2 = reinterpret_cast<const float2 *>(inv + 6ull * n);
-        const float2 u0 = i2[0], u1 = i2[1], u2 = i2[2];
+        const uint4 iw = reinterpret_cast<const uint4 *>(inv)[n];  // {scale, 6 x fp16} (k_sym_inverse)
         float a0 = 0.f, a1 = 0.f, a2 = 0.f;
         if (T.node_major)
         {
@@ -1064,8 +1082,14 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             p[d] = pk;
             rv[k] = rw;
         }
-        // symmetric block inverse, 6 floats per node {a00 a01 a02 a11 a12 a22} (three 8-B loads)
-        const float iv[9] = {u0.x, u0.y, u1.x, u0.y, u1.y, u2.x, u1.x, u2.x, u2.y};
+        // symmetric block inverse {a00 a01 a02 a11 a12 a22}: fp16 fractions of one fp32 scale, one 16-B load
+        const float sc = __uint_as_float(iw.x);
+        const auto h16 = [sc](uint32_t w, int hi) {
+            return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? w >> 16 : w & 0xffffu)) * sc;
+        };
+        const float b00 = h16(iw.y, 0), b01 = h16(iw.y, 1), b02 = h16(iw.z, 0), b11 = h16(iw.z, 1),
+                    b12 = h16(iw.w, 0), b22 = h16(iw.w, 1);
+        const float iv[9] = {b00, b01, b02, b01, b11, b12, b02, b12, b22};
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
