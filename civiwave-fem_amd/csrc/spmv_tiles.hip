@@ -323,6 +323,7 @@ struct PcgArgs
     unsigned it;
     double *hist;
     unsigned abl;  // diagnostic ablation bits (CWF_ABLATE), 0 in normal runs
+    float *pnew;   // out (PCG): the owner slot of every tile node stores the new p = z + beta p_old here
 };
 
 // Pipelined-kernel element body (GEO). With edge columns c_k = x_k - x_0 and r_k their cofactor rows
@@ -590,6 +591,13 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
         o[0] = a0;
         o[1] = a1;
         o[2] = a2;
+        if (MODE == 1 && pa.pnew && (tn.x & 0x80000000u))  // owner slot: the new p for the update pass
+        {
+            float *q = pa.pnew + 3ull * (tn.x & 0x7fffffffu);
+            q[0] = sp[i];
+            q[1] = sp[ms + i];
+            q[2] = sp[2 * ms + i];
+        }
         if (MODE == 1 && !(pa.abl & 4u) && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
         {
             const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
@@ -838,6 +846,13 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                     a0 = fmaf(m, p0, a0);
                     a1 = fmaf(m, p1, a1);
                     a2 = fmaf(m, p2, a2);
+                    if (pa.pnew)  // and stores the new p for the update pass (no z / p_old re-read there)
+                    {
+                        float *q = pa.pnew + 3ull * (tn.x & 0x7fffffffu);
+                        q[0] = p0;
+                        q[1] = p1;
+                        q[2] = p2;
+                    }
                 }
             }
             // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
@@ -970,7 +985,8 @@ __global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__
 
 __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, float *__restrict__ x,
-    float *__restrict__ r, float *__restrict__ z, float *__restrict__ p, Ctl *__restrict__ ctl,
+    float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold, float *__restrict__ pnew,
+    Ctl *__restrict__ ctl,
     const double *__restrict__ part_dot, unsigned ntp, double *__restrict__ prr, double *__restrict__ prz,
     unsigned it)
 {
@@ -1007,7 +1023,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         {
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                p[3u * n + k] = fmaf(beta, p[3u * n + k], z[3u * n + k]);
+                pnew[3u * n + k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
             continue;
         }
         // every independent load first: the partial run [q0, q1) (node-major: contiguous, no slot
@@ -1016,12 +1032,27 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         const uint32_t mk = T.off_mask ? o0 >> 29 : s.mask[n];
         // the tiles kernel folded m s_M p into the node's first partial; a node of no element has none
         const float m = q0 == q1 ? s.mass[n] * sM : 0.f;
-        float pv[3], zv[3], xv[3], rv0[3];
+        // a node in a tile has its new p from its owner slot (k_keff_tiles*: pnew); a node of no element
+        // forms it here, with the same expression
+        float pv[3], xv[3], rv0[3];
+        if (q0 != q1)
+        {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                pv[k] = pnew[3u * n + k];
+        }
+        else
+        {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+            {
+                pv[k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
+                pnew[3u * n + k] = pv[k];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
-            pv[k] = p[3u * n + k];
-            zv[k] = z[3u * n + k];
             xv[k] = x[3u * n + k];
             rv0[k] = r[3u * n + k];
         }
@@ -1068,7 +1099,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         for (int k = 0; k < 3; ++k)
         {
             const uint32_t d = 3u * n + k;
-            const float pk = fmaf(beta, pv[k], zv[k]);  // same expression as the tiles gather
+            const float pk = pv[k];
             const float apk = (mk & (1u << k)) ? pk : (q0 == q1 ? m * pk : av[k]);
             float xn = fmaf(alpha, pk, xv[k]);
             float rw = fmaf(-alpha, apk, rv0[k]);
@@ -1079,7 +1110,6 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             }
             x[d] = xn;
             r[d] = rw;
-            p[d] = pk;
             rv[k] = rw;
         }
         // symmetric block inverse {a00 a01 a02 a11 a12 a22}: fp16 fractions of one fp32 scale, one 16-B load
@@ -1253,6 +1283,11 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
         k_keff_finalize<false><<<g, 256, 0, st>>>(s, x, y);
 }
 
+// FAST search directions ping-pong by iteration parity between p and the (FAST-idle) Ap buffer:
+// iteration `it` reads p_old from one and writes the new p to the other (the prologue's p is in p)
+inline float *fast_p_old(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->Ap : h->p; }
+inline float *fast_p_new(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p : h->Ap; }
+
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
@@ -1266,14 +1301,14 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e
     // beta / convergence: a single handle folds the update kernel's per-workgroup {r.r, r.z} shares
     // directly; a shard reads the all-gathered per-rank pairs
     PcgArgs pa = fast_direct_fold(h)
-                     ? PcgArgs{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->part1, h->part2,
-                               fast_update_blocks(s), 1u, it, h->hist, abl}
-                     : PcgArgs{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
-                               (unsigned)h->nranks, 2u, it, h->hist, abl};
+                     ? PcgArgs{h->z, h->ctl, h->part0, h->part1, h->part2,
+                               fast_update_blocks(s), 1u, it, h->hist, abl, fast_p_new(h, it)}
+                     : PcgArgs{h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
+                               (unsigned)h->nranks, 2u, it, h->hist, abl, fast_p_new(h, it)};
     if (s.iso)
-        launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st, e0, e1);
+        launch_tiles<true, false, 1>(s, fast_p_old(h, it), pa, tile_threads(), st, e0, e1);
     else
-        launch_tiles<false, false, 1>(s, h->p, pa, tile_threads(), st, e0, e1);
+        launch_tiles<false, false, 1>(s, fast_p_old(h, it), pa, tile_threads(), st, e0, e1);
 }
 
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st)
@@ -1281,7 +1316,8 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
     const DevSys &s = h->ds;
     const bool direct = fast_direct_fold(h);
     k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
-        s, rhs, h->inv6, h->x, h->r, h->z, h->p, h->ctl, direct ? h->part0 : h->g_pap,
+        s, rhs, h->inv6, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
+        direct ? h->part0 : h->g_pap,
         direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it);
 }
 
@@ -1289,7 +1325,7 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    PcgArgs pa{abl & 2u ? h->Ap : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
+    PcgArgs pa{h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
                h->hist, abl | 32u};
     for (int i = 0; i < reps; ++i)
         launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
