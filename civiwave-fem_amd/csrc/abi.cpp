@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "blockinv_pack.hpp"
 #include "cwf_internal.hpp"
 
 namespace cwf
@@ -839,7 +840,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     }
     // solver scratch
     const uint64_t D = 3 * N;
-    for (float **v : {&h->x, &h->r, &h->p, &h->z, &h->Ap, &h->rhs, &h->tmp})
+    for (float **v : {&h->x, &h->r, &h->p, &h->p2, &h->z, &h->Ap, &h->rhs, &h->tmp})
         if (int st = dalloc(h, v, D))
             return bail(st);
     if (int st = dalloc(h, &h->inv, 9 * N))
@@ -1122,6 +1123,58 @@ int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64
         return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
     return 0;
+}
+
+int cwf_hip_fast_block_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int kind, uint32_t *packed_out,
+                               uint64_t *fallback_nodes)
+{
+    if (int st = check_ready(h))
+        return st;
+    const uint64_t N = h->ds.N, req = 9ull * N;
+    if (n < req)
+        return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
+                         "required=" + std::to_string(req) + " available=" + std::to_string(n));
+    if (h->mode != CWF_MODE_FAST)
+        return set_error(h, CWF_ERR_ARGUMENT, "FAST-mode operator requested on a PARITY handle");
+    fast_block_inverse(h, h->stream);
+    HIPTRY(h, hipGetLastError());
+    if (int st = vec_out(h, h->inv, inv_out, kind, 9))
+        return st;
+    if (packed_out || fallback_nodes)
+    {
+        std::vector<uint32_t> w(4 * N);
+        if (N)
+            HIPTRY(h, hipMemcpyAsync(w.data(), h->inv6, 16 * N, hipMemcpyDeviceToHost, h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+        std::vector<uint32_t> perm;  // caller's node of internal node i
+        if (h->perm)
+        {
+            perm.resize(N);
+            HIPTRY(h, hipMemcpy(perm.data(), h->perm, 4 * N, hipMemcpyDeviceToHost));
+        }
+        std::vector<uint32_t> out(4 * N);
+        uint64_t nf = 0;
+        for (uint64_t i = 0; i < N; ++i)
+        {
+            const uint64_t c = h->perm ? perm[i] : i;
+            for (int k = 0; k < 4; ++k)
+                out[4 * c + k] = w[4 * i + k];
+            nf += (int32_t)w[4 * i] < 0;
+        }
+        if (packed_out)
+            std::memcpy(packed_out, out.data(), out.size() * sizeof(uint32_t));
+        if (fallback_nodes)
+            *fallback_nodes = nf;
+    }
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_pack_block_inverse(const float *v, uint32_t mask, uint32_t *w, float *d)
+{
+    if (!v || !w || !d)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    return cwf::pack_block_inverse(v, mask, w, d) ? 1 : 0;
 }
 
 int cwf_hip_dot(cwf_hip_system *h, const float *a, const float *b, uint64_t n, int kind, double *out,

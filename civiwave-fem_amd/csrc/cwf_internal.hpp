@@ -149,9 +149,11 @@ struct cwf_hip_system
     std::vector<void *> owned;
     uint64_t bytes = 0;
     // solver scratch (f32 dofs) and partials
+    // Ap is scratch (apply_keff staging, PARITY's K p, the prologues' K x); FAST PCG never reads it
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
-    float *inv = nullptr;   // block Jacobi [9N]
-    float *inv6 = nullptr;  // FAST: symmetric block inverse packed to 16 B per node {fp32 scale, 6 x fp16}
+    float *p2 = nullptr;    // FAST: the search direction of odd iterations (p / p2 ping-pong, spmv_tiles.hip)
+    float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
+    float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
     uint64_t part_cap = 0;
     // FAST-mode internal node renumbering (Morton order of the coordinates): perm[i] = caller's node of

@@ -25,6 +25,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "blockinv_pack.hpp"
 #include "cwf_internal.hpp"
 
 namespace cwf
@@ -905,44 +906,29 @@ __global__ __launch_bounds__(1024) void k_fold_pair(const double *__restrict__ a
     }
 }
 
-// FAST: symmetrise the block inverse (upper triangle wins, so k_precond and the update agree) and
-// pack it to 16 B per node for the update pass: one fp32 scale (the largest magnitude of the block) and
-// the six upper-triangle entries as fp16 fractions of it. The dequantised values are written back to the
-// 9-float copy, so the prologue's z (k_precond) and the update's z use the same symmetric operator
-// (≤2^-11 relative per entry: a preconditioner change, the solve still stops at the same tolerance).
-__global__ __launch_bounds__(256) void k_sym_inverse(uint32_t N, float *__restrict__ inv9, float *__restrict__ inv6)
+// FAST: symmetrise the block inverse (upper triangle wins, so k_precond and the update agree) and pack
+// it to 16 B per node for the update pass in the Jacobi-scaled form of blockinv_pack.hpp (fp32 scale,
+// fp16 row scales and correlations; a flagged fp32 fallback for blocks that form does not hold). The
+// operator the solve applies is written back to the 9-float copy, so the prologue's z (k_precond) and
+// the update's z use the same symmetric preconditioner.
+__global__ __launch_bounds__(256) void k_sym_inverse(uint32_t N, const uint32_t *__restrict__ mask,
+                                                     float *__restrict__ inv9, float *__restrict__ inv6)
 {
     const uint32_t n = blockIdx.x * 256u + threadIdx.x;
     if (n >= N)
         return;
     float *a = inv9 + 9ull * n;
     const float v[6] = {a[0], a[1], a[2], a[4], a[5], a[8]};  // a00 a01 a02 a11 a12 a22
-    float sc = 0.f;
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-        sc = fmaxf(sc, fabsf(v[k]));
-    sc = sc > 0.f ? sc : 1.f;
-    const float rs = 1.f / sc;
-    _Float16 q[6];
+    uint32_t w[4];
     float d[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-    {
-        q[k] = (_Float16)(v[k] * rs);
-        d[k] = (float)q[k] * sc;  // the update's dequantisation, bit for bit
-    }
+    (void)pack_block_inverse(v, mask[n], w, d);
     a[0] = d[0];
     a[1] = a[3] = d[1];
     a[2] = a[6] = d[2];
     a[4] = d[3];
     a[5] = a[7] = d[4];
     a[8] = d[5];
-    uint4 w;
-    w.x = __float_as_uint(sc);
-    w.y = (uint32_t)__builtin_bit_cast(uint16_t, q[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, q[1]) << 16);
-    w.z = (uint32_t)__builtin_bit_cast(uint16_t, q[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, q[3]) << 16);
-    w.w = (uint32_t)__builtin_bit_cast(uint16_t, q[4]) | ((uint32_t)__builtin_bit_cast(uint16_t, q[5]) << 16);
-    reinterpret_cast<uint4 *>(inv6)[n] = w;
+    reinterpret_cast<uint4 *>(inv6)[n] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 __global__ __launch_bounds__(256) void k_halo_pack(const uint32_t *__restrict__ idx, uint64_t n,
@@ -984,7 +970,8 @@ __global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__
 }
 
 __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
-    DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, float *__restrict__ x,
+    DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, const float *__restrict__ inv9,
+    float *__restrict__ x,
     float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold, float *__restrict__ pnew,
     Ctl *__restrict__ ctl,
     const double *__restrict__ part_dot, unsigned ntp, double *__restrict__ prr, double *__restrict__ prz,
@@ -1056,7 +1043,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             xv[k] = x[3u * n + k];
             rv0[k] = r[3u * n + k];
         }
-        const uint4 iw = reinterpret_cast<const uint4 *>(inv)[n];  // {scale, 6 x fp16} (k_sym_inverse)
+        const uint4 iw = reinterpret_cast<const uint4 *>(inv)[n];  // 16-B record (k_sym_inverse)
         float a0 = 0.f, a1 = 0.f, a2 = 0.f;
         if (T.node_major)
         {
@@ -1112,13 +1099,22 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             r[d] = rw;
             rv[k] = rw;
         }
-        // symmetric block inverse {a00 a01 a02 a11 a12 a22}: fp16 fractions of one fp32 scale, one 16-B load
-        const float sc = __uint_as_float(iw.x);
-        const auto h16 = [sc](uint32_t w, int hi) {
-            return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? w >> 16 : w & 0xffffu)) * sc;
-        };
-        const float b00 = h16(iw.y, 0), b01 = h16(iw.y, 1), b02 = h16(iw.z, 0), b11 = h16(iw.z, 1),
-                    b12 = h16(iw.w, 0), b22 = h16(iw.w, 1);
+        // symmetric block inverse {a00 a01 a02 a11 a12 a22} from the 16-B Jacobi-scaled record
+        // (blockinv_pack.hpp); a flagged block (negative scale) reads its fp32 copy instead
+        float bv[6];
+        if ((int)iw.x >= 0)
+            unpack_block_inverse(iw.y, iw.z, iw.w, __uint_as_float(iw.x), bv);
+        else
+        {
+            const float *a9 = inv9 + 9ull * n;
+            bv[0] = a9[0];
+            bv[1] = a9[1];
+            bv[2] = a9[2];
+            bv[3] = a9[4];
+            bv[4] = a9[5];
+            bv[5] = a9[8];
+        }
+        const float b00 = bv[0], b01 = bv[1], b02 = bv[2], b11 = bv[3], b12 = bv[4], b22 = bv[5];
         const float iv[9] = {b00, b01, b02, b01, b11, b12, b02, b12, b22};
 #pragma unroll
         for (int k = 0; k < 3; ++k)
@@ -1283,10 +1279,10 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
         k_keff_finalize<false><<<g, 256, 0, st>>>(s, x, y);
 }
 
-// FAST search directions ping-pong by iteration parity between p and the (FAST-idle) Ap buffer:
-// iteration `it` reads p_old from one and writes the new p to the other (the prologue's p is in p)
-inline float *fast_p_old(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->Ap : h->p; }
-inline float *fast_p_new(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p : h->Ap; }
+// FAST search directions ping-pong by iteration parity between p and p2: iteration `it` reads p_old
+// from one and writes the new p to the other (the prologue's p is in p)
+inline float *fast_p_old(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p2 : h->p; }
+inline float *fast_p_new(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p : h->p2; }
 
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
@@ -1316,7 +1312,7 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
     const DevSys &s = h->ds;
     const bool direct = fast_direct_fold(h);
     k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
-        s, rhs, h->inv6, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
+        s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
         direct ? h->part0 : h->g_pap,
         direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it);
 }
@@ -1346,7 +1342,7 @@ void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
     else
         parity_block_jacobi(h, h->inv, st);
     if (h->ds.N)
-        k_sym_inverse<<<grid_for(h->ds.N, 256), 256, 0, st>>>(h->ds.N, h->inv, h->inv6);
+        k_sym_inverse<<<grid_for(h->ds.N, 256), 256, 0, st>>>(h->ds.N, h->ds.mask, h->inv, h->inv6);
 }
 
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st)

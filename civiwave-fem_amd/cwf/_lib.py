@@ -137,6 +137,8 @@ def load() -> C.CDLL:
         "cwf_hip_keff_timed": ([P, P, P, i32, P], i32),
         "cwf_hip_apply_keff": ([P, P, P, u64, i32], i32),
         "cwf_hip_build_block_jacobi_inverse": ([P, P, u64, i32], i32),
+        "cwf_hip_fast_block_inverse": ([P, P, u64, i32, P, P], i32),
+        "cwf_pack_block_inverse": ([P, C.c_uint32, P, P], i32),
         "cwf_hip_dot": ([P, P, P, u64, i32, P, P], i32),
         "cwf_hip_solve_pcg": ([P, P, P, P, P, u64, i32, P], i32),
         "cwf_hip_residual_history": ([P, P, u64, P], i32),

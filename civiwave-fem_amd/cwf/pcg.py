@@ -216,6 +216,33 @@ def build_block_jacobi_inverse(system: MatrixFreeSystem, workspace: MatrixFreeWo
     return Expected(None) if st == 0 else Expected(error=system._err())
 
 
+def fast_block_inverse(system: MatrixFreeSystem, out_inverse, packed=None) -> Expected:
+    """The preconditioner a FAST solve applies (no reference counterpart; cwf_hip_fast_block_inverse):
+    build_block_jacobi_inverse symmetrised, restricted to the free axes and dequantised from the
+    update pass's 16-B record. `packed` (optional host u32[4 N]) receives the records. The value is the
+    number of nodes applied from their fp32 block (the packing's fallback)."""
+    required = system.node_count * 9
+    if _size(out_inverse) < required:
+        return Expected(error=PcgError("block inverse span too small",
+                                       [f"required={required}", f"available={_size(out_inverse)}"]))
+    h = system.handle()
+    nf = C.c_uint64()
+    st = _lib.load().cwf_hip_fast_block_inverse(h, _lib.ptr(out_inverse), _size(out_inverse), _kind(out_inverse),
+                                                _lib.ptr(packed) if packed is not None else None, C.byref(nf))
+    return Expected(int(nf.value)) if st == 0 else Expected(error=system._err())
+
+
+def pack_block_inverse(upper, mask: int):
+    """Host packing of one node's block (blockinv_pack.hpp, the code the device runs): upper =
+    {a00 a01 a02 a11 a12 a22} f32, mask bit k = axis k constrained. Returns (packed, record u32[4],
+    applied upper triangle f32[6])."""
+    v = np.ascontiguousarray(upper, np.float32)
+    w = np.zeros(4, np.uint32)
+    d = np.zeros(6, np.float32)
+    ok = _lib.load().cwf_pack_block_inverse(_lib.ptr(v), int(mask), _lib.ptr(w), _lib.ptr(d))
+    return bool(ok), w, d
+
+
 def dot(system: MatrixFreeSystem, a, b, partials=None) -> Expected:
     """dot_accumulate (pcg.cpp:170-207)."""
     h = system.handle()

@@ -41,12 +41,13 @@ class Case:
 
 
 def make_config(xi=0.02, w=(5.0, 50.0), tol=3e-4, max_iterations=2000, dt=0.01, gravity=(0.0, 0.0, -9.81),
-                point=(0.0, 0.0, -500.0), point_group="TIP") -> Config:
+                point=(0.0, 0.0, -500.0), point_group="TIP", dirichlet=None) -> Config:
+    fixes = dirichlet if dirichlet is not None else [DirichletFix("FIXED", (True, True, True), (0.0, 0.0, 0.0))]
     return Config(materials=[Material("steel", 30.0e9, 0.2, 2500.0)], assignments=[Assignment("SOLID", "steel")],
                   damping=Damping(xi, w[0], w[1]), time=TimeSettings(dt, False, 0.0, 0.0),
                   solver=SolverSettings("pcg", "block_jacobi", tol, 1.0e-5, max_iterations),
                   loads=Loads(tuple(gravity), [], [PointLoad(point_group, tuple(point))]),
-                  dirichlet=[DirichletFix("FIXED", (True, True, True), (0.0, 0.0, 0.0))])
+                  dirichlet=fixes)
 
 
 def block_case(nx, ny, nz, h=0.1, jitter=False, element="tet4", **cfg_kw) -> Case:
@@ -95,3 +96,23 @@ def slab_case(key: str, nranks: int, rank: int, max_iterations: int = 2000):
     c = meshgen.CONFIGS[key]
     return slab_case_shape(c["shape"], nranks, rank, h=c["h"], max_iterations=max_iterations, xi=c["xi"],
                            w=c["w"], tol=c["tol"])
+
+
+def roller_case(nx, ny, nz, h=0.1, element="tet4", **cfg_kw) -> Case:
+    """Partial Dirichlet masks (config.hpp:208 constrain_axis): rollers on three faces -- x=0 fixed in x
+    only (FIXED), y=0 in y only (SIDE), z=0 in z only (BOTTOM) -- which remove the rigid modes while most
+    constrained nodes keep two free axes (edges one, the origin none). Loads as block_case."""
+    tm = meshgen.hex_block(nx, ny, nz, h) if element == "hex8" else meshgen.kuhn_block(nx, ny, nz, h)
+    A, B = nx + 1, ny + 1
+    n = np.arange(tm.coords.shape[0], dtype=np.int64)
+    i, j, k = n % A, (n // A) % B, n // (A * B)
+    tm.node_groups["SIDE"] = n[j == 0].astype(np.uint32)
+    tm.node_groups["BOTTOM"] = n[k == 0].astype(np.uint32)
+    assert np.array_equal(tm.node_groups["FIXED"], n[i == 0].astype(np.uint32))
+    mesh = pack.from_tetmesh(tm)
+    fixes = [DirichletFix("FIXED", (True, False, False), (0.0, None, None)),
+             DirichletFix("SIDE", (False, True, False), (None, 0.0, None)),
+             DirichletFix("BOTTOM", (False, False, True), (None, None, 0.0))]
+    cfg = make_config(dirichlet=fixes, **cfg_kw)
+    tag = "hex" if element == "hex8" else "kuhn"
+    return Case(f"{tag}{nx}x{ny}x{nz}-rollers", mesh, cfg, pack.build_packed_buffers(mesh, cfg))

@@ -161,8 +161,23 @@ int cwf_hip_keff_timed(cwf_hip_system *h, const float *x_dev, float *y_dev, int 
 int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, int ptr_kind);
 
 /* cwf::gpu::pcg::build_block_jacobi_inverse (pcg.hpp:226-227, pcg.cpp:479-503):
- * inv_out[node*9 + 3*i + j], row-major f32. n = node_count * 9. */
+ * inv_out[node*9 + 3*i + j], row-major f32. n = node_count * 9. This is the reference's inverse in
+ * every mode (constrained rows = identity). A FAST solve applies a symmetrised, 16-B-packed form of
+ * it instead; cwf_hip_fast_block_inverse exports that operator. */
 int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int ptr_kind);
+
+/* The preconditioner a FAST solve actually applies (no reference counterpart): the block inverse
+ * above, symmetrised (upper triangle), restricted to the free axes (constrained rows and columns 0:
+ * z and r are 0 there) and dequantised from the update pass's 16-B record (blockinv_pack.hpp).
+ * inv_out as above (n = node_count * 9); packed_out (nullable, host) receives the 16-B records,
+ * [node_count * 4] u32; *fallback_nodes (nullable) counts the nodes whose block is applied in fp32. */
+int cwf_hip_fast_block_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int ptr_kind, uint32_t *packed_out,
+                               uint64_t *fallback_nodes);
+
+/* Host restatement of that packing for one node (the same code the device runs): v = the block's
+ * upper triangle {a00 a01 a02 a11 a12 a22}, mask bit k = axis k constrained. Writes the 16-B record
+ * (w[4]) and the applied upper triangle (d[6]); returns 1 for a packed block, 0 for an fp32 fallback. */
+int cwf_pack_block_inverse(const float *v, uint32_t mask, uint32_t *w, float *d);
 
 /* dot_accumulate (pcg.cpp:170-207): chunked fp64 dot of two f32 DOF vectors. partials may be
  * NULL; otherwise [reduction_partials] chunk partials are written (host or device by ptr_kind). */

@@ -227,6 +227,72 @@ def test_fast_mode_solve_close(case):
     assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
 
 
+def _upper_sym(inv9):
+    b = inv9.reshape(-1, 3, 3)
+    return np.stack([b[:, 0, 0], b[:, 0, 1], b[:, 0, 2], b[:, 1, 1], b[:, 1, 2], b[:, 2, 2]], 1)
+
+
+def test_fast_block_inverse_record_matches_host_packing_of_reference_inverse():
+    """The device's 16-B records are the host packing (blockinv_pack.hpp) of the reference inverse
+    (oracle, symmetrised: upper triangle), word for word; the exported applied operator is their decode."""
+    case = scenarios.roller_case(9, 5, 4, tol=1e-6, max_iterations=800)
+    P = case.packing
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    applied = np.zeros(9 * P.node_count, np.float32)
+    packed = np.zeros(4 * P.node_count, np.uint32)
+    nfall = pcg.fast_block_inverse(s, applied, packed).value()
+    ref = oracle_system(P, case.materials, *case.scalars()).block_jacobi()
+    up = _upper_sym(ref)
+    want_w = np.zeros_like(packed)
+    want_d = np.zeros((P.node_count, 6), np.float32)
+    fb = 0
+    for n in range(P.node_count):
+        ok, w, d = pcg.pack_block_inverse(up[n], int(P.bc_mask[n]))
+        want_w[4 * n:4 * n + 4] = w
+        want_d[n] = d
+        fb += not ok
+    assert nfall == fb == 0
+    assert_bitwise(packed, want_w, "16-B records")
+    assert_bitwise(_upper_sym(applied), want_d, "applied inverse")
+    a = applied.reshape(-1, 3, 3)
+    assert np.array_equal(a, np.transpose(a, (0, 2, 1)))  # symmetric
+    # the reference-semantics export is unchanged in FAST mode
+    inv = np.zeros_like(applied)
+    pcg.build_block_jacobi_inverse(s, None, inv).value()
+    assert_bitwise(inv, ref, "reference inverse (FAST handle)")
+
+
+@pytest.mark.parametrize("shape", [(9, 5, 4), (16, 6, 6)])
+def test_fast_solve_with_partial_masks(shape):
+    """Rollers on three faces (most constrained nodes keep free axes) in physical units (E = 30 GPa):
+    FAST converges like the oracle. The old single-scale fp16 packing flushed these nodes' free entries
+    (~1e-10) to zero and stalled at max_iterations."""
+    case = scenarios.roller_case(*shape, tol=1e-6, max_iterations=2000)
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(2000, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, 2000, 1e-6)
+    assert t.converged and ref["telemetry"].converged
+    assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+
+
+def test_fast_stepper_with_partial_masks():
+    case = scenarios.roller_case(12, 4, 4, tol=1e-6, max_iterations=1500)
+    P = case.packing
+    ref = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_PARITY)
+    fast = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST)
+    for k in range(3):
+        tr = ref.step(0.01 * k).value()
+        tf = fast.step(0.01 * k).value()
+        assert tf.pcg.converged and tr.pcg.converged
+        assert abs(tf.pcg.iterations - tr.pcg.iterations) <= max(3, tr.pcg.iterations // 10)
+    ur, uf = ref.get_state(Stepper.DISPLACEMENT), fast.get_state(Stepper.DISPLACEMENT)
+    assert np.linalg.norm(uf - ur) <= 1e-4 * np.linalg.norm(ur)
+
+
 def test_cpp_mirror_single_tet_reference_outputs(tmp_path):
     """tests/cpp/pcg_api_test.cpp: the reference's single-tet fixture through include/cwf_hip.hpp."""
     import subprocess

@@ -187,7 +187,14 @@ def test_gpu_hex8_block_jacobi_matches_oracle(hcase):
         ref[c, k, :] = 0.0
         ref[c, k, k] = 1.0
     got = inv.reshape(-1, 3, 3).astype(np.float64)
-    assert np.max(np.abs(got - ref)) <= 1e-5 * np.max(np.abs(ref))
+    # constrained rows are identity (1.0) while free entries are ~1/K ~ 1e-10: compare each entry against
+    # its own row/column scale sqrt(B_ii B_jj) of the fp64 block, so the free entries are really checked
+    free = ((P.bc_mask[:, None] >> np.arange(3)[None]) & 1) == 0
+    d = np.abs(np.einsum("nii->ni", ref))
+    scale = np.sqrt(d[:, :, None] * d[:, None, :])
+    rows = np.repeat(free[:, :, None], 3, 2)
+    assert np.all(np.abs(got - ref)[rows] <= 1e-5 * scale[rows])
+    assert np.array_equal(got[~free], ref[~free])  # identity rows
 
 
 @pytest.mark.gpu
@@ -203,6 +210,25 @@ def test_gpu_hex8_pcg_solution_satisfies_oracle_operator(hcase):
                          P.bc_mask, rhs)
     # |r| <= 1e-6 |rhs| in the device's fp32 operator; against the fp64 solution (fp64 PCG to 1e-11)
     # the solutions agree to 1e-4 relative (fp32 operator rounding x the problem's conditioning)
+    assert np.linalg.norm(x - ref) <= 1e-4 * np.linalg.norm(ref)
+
+
+@pytest.mark.gpu
+def test_gpu_hex8_pcg_with_partial_masks():
+    """rollers on three faces (partial masks, physical units): the packed FAST preconditioner keeps the
+    free entries of the partly constrained nodes, so the solve converges to the fp64 solution"""
+    case = scenarios.roller_case(10, 5, 5, element="hex8", tol=1e-6, max_iterations=2000)
+    s = gpu_hex_system(case)
+    P = case.packing
+    sK, sM = case.scalars()
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(2000, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    assert t.converged and t.iterations < 1000
+    applied = np.zeros(9 * P.node_count, np.float32)
+    assert pcg.fast_block_inverse(s, applied).value() == 0  # no fp32 fallback block
+    ref = O.hex8_solve64(case.mesh.coords, case.mesh.tets, P.material_index, D_STEEL, sK, sM, P.lumped_mass,
+                         P.bc_mask, rhs)
     assert np.linalg.norm(x - ref) <= 1e-4 * np.linalg.norm(ref)
 
 
