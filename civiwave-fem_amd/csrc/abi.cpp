@@ -1024,13 +1024,13 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
     if (h->mode == CWF_MODE_FAST && s.t.ntiles)
     {
         // per tile: 16-B header; per tet: corner ids (8 B GEO, 48-B records otherwise) + 4 u16 local-CSR
-        // entries or (PUSH) positions (+ material id when M > 1); per tile node: {node, csr range} 8 B, coordinates 12 B (GEO),
-        // partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B + the new p written by its
-        // owner slot (12 B, PCG mode: the launches bench.py times)
+        // entries or (PUSH) positions (+ material id when M > 1); per tile node: {node, csr range} 8 B, coordinates 12 B (GEO), the node-major slot 4 B
+        // (pipelined / hex), partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B + the new
+        // p written by its owner slot (12 B, PCG mode: the launches bench.py times)
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
-        const uint64_t rec = s.t.hex ? 24 : s.t.geo ? 8 : 48;
-        *layout_bytes = 16ull * s.t.ntiles + E * (rec + 8 + (s.t.mat ? 4 : 0)) + T * (8 + (s.t.geo ? 12 : 0) + 12) +
-                        N * (24 + 4 + 12);
+        const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
+        *layout_bytes = 16ull * s.t.ntiles + E * (rec + (s.t.mat ? 4 : 0)) +
+                        T * (8 + (s.t.geo ? 12 : 0) + (s.t.node_major ? 4 : 0) + 12) + N * (24 + 4 + 12);
     }
     else  // PARITY node gather: 64-B element records + vol + CSR incidences, per node x in / y out + mass + mask
         *layout_bytes = E * (64 + 4 + 16 + (s.M > 1 ? 4 : 0)) + N * (4 + 12 + 12 + 4 + 4);

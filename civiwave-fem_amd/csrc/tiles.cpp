@@ -1,8 +1,10 @@
 // tiles.cpp -- host-side build of the FAST-mode element tiles.
 //
 // The fast K_eff is element-centric: one workgroup per tile of <= kTileElems consecutive
-// elements (Morton order of the element centroids when node coordinates are given, so a tile is
-// a compact 3-D block). Per tile the host precomputes
+// elements. With node coordinates, tet tiles are the leaves of a recursive coordinate bisection of
+// the element centroids (cuts at the widest centroid gap near the balanced count, so they run between
+// element layers), each leaf in Morton order inside; hex tiles are segments of the Morton curve. Per
+// tile the host precomputes
 //   * the tile's distinct nodes (sorted global ids) -> the workgroup gathers their p into LDS,
 //   * every element's 4 corners as u16 indices into that node list,
 //   * a local CSR  tile-node -> (element_local * 4 + corner), ascending element, so the LDS fold of
@@ -14,8 +16,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "cwf_internal.hpp"
@@ -34,6 +38,75 @@ inline uint64_t spread21(uint64_t v)
     v = (v | v << 2) & 0x1249249249249249ull;
     return v;
 }
+
+// Recursive coordinate bisection of the elements into leaves of at most max_elems (target ~7/8 of it).
+// Each range is cut along the longest axis of its centroid box near the count n * L1 / L (L leaves,
+// L1 = L / 2), at the widest gap between consecutive centroid coordinates within +-n/16 of that count.
+// A cut through such a gap runs between element layers instead of through them, so the two sides share
+// one node layer rather than the nodes of a whole sliced layer: for a Kuhn block the tile halo (T / N)
+// drops from ~2.5 (Morton-curve segments) to ~1.8. The leaves come out in k-d-tree order, so consecutive
+// tiles are neighbours. c: centroids [3E]; lo/hi: per-element min/max node coordinate [3E] (extent);
+// leaf_end receives each leaf's end in `order`.
+void rcb(const std::vector<double> &c, const double ext[3], std::vector<uint32_t> &order, uint64_t b, uint64_t e,
+         uint64_t max_elems, std::vector<uint64_t> &leaf_end)
+{
+    const uint64_t n = e - b;
+    if (n <= max_elems)
+    {
+        if (n)
+            leaf_end.push_back(e);
+        return;
+    }
+    const uint64_t target = std::max<uint64_t>(1, max_elems - max_elems / 16);
+    const uint64_t Lr = std::max<uint64_t>((n + target - 1) / target, 2);
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (uint64_t i = b; i < e; ++i)
+        for (int k = 0; k < 3; ++k)
+        {
+            lo[k] = std::min(lo[k], c[3ull * order[i] + k]);
+            hi[k] = std::max(hi[k], c[3ull * order[i] + k]);
+        }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (hi[k] - lo[k] > hi[ax] - lo[ax])
+            ax = k;
+    const auto less = [&](uint32_t x, uint32_t y) {
+        const double cx = c[3ull * x + ax], cy = c[3ull * y + ax];
+        return cx < cy || (cx == cy && x < y);  // ties by element id: deterministic
+    };
+    const uint64_t L1 = Lr / 2;
+    const uint64_t m = b + (n * L1 + Lr / 2) / Lr;
+    const uint64_t w = n / 16;
+    uint64_t cut = m;
+    std::nth_element(order.begin() + b, order.begin() + m, order.begin() + e, less);
+    if (w >= 2)
+    {
+        // candidates: the elements whose centroid lies within 1.5 mean element extents of the median's,
+        // sorted; everything before that band is <, after it > (two partitions, O(n))
+        const double vm = c[3ull * order[m] + ax], dl = 1.5 * ext[ax];
+        const auto mid = std::partition(order.begin() + b, order.begin() + e,
+                                        [&](uint32_t x) { return c[3ull * x + ax] < vm - dl; });
+        const auto top = std::partition(mid, order.begin() + e, [&](uint32_t x) { return c[3ull * x + ax] <= vm + dl; });
+        std::sort(mid, top, less);
+        const uint64_t wb = std::max<uint64_t>((uint64_t)(mid - order.begin()), m - w);
+        const uint64_t we = std::min<uint64_t>((uint64_t)(top - order.begin()), m + w + 1);
+        double best = -1.0;
+        cut = std::min(std::max(m, wb), we > wb ? we - 1 : wb);
+        for (uint64_t i = wb + 1; i < we; ++i)
+        {
+            const double gap = c[3ull * order[i] + ax] - c[3ull * order[i - 1] + ax];
+            const uint64_t dist = i > m ? i - m : m - i, bdist = cut > m ? cut - m : m - cut;
+            if (gap > best * (1.0 + 1e-9) || (gap >= best * (1.0 - 1e-9) && dist < bdist))
+            {
+                best = gap;
+                cut = i;
+            }
+        }
+    }
+    cut = std::min(std::max(cut, b + 1), e - 1);  // both sides non-empty (n > max_elems >= 1)
+    rcb(c, ext, order, b, cut, max_elems, leaf_end);
+    rcb(c, ext, order, cut, e, max_elems, leaf_end);
+}
 }  // namespace
 
 int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems, int corners)
@@ -42,6 +115,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
     const int K = corners == 8 ? 8 : 4;  // tet4 or hex8 (slots 0..K-1 of the 8-slot connectivity)
     std::vector<uint32_t> order(E);
     std::iota(order.begin(), order.end(), 0u);
+    std::vector<uint64_t> leaf_end;  // RCB leaf boundaries in `order` (empty: one run, greedy cuts only)
     if (d->node_coords && E)
     {
         double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
@@ -68,6 +142,43 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
             key[e] = spread21(q[0]) | spread21(q[1]) << 1 | spread21(q[2]) << 2;
         }
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+        static const int tile_order = [] {  // CWF_TILE_ORDER=morton|rcb (diagnostic; default by element)
+            const char *v = getenv("CWF_TILE_ORDER");
+            return !v ? -1 : std::string(v) == "morton" ? 0 : 1;
+        }();
+        // tets: RCB leaves (C3 tiles kernel 223 -> 200 us, same-box A/B); hex8: Morton segments, whose
+        // 128-hex tiles are already compact octant blocks (RCB measured 4% slower there)
+        if (tile_order == 1 || (tile_order == -1 && K == 4))
+        {
+            // tiles = RCB leaves (each kept in Morton order inside); the greedy pass below still splits
+            // a leaf whose node list exceeds max_nodes
+            std::vector<double> cen(3 * E);
+            double ext[3] = {0.0, 0.0, 0.0};  // mean element extent per axis
+            for (uint64_t e = 0; e < E; ++e)
+                for (int k = 0; k < 3; ++k)
+                {
+                    double v = 0.0, mn = 1e300, mx = -1e300;
+                    for (int a = 0; a < K; ++a)
+                    {
+                        const double x = d->node_coords[3 * (uint64_t)d->element_connectivity[e * 8 + a] + k];
+                        v += x;
+                        mn = std::min(mn, x);
+                        mx = std::max(mx, x);
+                    }
+                    cen[3 * e + k] = v / K;
+                    ext[k] += mx - mn;
+                }
+            for (int k = 0; k < 3; ++k)
+                ext[k] /= (double)E;
+            rcb(cen, ext, order, 0, E, max_elems, leaf_end);
+            uint64_t b = 0;
+            for (const uint64_t le : leaf_end)
+            {
+                std::stable_sort(order.begin() + b, order.begin() + le,
+                                 [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+                b = le;
+            }
+        }
     }
 
     out = HostTiles{};
@@ -94,12 +205,17 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
     std::vector<uint32_t> cnt;
     uint64_t e = 0;
     uint32_t tile = 0;
+    size_t leaf = 0;
     while (e < E)
     {
-        // greedy: up to kTileElems elements while the tile's node list fits kMaxTileNodes
+        // greedy: up to kTileElems elements of the current RCB leaf while the tile's node list fits
+        // kMaxTileNodes
         nodes.clear();
         const uint64_t e0 = e;
-        while (e < E && e - e0 < (uint64_t)max_elems)
+        while (leaf < leaf_end.size() && leaf_end[leaf] <= e0)
+            ++leaf;
+        const uint64_t stop = leaf < leaf_end.size() ? leaf_end[leaf] : E;
+        while (e < stop && e - e0 < (uint64_t)max_elems)
         {
             const uint32_t src = order[e];
             uint32_t add = 0;
