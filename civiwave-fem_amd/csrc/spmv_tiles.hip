@@ -44,6 +44,34 @@ __device__ __forceinline__ double wave_sum(double v)
     return v;
 }
 
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+
+// buffer descriptor over a whole allocation (base pointer wave-uniform: a kernel argument)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t whole_rsrc(const void *base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, -1, 0x00020000);
+}
+
+// 12-B store at float index 3 q; wt: write-through (sc1), so the line leaves L2 during the kernel instead of
+// in the end-of-kernel write-back the next launch waits for (the update pass's x / r / z: C2 +2.7% PCG it/s,
+// C3 neutral, same-box A/B; the tiles kernel's scattered partial / p stores measured 5% slower that way)
+__device__ __forceinline__ void store3(float *base, __amdgpu_buffer_rsrc_t rs, uint64_t q, float a, float b, float c,
+                                       bool wt)
+{
+    if (wt)
+    {
+        const u32x3 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c)};
+        __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 16);
+    }
+    else
+    {
+        float *o = base + 3ull * q;
+        o[0] = a;
+        o[1] = b;
+        o[2] = c;
+    }
+}
+
 // NT-thread block sum in a fixed order; result valid in every thread. red: NT/64 doubles.
 template <int NT> __device__ __forceinline__ double block_sum(double v, double *red)
 {
@@ -975,7 +1003,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold, float *__restrict__ pnew,
     Ctl *__restrict__ ctl,
     const double *__restrict__ part_dot, unsigned ntp, double *__restrict__ prr, double *__restrict__ prz,
-    unsigned it)
+    unsigned it, int wt)
 {
     __shared__ double red[kUpdThreads / 64];
     if (!ctl->active)
@@ -1081,7 +1109,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
                 a2 += pp[2];
             }
         const float av[3] = {a0, a1, a2};
-        float rv[3];
+        float rv[3], xs[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
@@ -1095,10 +1123,11 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
                 xn = rhs[d];
                 rw = 0.0f;
             }
-            x[d] = xn;
-            r[d] = rw;
+            xs[k] = xn;
             rv[k] = rw;
         }
+        store3(x, whole_rsrc(x), n, xs[0], xs[1], xs[2], wt);
+        store3(r, whole_rsrc(r), n, rv[0], rv[1], rv[2], wt);
         // symmetric block inverse {a00 a01 a02 a11 a12 a22} from the 16-B Jacobi-scaled record
         // (blockinv_pack.hpp); a flagged block (negative scale) reads its fp32 copy instead
         float bv[6];
@@ -1116,15 +1145,17 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         }
         const float b00 = bv[0], b01 = bv[1], b02 = bv[2], b11 = bv[3], b12 = bv[4], b22 = bv[5];
         const float iv[9] = {b00, b01, b02, b01, b11, b12, b02, b12, b22};
+        float zs[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
             float zk = fmaf(iv[3 * k + 2], rv[2], fmaf(iv[3 * k + 1], rv[1], iv[3 * k] * rv[0]));
             zk = (mk & (1u << k)) ? 0.0f : zk;
-            z[3u * n + k] = zk;
+            zs[k] = zk;
             rr += (double)rv[k] * (double)rv[k];
             rz += (double)rv[k] * (double)zk;
         }
+        store3(z, whole_rsrc(z), n, zs[0], zs[1], zs[2], wt);
     }
     const double t0 = block_sum<kUpdThreads>(rr, red);
     const double t1 = block_sum<kUpdThreads>(rz, red);
@@ -1284,6 +1315,16 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
 inline float *fast_p_old(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p2 : h->p; }
 inline float *fast_p_new(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p : h->p2; }
 
+// CWF_WT=0 (diagnostic): plain x / r / z stores in the update pass instead of write-through
+static bool update_write_through()
+{
+    static const bool v = [] {
+        const char *e = getenv("CWF_WT");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
@@ -1314,7 +1355,7 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
     k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
         direct ? h->part0 : h->g_pap,
-        direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it);
+        direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it, update_write_through());
 }
 
 // diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
