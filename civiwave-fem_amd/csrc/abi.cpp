@@ -67,6 +67,9 @@ template <class T> int dalloc(cwf_hip_system *h, T **p, size_t count)
     return 0;
 }
 
+// the Dirichlet mask can ride in node_part_off's top bits when the offsets leave them free
+inline bool ht_off_mask_ok(const std::vector<uint32_t> &npo) { return npo.back() <= cwf::kPartOffBits; }
+
 template <class T> int upload(cwf_hip_system *h, T **dst, const T *src, size_t count)
 {
     if (int st = dalloc(h, dst, count))
@@ -645,6 +648,94 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             const char *pp = getenv("CWF_TILE_PIPE");  // diagnostic: 0 = the one-tile-per-workgroup kernel
             t.pipe = t.geo && !(pp && pp[0] == '0') ? 1 : 0;
         }
+        // fan groups (groups.cpp, k_keff_groups_pipe): the default FAST tet path when the mesh groups into
+        // fans of >= 3 tets on average (CWF_GROUPS=0: the per-tet tiles below)
+        bool grouped = false;
+        {
+            const char *gv = getenv("CWF_GROUPS");
+            if (!hex && t.pipe && !(gv && gv[0] == '0'))
+            {
+                GroupTiles gt;
+                int gst = -1;
+                try
+                {
+                    gst = build_group_tiles(d, gt, kGroupThreads, kGroupMaxNodes, kGroupSlots);
+                }
+                catch (const std::bad_alloc &)
+                {
+                    return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
+                }
+                if (getenv("CWF_VERBOSE"))
+                    fprintf(stderr, "[cwf] fan groups: status %d, %u groups (%.2f tets each), %u tiles, %zu tile nodes "
+                                    "(%.3f per node), max %u nodes / %u slots per tile\n",
+                            gst, gt.ngroups, gt.tets_per_group, gt.ntiles, gt.tile_nodes.size(),
+                            N ? (double)gt.tile_nodes.size() / (double)N : 0.0, gt.max_tile_nodes, gt.max_tile_slots);
+                if (gst == 0 && gt.tets_per_group >= 3.0)
+                {
+                    const size_t T = gt.tile_nodes.size();
+                    std::vector<uint2> tnode(T);
+                    for (size_t q = 0; q < T; ++q)
+                        tnode[q] = uint2{gt.tile_nodes[q], gt.run[q]};
+                    if (ht_off_mask_ok(gt.node_part_off))
+                    {
+                        for (uint64_t n = 0; n < N; ++n)
+                            gt.node_part_off[n] |= (d->bc_mask[n] & 7u) << 29;
+                        t.off_mask = 1;
+                    }
+                    uint4 *ga, *gb, *dh;
+                    uint2 *dtn;
+                    uint32_t *npo, *tsl;
+                    float *tc, *part;
+                    if (int st = upload(h, &ga, gt.grecA.data(), gt.grecA.size()))
+                        return bail(st);
+                    if (int st = upload(h, &gb, gt.grecB.data(), gt.grecB.size()))
+                        return bail(st);
+                    if (!gt.gmat.empty())
+                    {
+                        uint32_t *gm;
+                        if (int st = upload(h, &gm, gt.gmat.data(), gt.gmat.size()))
+                            return bail(st);
+                        t.mat = gm;
+                    }
+                    if (int st = upload(h, &dh, gt.hdr.data(), gt.hdr.size()))
+                        return bail(st);
+                    if (int st = upload(h, &dtn, tnode.data(), T))
+                        return bail(st);
+                    if (int st = upload(h, &npo, gt.node_part_off.data(), gt.node_part_off.size()))
+                        return bail(st);
+                    if (int st = upload(h, &tsl, gt.tile_slot.data(), T))
+                        return bail(st);
+                    if (int st = dalloc(h, &tc, 3 * T))
+                        return bail(st);
+                    for (int q = 0; q < 3; ++q)
+                        HIPTRY(h, hipMemcpy(tc + q * T, gt.tcoord[q].data(), T * sizeof(float), hipMemcpyHostToDevice));
+                    if (int st = dalloc(h, &part, 3 * (T + 2)))  // + 2 padding slots (update pass)
+                        return bail(st);
+                    t.grp = 1;
+                    t.grecA = ga;
+                    t.grecB = gb;
+                    t.hdr = dh;
+                    t.tnode = dtn;
+                    t.tslot = tsl;
+                    t.tcoord = tc;
+                    t.node_part_off = npo;
+                    t.part = part;
+                    t.node_major = 1;
+                    t.push = 1;
+                    t.pipe = 1;
+                    t.pipe_nt = (int)kGroupThreads;
+                    t.ntiles = gt.ntiles;
+                    t.ngroups = gt.ngroups;
+                    t.max_tile_nodes = gt.max_tile_nodes;
+                    t.total_tile_nodes = (uint32_t)T;
+                    t.E = (uint32_t)E;
+                    t.pipe_grid = fast_pipe_grid(s);
+                    grouped = true;
+                }
+            }
+        }
+        if (!grouped)
+        {
         try
         {
             // pipelined tiles: 256-thread workgroups over 512-element tiles, or 128 over 256 (CWF_PIPE_NT, or
@@ -820,6 +911,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.part = part;
         if (t.pipe || t.hex)
             t.pipe_grid = fast_pipe_grid(s);
+        }  // !grouped
     }
     if (hex)  // the hex block-Jacobi setup integrates from the global corners (fp64)
     {
@@ -1028,7 +1120,14 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // (pipelined / hex), partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B + the new
         // p written by its owner slot (12 B, PCG mode: the launches bench.py times)
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
+        // fan groups: 32-B group record (+ material id when M > 1) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
+        if (s.t.grp)
+        {
+            *layout_bytes = 16ull * s.t.ntiles + (uint64_t)s.t.ngroups * (32 + (s.t.mat ? 4 : 0)) +
+                            T * (8 + 12 + 4 + 12) + N * (24 + 4 + 12);
+            return 0;
+        }
         *layout_bytes = 16ull * s.t.ntiles + E * (rec + (s.t.mat ? 4 : 0)) +
                         T * (8 + (s.t.geo ? 12 : 0) + (s.t.node_major ? 4 : 0) + 12) + N * (24 + 4 + 12);
     }

@@ -25,6 +25,9 @@ namespace cwf
 constexpr int kTileElems = 512;      // elements per tile (= per 256-thread workgroup)
 constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two node slots per thread)
 constexpr uint32_t kHexTileThreads = 128;  // hex8 tiles: <= 128 hexes and <= 256 nodes per 128-lane workgroup
+constexpr uint32_t kGroupThreads = 128;    // fan-group tiles: <= 128 groups (one per lane) ...
+constexpr uint32_t kGroupMaxNodes = 256;   // ... <= 256 nodes (two per lane; u8 local ids) ...
+constexpr uint32_t kGroupSlots = 1536;     // ... and <= 1536 pushed-force slots (padded runs, LDS)
 
 struct DevTiles
 {
@@ -48,6 +51,11 @@ struct DevTiles
                                               // (csr range relative to the tile's first entry 4*e0)
     const uint16_t *csr_ent = nullptr;        // [4E] element_local*4 + corner
     const uint2 *epos = nullptr;              // [E] (PUSH) each corner's position in the tile's local CSR
+    // tet fan groups (groups.cpp): k_keff_groups_pipe, one group per lane, pushes per group node
+    int grp = 0;
+    uint32_t ngroups = 0;
+    const uint4 *grecA = nullptr;  // [G] {8 x u8 local node ids (a b r0 .. r5), tet count, 0}
+    const uint4 *grecB = nullptr;  // [G] 8 x u16 push positions
     // native hex8: k_keff_hex_tiles, 128-thread persistent grid (pipe_grid), push fold
     int hex = 0;
     int hex_all_affine = 0;        // every hex tile is a parallelepiped tile (affine-only kernel variant)
@@ -86,6 +94,33 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes = k
 // true when the supplied gradients / volumes are those of the supplied node coordinates (so FAST may
 // recompute them on the fly instead of streaming them)
 bool geometry_matches(const cwf_system_desc *d);
+uint64_t spread21(uint64_t v);  // 21-bit Morton spread (one axis of a 63-bit key)
+// recursive coordinate bisection of order's items (centroids c[3 id], mean extents ext) into leaves of at most
+// max_elems, cut between layers (tiles.cpp); leaf_end receives each leaf's end in `order`
+void rcb_partition(const std::vector<double> &c, const double ext[3], std::vector<uint32_t> &order,
+                   uint64_t max_elems, std::vector<uint64_t> &leaf_end);
+
+// FAST tet "fan groups" (groups.cpp): tets grouped around a shared edge (a, b) -- a closed or open fan of
+// up to 6 tets {a, b, r_i, r_{(i+1) mod 6}} -- so one lane computes a group with its <= 8 nodes in
+// registers and pushes one force per node instead of one per (tet, corner). A Kuhn-split hex is one
+// closed 6-tet fan around its diagonal.
+struct GroupTiles
+{
+    uint32_t ntiles = 0, ngroups = 0, max_tile_nodes = 0, max_tile_slots = 0;
+    double tets_per_group = 0.0;
+    std::vector<uint4> grecA;  // [G] {a b r0 r1 (u8 local ids), r2 r3 r4 r5, tet count f, 0}
+    std::vector<uint4> grecB;  // [G] u16 push positions of slots a b r0 .. r5 (tile-relative, padded runs)
+    std::vector<uint32_t> gmat;            // [G] material (when M > 1; groups are single-material)
+    std::vector<uint4> hdr;                // [ntiles] {first group, #groups, first tile node, #nodes}
+    std::vector<uint32_t> tile_nodes;      // [T] global node | owner bit 31
+    std::vector<uint32_t> run;             // [T] padded run begin | end << 16
+    std::vector<float> tcoord[3];          // [T] tile-relative coordinates
+    std::vector<uint32_t> node_part_off, tile_slot;  // [N+1] node -> slot range; [T] node-major slot
+    std::vector<uint32_t> tet_group;       // [E] group of each tet (validation)
+};
+// nt: lanes per workgroup (one group per lane); max_nodes <= 256 (u8 local ids); slot_budget: LDS push slots
+int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
+                      uint32_t slot_budget);
 
 constexpr uint32_t kPartOffBits = 0x1fffffffu;  // node_part_off value bits (the rest: bc_mask, off_mask)
 

@@ -1,0 +1,408 @@
+// groups.cpp -- host build of the FAST-mode tet fan groups and their tiles (GroupTiles, cwf_internal.hpp).
+//
+// The reference's operator is a loop over tets that scatters 12 forces per tet (pcg.cpp:561-662). The
+// tiles kernel of round 1 pushes those 12 forces through LDS one (tet, corner) at a time and reads every
+// corner's coordinates and value from LDS, so LDS traffic, not HBM, bounds it on small meshes. A fan group
+// gathers the tets around one edge (a, b): tet i = {a, b, r_i, r_{(i+1) mod 6}}, i < f <= 6, so a lane
+// holds the group's <= 8 nodes in registers, computes its f tets with static register indices, sums the
+// forces per node and pushes one force per node. A Kuhn-split hex is one closed 6-tet fan around its
+// diagonal (8 nodes for 24 corners); an unstructured mesh forms fans around its edges (~5 tets each).
+// The element math per tet is unchanged (fp32, corner order free: the gradients and |det| are intrinsic).
+//
+// Grouping: tets in Morton order of their centroids; an unassigned tet seeds a group on the edge whose
+// fan of unassigned, same-material tets (walked both ways around the edge from the seed) is longest
+// (closed fans preferred); a closed fan of f < 6 tets repeats r_0 in slot f, an open fan holds <= 5 tets.
+// Tiles: recursive coordinate bisection of the group centroids (rcb_partition) into <= nt groups, split
+// further while a tile's node list exceeds max_nodes; the local CSR of pushed forces is ordered by
+// (node, group), the fold order, and every run is padded as for the tet tiles (abi.cpp).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "cwf_internal.hpp"
+
+namespace cwf
+{
+namespace
+{
+struct Fan
+{
+    uint32_t a = 0, b = 0;
+    uint32_t r[7] = {};  // ring nodes in walk order
+    int nr = 0;
+    uint32_t t[6] = {};  // tets in fan order: t[i] = {a, b, r[i], r[i + 1]} (closed: r[f] == r[0])
+    int f = 0;
+    bool closed = false;
+};
+
+// the two nodes of tet `t` other than u, v
+inline void others(const uint32_t *c, uint32_t u, uint32_t v, uint32_t &p, uint32_t &q)
+{
+    uint32_t o[2];
+    int k = 0;
+    for (int i = 0; i < 4; ++i)
+        if (c[i] != u && c[i] != v && k < 2)
+            o[k++] = c[i];
+    p = o[0];
+    q = k > 1 ? o[1] : o[0];
+}
+
+// longest fan of unassigned same-material tets around edge (u, v) through seed tet t
+Fan walk_fan(const uint32_t *conn, const std::vector<uint32_t> &off, const std::vector<uint32_t> &lst,
+             const std::vector<uint32_t> &group, const uint32_t *mat, uint32_t t, uint32_t u, uint32_t v,
+             std::vector<uint32_t> &star)
+{
+    // star = tets of u that also contain v, unassigned, same material as t (both lists ascending)
+    star.clear();
+    for (uint32_t i = off[u], j = off[v]; i < off[u + 1] && j < off[v + 1];)
+    {
+        if (lst[i] < lst[j])
+            ++i;
+        else if (lst[i] > lst[j])
+            ++j;
+        else
+        {
+            const uint32_t s = lst[i];
+            if (group[s] == ~0u && (!mat || mat[s] == mat[t]))
+                star.push_back(s);
+            ++i;
+            ++j;
+        }
+    }
+    Fan F;
+    F.a = u;
+    F.b = v;
+    uint32_t p, q;
+    others(conn + 8ull * t, u, v, p, q);
+    uint32_t R[13];
+    uint32_t TT[12];
+    int head = 6, tail = 7;  // R[head..tail], TT[head..tail-1]
+    R[6] = p;
+    R[7] = q;
+    TT[6] = t;
+    std::vector<char> used(star.size(), 0);
+    for (size_t k = 0; k < star.size(); ++k)
+        used[k] = star[k] == t;
+    const auto next = [&](uint32_t from, uint32_t &to, uint32_t &tet) -> bool {
+        for (size_t k = 0; k < star.size(); ++k)
+            if (!used[k])
+            {
+                uint32_t x, y;
+                others(conn + 8ull * star[k], u, v, x, y);
+                if (x == from || y == from)
+                {
+                    used[k] = 1;
+                    to = x == from ? y : x;
+                    tet = star[k];
+                    return true;
+                }
+            }
+        return false;
+    };
+    bool closed = false;
+    // forward from q
+    while (tail - head < 6)
+    {
+        uint32_t to, tet;
+        if (!next(R[tail], to, tet))
+            break;
+        if (to == R[head])  // back at the start: the ring closes
+        {
+            TT[tail] = tet;
+            closed = true;
+            break;
+        }
+        if (tail - head == 5)  // an open fan holds <= 5 tets (<= 6 ring slots); leave this one
+        {
+            break;
+        }
+        ++tail;
+        R[tail] = to;
+        TT[tail - 1] = tet;
+    }
+    if (!closed)
+        while (tail - head < 5)  // backward from p
+        {
+            uint32_t to, tet;
+            if (!next(R[head], to, tet))
+                break;
+            if (to == R[tail])
+                break;  // closing from this side would need the forward tet already tried
+            --head;
+            R[head] = to;
+            TT[head] = tet;
+        }
+    F.closed = closed;
+    F.nr = tail - head + 1;
+    for (int i = 0; i < F.nr; ++i)
+        F.r[i] = R[head + i];
+    F.f = closed ? F.nr : F.nr - 1;
+    for (int i = 0; i < F.f; ++i)
+        F.t[i] = TT[head + i];
+    return F;
+}
+}  // namespace
+
+int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
+                      uint32_t slot_budget)
+{
+    out = GroupTiles{};
+    const uint64_t N = d->node_count, E = d->element_count;
+    const uint32_t *conn = d->element_connectivity;
+    const uint32_t *mat = d->material_count > 1 ? d->element_material_index : nullptr;
+    if (!d->node_coords || !E || max_nodes > 256)
+        return -1;
+    // node -> tets, ascending tet
+    std::vector<uint32_t> off(N + 1, 0), lst(4 * E);
+    for (uint64_t e = 0; e < E; ++e)
+        for (int a = 0; a < 4; ++a)
+            ++off[conn[8 * e + a] + 1];
+    for (uint64_t n = 0; n < N; ++n)
+        off[n + 1] += off[n];
+    {
+        std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+        for (uint64_t e = 0; e < E; ++e)
+            for (int a = 0; a < 4; ++a)
+                lst[cur[conn[8 * e + a]]++] = (uint32_t)e;
+    }
+    // seed order: Morton order of the tet centroids
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    for (uint64_t n = 0; n < N; ++n)
+        for (int k = 0; k < 3; ++k)
+        {
+            lo[k] = std::min(lo[k], d->node_coords[3 * n + k]);
+            hi[k] = std::max(hi[k], d->node_coords[3 * n + k]);
+        }
+    double ext = 0.0;
+    for (int k = 0; k < 3; ++k)
+        ext = std::max(ext, hi[k] - lo[k]);
+    const double scale = ext > 0 ? (double)((1u << 21) - 1) / ext : 0.0;
+    std::vector<uint64_t> key(E);
+    for (uint64_t e = 0; e < E; ++e)
+    {
+        uint64_t q[3];
+        for (int k = 0; k < 3; ++k)
+        {
+            double c = 0.0;
+            for (int a = 0; a < 4; ++a)
+                c += d->node_coords[3ull * conn[8 * e + a] + k];
+            q[k] = (uint64_t)std::llround((c / 4.0 - lo[k]) * scale);
+        }
+        key[e] = spread21(q[0]) | spread21(q[1]) << 1 | spread21(q[2]) << 2;
+    }
+    std::vector<uint32_t> seed(E);
+    std::iota(seed.begin(), seed.end(), 0u);
+    std::stable_sort(seed.begin(), seed.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
+    key.clear();
+    key.shrink_to_fit();
+
+    // fans
+    std::vector<uint32_t> group(E, ~0u);
+    std::vector<Fan> fans;
+    fans.reserve(E / 4 + 1);
+    std::vector<uint32_t> star;
+    static const int EDGES[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
+    for (const uint32_t t : seed)
+    {
+        if (group[t] != ~0u)
+            continue;
+        const uint32_t *c = conn + 8ull * t;
+        Fan best;
+        for (int q = 0; q < 6; ++q)
+        {
+            const Fan F = walk_fan(conn, off, lst, group, mat, t, c[EDGES[q][0]], c[EDGES[q][1]], star);
+            if (F.f > best.f || (F.f == best.f && F.closed && !best.closed))
+                best = F;
+        }
+        const uint32_t g = (uint32_t)fans.size();
+        for (int i = 0; i < best.f; ++i)
+            group[best.t[i]] = g;
+        fans.push_back(best);
+    }
+    const uint64_t G = fans.size();
+    out.ngroups = (uint32_t)G;
+    out.tets_per_group = (double)E / (double)G;
+    // slots of a group: 0 = a, 1 = b, 2 + i = ring node i (closed f < 6: ring slot f repeats r_0);
+    // used: a, b and ring slots 0 .. min(f + 1, 6) - 1
+    const auto slot_node = [&](const Fan &F, int s) -> uint32_t {
+        if (s == 0)
+            return F.a;
+        if (s == 1)
+            return F.b;
+        const int i = s - 2;
+        if (i < F.nr)
+            return F.r[i];
+        return F.closed && i == F.nr ? F.r[0] : F.a;  // the closing repeat; unused slots point at a
+    };
+    const auto slots_used = [](const Fan &F) { return 2 + std::min(F.f + 1, 6); };
+    // group centroids and extents for the RCB
+    std::vector<double> cen(3 * G);
+    double gext[3] = {0.0, 0.0, 0.0};
+    for (uint64_t g = 0; g < G; ++g)
+    {
+        const Fan &F = fans[g];
+        const int su = slots_used(F);
+        for (int k = 0; k < 3; ++k)
+        {
+            double v = 0.0, mn = 1e300, mx = -1e300;
+            for (int s = 0; s < su; ++s)
+            {
+                const double x = d->node_coords[3ull * slot_node(F, s) + k];
+                v += x;
+                mn = std::min(mn, x);
+                mx = std::max(mx, x);
+            }
+            cen[3 * g + k] = v / su;
+            gext[k] += mx - mn;
+        }
+    }
+    for (int k = 0; k < 3; ++k)
+        gext[k] /= (double)G;
+    std::vector<uint32_t> order(G);
+    std::iota(order.begin(), order.end(), 0u);
+    std::vector<uint64_t> leaf_end;
+    rcb_partition(cen, gext, order, nt, leaf_end);
+
+    // tiles: each RCB leaf, split greedily while its node list would exceed max_nodes
+    std::vector<uint32_t> stamp(N, ~0u), local(N, 0);
+    std::vector<uint32_t> nodes, cnt, cur;
+    out.hdr.clear();
+    out.grecA.resize(G);
+    out.grecB.resize(G);
+    if (mat)
+        out.gmat.resize(G);
+    uint64_t p = 0;
+    uint32_t tile = 0;
+    size_t leaf = 0;
+    std::vector<uint32_t> gorder;  // groups in tile order
+    gorder.reserve(G);
+    while (p < G)
+    {
+        while (leaf < leaf_end.size() && leaf_end[leaf] <= p)
+            ++leaf;
+        const uint64_t stop = leaf < leaf_end.size() ? leaf_end[leaf] : G;
+        nodes.clear();
+        const uint64_t p0 = p;
+        while (p < stop && p - p0 < nt)
+        {
+            const Fan &F = fans[order[p]];
+            uint32_t add = 0;
+            for (int s = 0; s < slots_used(F); ++s)
+            {
+                const uint32_t n = slot_node(F, s);
+                if (stamp[n] != tile)
+                {
+                    stamp[n] = tile;
+                    ++add;
+                    nodes.push_back(n);
+                }
+            }
+            if (nodes.size() > max_nodes)
+            {
+                // undo this group's new nodes and close the tile before it
+                for (uint32_t k = 0; k < add; ++k)
+                {
+                    stamp[nodes.back()] = ~0u;
+                    nodes.pop_back();
+                }
+                break;
+            }
+            ++p;
+        }
+        if (p == p0)
+            return -2;  // one group alone exceeds max_nodes (cannot happen: <= 8 nodes)
+        std::sort(nodes.begin(), nodes.end());
+        const uint32_t nn = (uint32_t)nodes.size(), ng = (uint32_t)(p - p0);
+        for (uint32_t i = 0; i < nn; ++i)
+            local[nodes[i]] = i;
+        // push entries per node, ascending group within the tile
+        cnt.assign(nn, 0);
+        for (uint64_t q = p0; q < p; ++q)
+        {
+            const Fan &F = fans[order[q]];
+            for (int s = 0; s < slots_used(F); ++s)
+                ++cnt[local[slot_node(F, s)]];
+        }
+        // padded runs: even starts, 2 (mod 4) slots where the budget allows (the tet tiles' rule, abi.cpp)
+        std::vector<uint32_t> start(nn);
+        for (int spread = 1; spread >= 0; --spread)
+        {
+            uint32_t padded = 0;
+            for (uint32_t i = 0; i < nn; ++i)
+            {
+                start[i] = padded;
+                uint32_t len = (cnt[i] + 1u) & ~1u;
+                if (spread && (len / 2u) % 2u == 0u)
+                    len += 2u;
+                padded += len;
+            }
+            out.max_tile_slots = std::max(out.max_tile_slots, padded);
+            if (padded <= slot_budget || !spread)
+                break;
+        }
+        cur.assign(start.begin(), start.end());
+        const uint32_t nb = (uint32_t)out.tile_nodes.size();
+        for (uint64_t q = p0; q < p; ++q)
+        {
+            const uint32_t g = order[q];
+            const Fan &F = fans[g];
+            const uint64_t gi = gorder.size();
+            gorder.push_back(g);
+            uint32_t id[8], pos[8];
+            for (int s = 0; s < 8; ++s)
+            {
+                id[s] = local[slot_node(F, s)];
+                pos[s] = s < slots_used(F) ? cur[id[s]]++ : 0u;
+            }
+            out.grecA[gi] = uint4{id[0] | id[1] << 8 | id[2] << 16 | id[3] << 24,
+                                  id[4] | id[5] << 8 | id[6] << 16 | id[7] << 24, (uint32_t)F.f, 0u};
+            out.grecB[gi] = uint4{pos[0] | pos[1] << 16, pos[2] | pos[3] << 16, pos[4] | pos[5] << 16,
+                                  pos[6] | pos[7] << 16};
+            if (mat)
+                out.gmat[gi] = mat[F.t[0]];
+        }
+        const double *o = d->node_coords + 3ull * nodes[0];
+        for (uint32_t i = 0; i < nn; ++i)
+        {
+            out.tile_nodes.push_back(nodes[i]);
+            out.run.push_back(start[i] | ((start[i] + cnt[i]) << 16));
+            for (int k = 0; k < 3; ++k)
+                out.tcoord[k].push_back((float)(d->node_coords[3ull * nodes[i] + k] - o[k]));
+        }
+        out.hdr.push_back(uint4{(uint32_t)p0, ng, nb, nn});
+        out.max_tile_nodes = std::max(out.max_tile_nodes, nn);
+        ++tile;
+    }
+    out.ntiles = tile;
+    // groups were emitted in tile order: gorder[gi] = fan index; tets map to the emitted index
+    std::vector<uint32_t> emitted(G);
+    for (uint64_t gi = 0; gi < G; ++gi)
+        emitted[gorder[gi]] = (uint32_t)gi;
+    out.tet_group.resize(E);
+    for (uint64_t e = 0; e < E; ++e)
+        out.tet_group[e] = emitted[group[e]];
+    // node -> slots ascending tile, node-major slot of every tile node, owner = first slot (bit 31)
+    const uint64_t T = out.tile_nodes.size();
+    out.node_part_off.assign(N + 1, 0);
+    for (uint64_t s = 0; s < T; ++s)
+        ++out.node_part_off[out.tile_nodes[s] + 1];
+    for (uint64_t n = 0; n < N; ++n)
+        out.node_part_off[n + 1] += out.node_part_off[n];
+    out.tile_slot.resize(T);
+    {
+        std::vector<uint32_t> c2(out.node_part_off.begin(), out.node_part_off.end() - 1);
+        for (uint64_t s = 0; s < T; ++s)
+        {
+            const uint32_t n = out.tile_nodes[s];
+            if (c2[n] == out.node_part_off[n])
+                out.tile_nodes[s] |= 0x80000000u;  // the node's first (lowest-tile) slot owns it
+            out.tile_slot[s] = c2[n]++;
+        }
+    }
+    return 0;
+}
+
+}  // namespace cwf

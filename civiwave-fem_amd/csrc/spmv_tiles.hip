@@ -361,21 +361,12 @@ struct PcgArgs
 // the strain is built from the unscaled r_a and ONE scale lands on the 6 stresses (no per-gradient
 // division, no per-force volume multiply). FAST arithmetic: FMA contractions and the hardware
 // reciprocal (1 ulp), tolerance-checked against the oracle.
+// the element body from register operands: corners X[a] = {x, y, z, p_x}, Q[a] = {p_y, p_z}
 template <bool ISO>
-__device__ __forceinline__ void geo_element_forces(const DevSys &s, uint2 id, const float4 *sxp, const float2 *sq,
-                                                   float sK6, uint32_t mi, const float *dtab, float f[12])
+__device__ __forceinline__ void tet_forces_reg(const DevSys &s, const float4 X[4], const float2 Q[4], float sK6,
+                                               uint32_t mi, const float *dtab, float f[12])
 {
     constexpr int kTab = ISO ? 12 : 36;
-    const uint32_t li[4] = {id.x & 0xffffu, id.x >> 16, id.y & 0xffffu, id.y >> 16};
-    // one ds_read_b128 {x, y, z, p_x} + one ds_read_b64 {p_y, p_z} per corner
-    float4 X[4];
-    float2 Q[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-    {
-        X[a] = sxp[li[a]];
-        Q[a] = sq[li[a]];
-    }
     float c[3][3];
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -434,6 +425,23 @@ __device__ __forceinline__ void geo_element_forces(const DevSys &s, uint2 id, co
         f[3 * a + 1] = fmaf(az, sig[4], fmaf(ax, sig[3], ay * sig[1]));
         f[3 * a + 2] = fmaf(ax, sig[5], fmaf(ay, sig[4], az * sig[2]));
     }
+}
+
+template <bool ISO>
+__device__ __forceinline__ void geo_element_forces(const DevSys &s, uint2 id, const float4 *sxp, const float2 *sq,
+                                                   float sK6, uint32_t mi, const float *dtab, float f[12])
+{
+    const uint32_t li[4] = {id.x & 0xffffu, id.x >> 16, id.y & 0xffffu, id.y >> 16};
+    // one ds_read_b128 {x, y, z, p_x} + one ds_read_b64 {p_y, p_z} per corner
+    float4 X[4];
+    float2 Q[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        X[a] = sxp[li[a]];
+        Q[a] = sq[li[a]];
+    }
+    tet_forces_reg<ISO>(s, X, Q, sK6, mi, dtab, f);
 }
 
 // MODE 0: apply (gather x, optional sanitize); MODE 1: PCG (gather z, p_old -> p_new).
@@ -906,6 +914,262 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
     }
 }
 
+// ---- fan groups (groups.cpp) ----
+// Persistent, XCD-aware, software-pipelined like k_keff_tiles_pipe, over tiles of <= NT fan groups (one per
+// lane) and <= 2 NT nodes (two per lane). A lane loads its group's <= 8 nodes {x y z v_x}{v_y v_z} from LDS
+// once, runs the group's f <= 6 tets {a, b, r_i, r_(i+1) mod 6} through the same fp32 element body with
+// static register indices, sums the forces per node in registers and pushes one force per node to its
+// position in the tile's local CSR; the node fold, partial stores, p.Ap share and owner p store are those of
+// k_keff_tiles_pipe.
+struct GroupNext
+{
+    uint2 tn[2];          // records of tile nodes threadIdx.x, threadIdx.x + NT
+    uint32_t slot[2];     // their node-major partial slots
+    float c[2][3];        // their tile-relative coordinates
+    float v[2][3], w[2][3], m[2];  // x / p_old, z and lumped mass at them
+    uint4 ga, gb;         // record of group threadIdx.x
+    uint32_t gm;          // its material (0 when M == 1)
+};
+
+template <int NT, bool SANITIZE, int MODE>
+__device__ __forceinline__ void group_issue_records(const DevSys &s, uint4 hd, GroupNext &n)
+{
+    const DevTiles &T = s.t;
+    const uint32_t g0 = hd.x, ng = hd.y, nb = hd.z, nn = hd.w;
+    const uint32_t T3 = T.total_tile_nodes;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+        const uint32_t i = threadIdx.x + k * (uint32_t)NT;
+        const uint32_t q = nb + (i < nn ? i : 0u);
+        n.tn[k] = i < nn ? T.tnode[q] : uint2{0u, 0u};
+        n.slot[k] = T.tslot[q];
+        n.c[k][0] = T.tcoord[q];
+        n.c[k][1] = T.tcoord[T3 + q];
+        n.c[k][2] = T.tcoord[2 * T3 + q];
+    }
+    const uint32_t gi = g0 + (threadIdx.x < ng ? threadIdx.x : 0u);
+    n.ga = T.grecA[gi];
+    n.gb = T.grecB[gi];
+    n.gm = T.mat ? T.mat[gi] : 0u;
+}
+
+template <bool SANITIZE, int MODE>
+__device__ __forceinline__ void group_issue_gather(const DevSys &s, const float *__restrict__ x,
+                                                   const float *__restrict__ z, GroupNext &n)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+    {
+        const uint32_t g = n.tn[k].x & 0x7fffffffu;  // node 0 for idle lanes (harmless, in range)
+        n.m[k] = 0.f;
+        n.v[k][0] = x[3u * g + 0];
+        n.v[k][1] = x[3u * g + 1];
+        n.v[k][2] = x[3u * g + 2];
+        if constexpr (MODE == 1)
+        {
+            n.w[k][0] = z[3u * g + 0];
+            n.w[k][1] = z[3u * g + 1];
+            n.w[k][2] = z[3u * g + 2];
+            n.m[k] = s.mass[g];
+        }
+        else if constexpr (SANITIZE)
+        {
+            const uint32_t mk = s.mask[g];
+            n.v[k][0] = (mk & 1u) ? 0.f : n.v[k][0];
+            n.v[k][1] = (mk & 2u) ? 0.f : n.v[k][1];
+            n.v[k][2] = (mk & 4u) ? 0.f : n.v[k][2];
+        }
+    }
+}
+
+// one fan group: tets i < f of {slot 0, slot 1, slot 2 + i, slot 2 + (i + 1) mod 6}; forces summed per slot
+// and pushed to the slots' local-CSR positions (gb), slots a, b and ring 0 .. min(f + 1, 6) - 1 only
+template <bool ISO>
+__device__ __forceinline__ void group_forces(const DevSys &s, uint4 ga, uint4 gb, uint32_t mi, const float4 *sxp,
+                                             const float2 *sq, float sK6, const float *dtab, float2 *sfxy,
+                                             float *sfz)
+{
+    float4 X[8];
+    float2 Q[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+    {
+        const uint32_t id = ((k < 4 ? ga.x : ga.y) >> (8 * (k & 3))) & 0xffu;
+        X[k] = sxp[id];
+        Q[k] = sq[id];
+    }
+    const int f = (int)ga.z;
+    float F[8][3];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        F[k][0] = F[k][1] = F[k][2] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+    {
+        if (i < f)
+        {
+            const int c2 = 2 + i, c3 = 2 + (i + 1) % 6;
+            const float4 Xt[4] = {X[0], X[1], X[c2], X[c3]};
+            const float2 Qt[4] = {Q[0], Q[1], Q[c2], Q[c3]};
+            float ft[12];
+            tet_forces_reg<ISO>(s, Xt, Qt, sK6, mi, dtab, ft);
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+            {
+                F[0][q] += ft[q];
+                F[1][q] += ft[3 + q];
+                F[c2][q] += ft[6 + q];
+                F[c3][q] += ft[9 + q];
+            }
+        }
+    }
+    const int used = 2 + (f + 1 < 6 ? f + 1 : 6);
+    const uint32_t pw[4] = {gb.x, gb.y, gb.z, gb.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (k < used)
+        {
+            const uint32_t pos = (k & 1) ? pw[k >> 1] >> 16 : pw[k >> 1] & 0xffffu;
+            sfxy[pos] = float2{F[k][0], F[k][1]};
+            sfz[pos] = F[k][2];
+        }
+}
+
+template <bool ISO, bool SANITIZE, int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
+                                                         const uint4 *__restrict__ hdr)
+{
+    constexpr int kTab = ISO ? 12 : 36;
+    constexpr int SP = (int)kGroupSlots, MS = 2 * NT;
+    extern __shared__ float lds[];
+    const DevTiles &T = s.t;
+    float2 *sfxy = reinterpret_cast<float2 *>(lds);           // [SP]
+    float *sfz = lds + 2 * SP;                                // [SP]
+    float4 *sxp = reinterpret_cast<float4 *>(lds + 3 * SP);  // [MS] {x, y, z, v_x}
+    float2 *sq = reinterpret_cast<float2 *>(sxp + MS);       // [MS] {v_y, v_z}
+    __shared__ float dtab[kMaxM * kTab];
+    __shared__ double red[NT / 64];
+    if constexpr (MODE == 1)
+    {
+        if (!pa.ctl->active)
+            return;
+    }
+    const uint32_t nxcd = 8u, xcd = blockIdx.x % nxcd, lb = blockIdx.x / nxcd, nbx = gridDim.x / nxcd;
+    const uint32_t t_end = (uint32_t)(((uint64_t)(xcd + 1) * T.ntiles) / nxcd);
+    uint32_t t = (uint32_t)(((uint64_t)xcd * T.ntiles) / nxcd) + lb;
+    GroupNext cur;
+    uint4 hd = t < t_end ? hdr[t] : uint4{0u, 0u, 0u, 0u};
+    uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
+    if (t < t_end)
+    {
+        group_issue_records<NT, SANITIZE, MODE>(s, hd, cur);
+        group_issue_gather<SANITIZE, MODE>(s, x, pa.z, cur);
+    }
+    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
+    for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
+        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
+    float beta = 0.f;
+    if constexpr (MODE == 1)
+    {
+        if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta, pa.abl & 32u))
+            return;
+    }
+    const float sK6 = (float)(s.sK / 6.0), sM = (float)s.sM;
+    double pap = 0.0;
+    for (; t < t_end; t += nbx)
+    {
+        const uint32_t ng = hd.y, nn = hd.w;
+        // (a) LDS fill of tile t's nodes (two per lane) from the prefetched registers
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+        {
+            const uint32_t i = threadIdx.x + k * NT;
+            if (i < nn)
+            {
+                float v0 = cur.v[k][0], v1 = cur.v[k][1], v2 = cur.v[k][2];
+                if constexpr (MODE == 1)
+                {
+                    v0 = fmaf(beta, v0, cur.w[k][0]);
+                    v1 = fmaf(beta, v1, cur.w[k][1]);
+                    v2 = fmaf(beta, v2, cur.w[k][2]);
+                }
+                sxp[i] = float4{cur.c[k][0], cur.c[k][1], cur.c[k][2], v0};
+                sq[i] = float2{v1, v2};
+            }
+        }
+        const uint4 ga = cur.ga, gb = cur.gb;
+        const uint32_t gm = cur.gm;
+        const uint2 tn_own[2] = {cur.tn[0], cur.tn[1]};
+        const uint32_t slot_own[2] = {cur.slot[0], cur.slot[1]};
+        const float m_own[2] = {cur.m[0], cur.m[1]};
+        __syncthreads();
+        // (b) next tile's records in flight during this tile's group and fold work
+        const uint32_t tn_next = t + nbx;
+        const uint4 hdn = hd2;
+        if (tn_next < t_end)
+            group_issue_records<NT, SANITIZE, MODE>(s, hdn, cur);
+        hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
+        // (c) this lane's group (ablation bit 64: skipped, diagnostic timing only)
+        if (threadIdx.x < ng && !(pa.abl & 64u))
+            group_forces<ISO>(s, ga, gb, gm, sxp, sq, sK6, dtab, sfxy, sfz);
+        __syncthreads();
+        // (d) next tile's gathers (ablation bit 256: skipped)
+        if (tn_next < t_end && !(pa.abl & 256u))
+            group_issue_gather<SANITIZE, MODE>(s, x, pa.z, cur);
+        // (e) fold per tile node -> node-major partials (+ p.Ap) (ablation bit 128: skipped)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+        {
+            const uint32_t i = threadIdx.x + k * NT;
+            if (i < ((pa.abl & 128u) ? 0u : nn))
+            {
+                const uint2 tn = tn_own[k];
+                float a0, a1, a2;
+                fold_run(sfxy, sfz, tn.y & 0xffffu, tn.y >> 16, a0, a1, a2);
+                float p0 = 0.f, p1 = 0.f, p2 = 0.f;
+                if constexpr (MODE == 1)
+                {
+                    p0 = sxp[i].w;
+                    p1 = sq[i].x;
+                    p2 = sq[i].y;
+                    if (tn.x & 0x80000000u)  // the node's owner slot carries its mass term m s_M p (once)
+                    {
+                        const float m = m_own[k] * sM;
+                        a0 = fmaf(m, p0, a0);
+                        a1 = fmaf(m, p1, a1);
+                        a2 = fmaf(m, p2, a2);
+                        if (pa.pnew)  // and stores the new p for the update pass
+                        {
+                            float *q = pa.pnew + 3ull * (tn.x & 0x7fffffffu);
+                            q[0] = p0;
+                            q[1] = p1;
+                            q[2] = p2;
+                        }
+                    }
+                }
+                if (!(pa.abl & 512u))
+                {
+                    float *o = T.part + 3ull * slot_own[k];
+                    o[0] = a0;
+                    o[1] = a1;
+                    o[2] = a2;
+                }
+                if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
+                    pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+            }
+        }
+        __syncthreads();  // LDS is refilled by the next tile
+        hd = hdn;
+    }
+    if constexpr (MODE == 1)
+    {
+        const double tt = block_sum<NT>(pap, red);
+        if (threadIdx.x == 0)
+            pa.part_dot[blockIdx.x] = tt;
+    }
+}
+
 // pcg.cpp:862-895 for the last iteration of a batch (the next batch's tiles kernel repeats it
 // idempotently): one workgroup
 __global__ __launch_bounds__(256) void k_pcg_check(Ctl *ctl, const double *__restrict__ prr,
@@ -1221,12 +1485,42 @@ void launch_pipe(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t
         k_keff_tiles_pipe<ISO, SAN, MODE, NT><<<s.t.pipe_grid, NT, lds, st>>>(s, x, pa, s.t.hdr);
 }
 
+constexpr size_t kGroupLds = sizeof(float) * 3 * kGroupSlots + 2 * kGroupThreads * (16 + 8);
+
+template <bool ISO>
+unsigned group_grid_query()
+{
+    int dev = 0, bpc = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_groups_pipe<ISO, false, 1, kGroupThreads>,
+                                                       kGroupThreads, kGroupLds);
+    unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
+    return g < 8u ? 8u : g - g % 8u;  // whole XCD groups
+}
+
+template <bool ISO, bool SAN, int MODE>
+void launch_groups(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
+{
+    if (e0 && e1)
+        hipExtLaunchKernelGGL(k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads>, dim3(s.t.pipe_grid),
+                              dim3(kGroupThreads), (uint32_t)kGroupLds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+    else
+        k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads><<<s.t.pipe_grid, kGroupThreads, kGroupLds, st>>>(
+            s, x, pa, s.t.hdr);
+}
+
 // e0/e1 (optional): hipExtLaunchKernel stamps them from the dispatch packet itself, so the timed
 // interval is the kernel's own execution (what rocprofv3 --kernel-trace reports), not marker latency
 template <bool ISO, bool SAN, int MODE>
 void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st,
                   hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
+    if (s.t.grp)
+    {
+        launch_groups<ISO, SAN, MODE>(s, x, pa, st, e0, e1);
+        return;
+    }
     if (s.t.hex)
     {
         launch_hex<ISO, SAN, MODE>(s, x, pa, st, e0, e1);
@@ -1255,6 +1549,12 @@ unsigned fast_tile_blocks(const DevSys &s) { return (s.t.pipe || s.t.hex) ? s.t.
 
 unsigned fast_pipe_grid(const DevSys &s)
 {
+    if (s.t.grp)
+    {
+        const unsigned g = s.iso ? group_grid_query<true>() : group_grid_query<false>();
+        const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
+        return g < need ? g : (need ? need : 8u);
+    }
     if (s.t.hex)
         return s.iso ? hex_grid_query<true>(s) : hex_grid_query<false>(s);
     if (s.t.pipe_nt == 128)

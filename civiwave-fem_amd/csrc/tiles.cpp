@@ -26,9 +26,7 @@
 
 namespace cwf
 {
-namespace
-{
-inline uint64_t spread21(uint64_t v)
+uint64_t spread21(uint64_t v)
 {
     v &= 0x1fffff;
     v = (v | v << 32) & 0x1f00000000ffffull;
@@ -38,6 +36,9 @@ inline uint64_t spread21(uint64_t v)
     v = (v | v << 2) & 0x1249249249249249ull;
     return v;
 }
+
+namespace
+{
 
 // Recursive coordinate bisection of the elements into leaves of at most max_elems (target ~7/8 of it).
 // Each range is cut along the longest axis of its centroid box near the count n * L1 / L (L leaves,
@@ -108,6 +109,12 @@ void rcb(const std::vector<double> &c, const double ext[3], std::vector<uint32_t
     rcb(c, ext, order, cut, e, max_elems, leaf_end);
 }
 }  // namespace
+
+void rcb_partition(const std::vector<double> &c, const double ext[3], std::vector<uint32_t> &order,
+                   uint64_t max_elems, std::vector<uint64_t> &leaf_end)
+{
+    rcb(c, ext, order, 0, order.size(), max_elems, leaf_end);
+}
 
 int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems, int corners)
 {
