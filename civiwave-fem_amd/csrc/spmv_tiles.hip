@@ -983,57 +983,164 @@ __device__ __forceinline__ void group_issue_gather(const DevSys &s, const float 
     }
 }
 
-// one fan group: tets i < f of {slot 0, slot 1, slot 2 + i, slot 2 + (i + 1) mod 6}; forces summed per slot
-// and pushed to the slots' local-CSR positions (gb), slots a, b and ring 0 .. min(f + 1, 6) - 1 only
+// stress of one tet from its strain, D and the |det| scale (the body of tet_forces_reg)
+template <bool ISO>
+__device__ __forceinline__ void fan_stress(const DevSys &s, uint32_t mi, const float *dtab, const float eps[6],
+                                           float scale, float sig[6])
+{
+    constexpr int kTab = ISO ? 12 : 36;
+    if (s.M == 1)
+        stress_f32<ISO>(s.d1, eps, sig);
+    else if (mi < (uint32_t)kMaxM)
+        stress_f32<ISO>(dtab + kTab * mi, eps, sig);
+    else
+    {
+        float tab[36];
+        for (int t = 0; t < kTab; ++t)
+            tab[t] = (float)s.dmat[36u * mi + dsrc(ISO, t)];
+        stress_f32<ISO>(tab, eps, sig);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+        sig[r] *= scale;
+}
+
+__device__ __forceinline__ void cross3(const float u[3], const float v[3], float w[3])
+{
+    w[0] = fmaf(u[1], v[2], -u[2] * v[1]);
+    w[1] = fmaf(u[2], v[0], -u[0] * v[2]);
+    w[2] = fmaf(u[0], v[1], -u[1] * v[0]);
+}
+
+// force on a corner with (unscaled) gradient g from the scaled stress: B(g)^T sig
+__device__ __forceinline__ void corner_force(const float g[3], const float sig[6], float f[3])
+{
+    f[0] = fmaf(g[2], sig[5], fmaf(g[1], sig[3], g[0] * sig[0]));
+    f[1] = fmaf(g[2], sig[4], fmaf(g[0], sig[3], g[1] * sig[1]));
+    f[2] = fmaf(g[0], sig[5], fmaf(g[1], sig[4], g[2] * sig[2]));
+}
+
+// One fan group around edge (a, b): tets i < f are {a, b, r_i, r_j}, j = (i + 1) mod 6. With e = x_b - x_a,
+// d_k = x_(r_k) - x_a and w_k = e x d_k, tet i's cofactor rows (tet_forces_reg's g_1..g_3 for the corner
+// order a, b, r_i, r_j) are d_i x d_j, -w_j and w_i, so each ring node's edge vector and cross product is
+// formed once for the two tets that share it. The ring is walked with a rolling window (ring node i, ring
+// node j; ring node 0 kept for the closing tet), and a ring slot's summed force is pushed as soon as its
+// last tet is done; a, b and ring 0 are pushed at the end. gb: 8 u16 push positions (slots a b r0 .. r5).
 template <bool ISO>
 __device__ __forceinline__ void group_forces(const DevSys &s, uint4 ga, uint4 gb, uint32_t mi, const float4 *sxp,
                                              const float2 *sq, float sK6, const float *dtab, float2 *sfxy,
                                              float *sfz)
 {
-    float4 X[8];
-    float2 Q[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-    {
-        const uint32_t id = ((k < 4 ? ga.x : ga.y) >> (8 * (k & 3))) & 0xffu;
-        X[k] = sxp[id];
-        Q[k] = sq[id];
-    }
+    const auto lid = [&](int k) { return ((k < 4 ? ga.x : ga.y) >> (8 * (k & 3))) & 0xffu; };
+    const auto pos = [&](int k) {
+        const uint32_t w = k < 2 ? gb.x : k < 4 ? gb.y : k < 6 ? gb.z : gb.w;
+        return (k & 1) ? w >> 16 : w & 0xffffu;
+    };
+    const auto push = [&](int k, const float F[3]) {
+        const uint32_t q = pos(k);
+        sfxy[q] = float2{F[0], F[1]};
+        sfz[q] = F[2];
+    };
     const int f = (int)ga.z;
-    float F[8][3];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        F[k][0] = F[k][1] = F[k][2] = 0.f;
+    const float4 Xa = sxp[lid(0)], Xb = sxp[lid(1)];
+    const float2 Qa = sq[lid(0)], Qb = sq[lid(1)];
+    const float e[3] = {Xb.x - Xa.x, Xb.y - Xa.y, Xb.z - Xa.z};
+    const float ua[3] = {Xa.w, Qa.x, Qa.y};
+    // relative values du_k = u_k - u_a (the strain is sum over k of g_k (x) du_k, g_a = -(g_1 + g_2 + g_3))
+    const float db[3] = {Xb.w - ua[0], Qb.x - ua[1], Qb.y - ua[2]};
+    float Fa[3] = {0.f, 0.f, 0.f}, Fb[3] = {0.f, 0.f, 0.f}, F0[3] = {0.f, 0.f, 0.f};
+    // ring node k: its edge vector from a, its value relative to a's, and e x d (ring node 0 is read again
+    // for the closing tet rather than kept live through the walk)
+    const auto ring = [&](int k, float d[3], float w[3], float du[3]) {
+        const float4 X = sxp[lid(2 + k)];
+        const float2 Q = sq[lid(2 + k)];
+        d[0] = X.x - Xa.x;
+        d[1] = X.y - Xa.y;
+        d[2] = X.z - Xa.z;
+        du[0] = X.w - ua[0];
+        du[1] = Q.x - ua[1];
+        du[2] = Q.y - ua[2];
+        cross3(e, d, w);
+    };
+    float di[3], wi[3], dui[3];
+    ring(0, di, wi, dui);
+    float Fi[3] = {0.f, 0.f, 0.f};  // ring node i's running sum (ring 0's lives in F0)
 #pragma unroll
     for (int i = 0; i < 6; ++i)
     {
-        if (i < f)
+        if (i >= f)
+            break;
+        const int j = (i + 1) % 6;
+        float dj[3], wj[3], duj[3];
+        ring(j, dj, wj, duj);
+        // cofactor rows (unscaled gradients) of corners b, r_i, r_j; corner a's is minus their sum
+        float g1[3];
+        cross3(di, dj, g1);
+        const float det = fmaf(e[0], g1[0], fmaf(e[1], g1[1], e[2] * g1[2]));
+        const float scale = sK6 * __builtin_amdgcn_rcpf(fabsf(det));
+        // strain = sum over k in {b, r_i, r_j} of B(g_k) (u_k - u_a): g_b = g1, g_ri = -w_j, g_rj = w_i
+        float eps[6];
+        eps[0] = fmaf(-wj[0], dui[0], fmaf(wi[0], duj[0], g1[0] * db[0]));
+        eps[1] = fmaf(-wj[1], dui[1], fmaf(wi[1], duj[1], g1[1] * db[1]));
+        eps[2] = fmaf(-wj[2], dui[2], fmaf(wi[2], duj[2], g1[2] * db[2]));
+        eps[3] = fmaf(g1[0], db[1], g1[1] * db[0]);
+        eps[3] = fmaf(wi[0], duj[1], fmaf(wi[1], duj[0], eps[3]));
+        eps[3] = fmaf(-wj[0], dui[1], fmaf(-wj[1], dui[0], eps[3]));
+        eps[4] = fmaf(g1[1], db[2], g1[2] * db[1]);
+        eps[4] = fmaf(wi[1], duj[2], fmaf(wi[2], duj[1], eps[4]));
+        eps[4] = fmaf(-wj[1], dui[2], fmaf(-wj[2], dui[1], eps[4]));
+        eps[5] = fmaf(g1[0], db[2], g1[2] * db[0]);
+        eps[5] = fmaf(wi[0], duj[2], fmaf(wi[2], duj[0], eps[5]));
+        eps[5] = fmaf(-wj[0], dui[2], fmaf(-wj[2], dui[0], eps[5]));
+        float sig[6];
+        fan_stress<ISO>(s, mi, dtab, eps, scale, sig);
+        float fb[3], fi[3], fj[3];
+        corner_force(g1, sig, fb);
+        const float mwj[3] = {-wj[0], -wj[1], -wj[2]};
+        corner_force(mwj, sig, fi);
+        corner_force(wi, sig, fj);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
         {
-            const int c2 = 2 + i, c3 = 2 + (i + 1) % 6;
-            const float4 Xt[4] = {X[0], X[1], X[c2], X[c3]};
-            const float2 Qt[4] = {Q[0], Q[1], Q[c2], Q[c3]};
-            float ft[12];
-            tet_forces_reg<ISO>(s, Xt, Qt, sK6, mi, dtab, ft);
+            Fb[q] += fb[q];
+            Fa[q] -= fb[q] + fi[q] + fj[q];
+        }
+        if (i == 0)
+        {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                F0[q] += fi[q];
+        }
+        else
+        {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                Fi[q] += fi[q];
+            push(2 + i, Fi);  // ring node i has had both its tets
+        }
+        if (j == 0)
+        {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                F0[q] += fj[q];
+        }
+        else
+        {
 #pragma unroll
             for (int q = 0; q < 3; ++q)
             {
-                F[0][q] += ft[q];
-                F[1][q] += ft[3 + q];
-                F[c2][q] += ft[6 + q];
-                F[c3][q] += ft[9 + q];
+                Fi[q] = fj[q];  // ring node j's first tet; its second is the next one
+                di[q] = dj[q];
+                wi[q] = wj[q];
+                dui[q] = duj[q];
             }
         }
     }
-    const int used = 2 + (f + 1 < 6 ? f + 1 : 6);
-    const uint32_t pw[4] = {gb.x, gb.y, gb.z, gb.w};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (k < used)
-        {
-            const uint32_t pos = (k & 1) ? pw[k >> 1] >> 16 : pw[k >> 1] & 0xffffu;
-            sfxy[pos] = float2{F[k][0], F[k][1]};
-            sfz[pos] = F[k][2];
-        }
+    if (f < 6)
+        push(2 + f, Fi);  // the open fan's last ring node (or a closed fan's repeat of ring node 0)
+    push(2, F0);
+    push(0, Fa);
+    push(1, Fb);
 }
 
 template <bool ISO, bool SANITIZE, int MODE, int NT>
