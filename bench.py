@@ -180,6 +180,7 @@ def main():
     alg_bytes, ref_bytes = float(lay_b.value), float(ref_b.value)
     achieved = alg_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
     ref_equiv = ref_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
+    kname = (L.cwf_hip_system_keff_kernel(h) or b"").decode()
     traffic, traffic_src = None, None
     tpath = args.traffic
     if tpath == "auto":
@@ -189,8 +190,11 @@ def main():
         cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc.json")))
         tpath = cands[-1] if cands and world == 1 else None
     if tpath and os.path.exists(tpath):
-        traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-        traffic_src = os.path.relpath(tpath, ROOT)
+        pmc = json.load(open(tpath))
+        # only a profile of the same kernel counts (a committed profile of an older kernel is not this one's)
+        if any(kname in k for k in pmc.get("kernels", {})):
+            traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(tpath, ROOT)
     result = None
     copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
     if rank == 0:
@@ -223,8 +227,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": ("k_keff_hex_tiles" if args.element == "hex8" else "k_keff_tiles_pipe")
-                                   if args.mode == "fast" else "k_keff_parity",
+                         "kernel": kname,
                          "avg_launch_ms": avg_keff_ms, "launches": int(keff_n.value),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "reference_layout_bytes_per_launch": ref_bytes,

@@ -1136,6 +1136,16 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
     return 0;
 }
 
+const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
+{
+    if (!h)
+        return nullptr;
+    const DevTiles &t = h->ds.t;
+    if (h->mode != CWF_MODE_FAST || !t.ntiles)
+        return "k_keff_parity";
+    return t.grp ? "k_keff_groups_pipe" : t.hex ? "k_keff_hex_tiles" : t.pipe ? "k_keff_tiles_pipe" : "k_keff_tiles";
+}
+
 int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_kind, float *elements,
                            float *nodes, int out_kind)
 {

@@ -144,6 +144,9 @@ int cwf_hip_bandwidth_probe(int device, uint64_t bytes, int reps, double *gbs);
  * once (the headline roofline uses the build's own layout when it reads less);
  * `reference_layout_bytes` = 32 N + 72 E, the same SpMV over the reference's packed layout. */
 int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes, uint64_t *reference_layout_bytes);
+/* Name of the kernel the handle's K_eff launches in its current mode ("k_keff_groups_pipe",
+ * "k_keff_tiles_pipe", "k_keff_tiles", "k_keff_hex_tiles" or "k_keff_parity"); NULL for a NULL handle. */
+const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
 
 /* Live kernel timing (measurement support, not a reference interface): when enabled, every
  * K_eff launch inside solve_pcg / stepper_step is bracketed by hipEvents on the handle's stream;

@@ -6,7 +6,7 @@ set -o pipefail
 TAG=${1:-r01}
 O=gpurun_out/round
 mkdir -p $O
-K="k_keff_tiles_pipe<true, false, 1,"
+K="k_keff_groups_pipe<true, false, 1,"
 timeout -k 10 400 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/${TAG}_gpu_tests.log 2>&1; tail -1 $O/${TAG}_gpu_tests.log
 timeout -k 10 300 python -u bench.py > $O/${TAG}_bench_c2.log 2>&1 && tail -1 $O/${TAG}_bench_c2.log > $O/${TAG}_bench_c2_fast.json &&
 timeout -k 10 300 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_c3.log 2>&1 && tail -1 $O/${TAG}_bench_c3.log > $O/${TAG}_bench_c3_fast.json &&
