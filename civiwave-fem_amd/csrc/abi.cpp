@@ -649,11 +649,12 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             t.pipe = t.geo && !(pp && pp[0] == '0') ? 1 : 0;
         }
         // fan groups (groups.cpp, k_keff_groups_pipe): the default FAST tet path when the mesh groups into
-        // fans of >= 3 tets on average (CWF_GROUPS=0: the per-tet tiles below)
+        // fans of >= 3 tets on average and has <= 16 materials (D from kernel arguments or an LDS table);
+        // CWF_GROUPS=0: the per-tet tiles below
         bool grouped = false;
         {
             const char *gv = getenv("CWF_GROUPS");
-            if (!hex && t.pipe && !(gv && gv[0] == '0'))
+            if (!hex && t.pipe && !(gv && gv[0] == '0') && d->material_count <= 16)
             {
                 GroupTiles gt;
                 int gst = -1;
@@ -682,21 +683,12 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                             gt.node_part_off[n] |= (d->bc_mask[n] & 7u) << 29;
                         t.off_mask = 1;
                     }
-                    uint4 *ga, *gb, *dh;
+                    uint4 *ga, *dh;
                     uint2 *dtn;
                     uint32_t *npo, *tsl;
                     float *tc, *part;
-                    if (int st = upload(h, &ga, gt.grecA.data(), gt.grecA.size()))
+                    if (int st = upload(h, &ga, gt.grec.data(), gt.grec.size()))
                         return bail(st);
-                    if (int st = upload(h, &gb, gt.grecB.data(), gt.grecB.size()))
-                        return bail(st);
-                    if (!gt.gmat.empty())
-                    {
-                        uint32_t *gm;
-                        if (int st = upload(h, &gm, gt.gmat.data(), gt.gmat.size()))
-                            return bail(st);
-                        t.mat = gm;
-                    }
                     if (int st = upload(h, &dh, gt.hdr.data(), gt.hdr.size()))
                         return bail(st);
                     if (int st = upload(h, &dtn, tnode.data(), T))
@@ -712,8 +704,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     if (int st = dalloc(h, &part, 3 * (T + 2)))  // + 2 padding slots (update pass)
                         return bail(st);
                     t.grp = 1;
-                    t.grecA = ga;
-                    t.grecB = gb;
+                    t.grec = ga;
                     t.hdr = dh;
                     t.tnode = dtn;
                     t.tslot = tsl;
@@ -1120,11 +1111,11 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // (pipelined / hex), partial written 12 B; per node: p_old and z read once (24 B) + mass 4 B + the new
         // p written by its owner slot (12 B, PCG mode: the launches bench.py times)
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
-        // fan groups: 32-B group record (+ material id when M > 1) instead of the per-tet records
+        // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
         if (s.t.grp)
         {
-            *layout_bytes = 16ull * s.t.ntiles + (uint64_t)s.t.ngroups * (32 + (s.t.mat ? 4 : 0)) +
+            *layout_bytes = 16ull * s.t.ntiles + (uint64_t)s.t.ngroups * 16 +
                             T * (8 + 12 + 4 + 12) + N * (24 + 4 + 12);
             return 0;
         }

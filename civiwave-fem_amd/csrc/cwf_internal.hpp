@@ -27,7 +27,8 @@ constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two n
 constexpr uint32_t kHexTileThreads = 128;  // hex8 tiles: <= 128 hexes and <= 256 nodes per 128-lane workgroup
 constexpr uint32_t kGroupThreads = 128;    // fan-group tiles: <= 128 groups (one per lane) ...
 constexpr uint32_t kGroupMaxNodes = 256;   // ... <= 256 nodes (two per lane; u8 local ids) ...
-constexpr uint32_t kGroupSlots = 1536;     // ... and <= 1536 pushed-force slots (padded runs, LDS)
+constexpr uint32_t kGroupSlots = 1536;     // ... and <= 1536 pushed-force slots (padded runs, LDS) ...
+constexpr uint32_t kGroupMaxRun = 16;      // ... and <= 16 pushes per tile node (4-bit ranks in the record)
 
 struct DevTiles
 {
@@ -54,8 +55,9 @@ struct DevTiles
     // tet fan groups (groups.cpp): k_keff_groups_pipe, one group per lane, pushes per group node
     int grp = 0;
     uint32_t ngroups = 0;
-    const uint4 *grecA = nullptr;  // [G] {8 x u8 local node ids (a b r0 .. r5), tet count, 0}
-    const uint4 *grecB = nullptr;  // [G] 8 x u16 push positions
+    // [G] {u8 local node ids of slots a b r0 r1, of r2 .. r5, 8 x 4-bit ranks in the slots' runs,
+    //      tet count f | material << 3}
+    const uint4 *grec = nullptr;
     // native hex8: k_keff_hex_tiles, 128-thread persistent grid (pipe_grid), push fold
     int hex = 0;
     int hex_all_affine = 0;        // every hex tile is a parallelepiped tile (affine-only kernel variant)
@@ -108,9 +110,9 @@ struct GroupTiles
 {
     uint32_t ntiles = 0, ngroups = 0, max_tile_nodes = 0, max_tile_slots = 0;
     double tets_per_group = 0.0;
-    std::vector<uint4> grecA;  // [G] {a b r0 r1 (u8 local ids), r2 r3 r4 r5, tet count f, 0}
-    std::vector<uint4> grecB;  // [G] u16 push positions of slots a b r0 .. r5 (tile-relative, padded runs)
-    std::vector<uint32_t> gmat;            // [G] material (when M > 1; groups are single-material)
+    // [G] {a b r0 r1 (u8 local ids), r2 r3 r4 r5, 4-bit rank of each used slot in its node's run (push
+    // position = run start + rank), tet count f | material << 3 (groups are single-material)}
+    std::vector<uint4> grec;
     std::vector<uint4> hdr;                // [ntiles] {first group, #groups, first tile node, #nodes}
     std::vector<uint32_t> tile_nodes;      // [T] global node | owner bit 31
     std::vector<uint32_t> run;             // [T] padded run begin | end << 16

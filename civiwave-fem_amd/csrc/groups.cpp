@@ -13,8 +13,10 @@
 // fan of unassigned, same-material tets (walked both ways around the edge from the seed) is longest
 // (closed fans preferred); a closed fan of f < 6 tets repeats r_0 in slot f, an open fan holds <= 5 tets.
 // Tiles: recursive coordinate bisection of the group centroids (rcb_partition) into <= nt groups, split
-// further while a tile's node list exceeds max_nodes; the local CSR of pushed forces is ordered by
-// (node, group), the fold order, and every run is padded as for the tet tiles (abi.cpp).
+// further while a tile's node list exceeds max_nodes or a node's run exceeds kGroupMaxRun pushes; the local
+// CSR of pushed forces is ordered by (node, group), the fold order, and every run is padded as for the tet
+// tiles (abi.cpp). A group's push position for slot s is its node's run start (kept in LDS by the kernel)
+// plus the group's rank in that run, so the 16-B record carries 4-bit ranks instead of 16-bit positions.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -267,13 +269,10 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
     rcb_partition(cen, gext, order, nt, leaf_end);
 
     // tiles: each RCB leaf, split greedily while its node list would exceed max_nodes
-    std::vector<uint32_t> stamp(N, ~0u), local(N, 0);
+    std::vector<uint32_t> stamp(N, ~0u), local(N, 0), tcnt(N, 0);
     std::vector<uint32_t> nodes, cnt, cur;
     out.hdr.clear();
-    out.grecA.resize(G);
-    out.grecB.resize(G);
-    if (mat)
-        out.gmat.resize(G);
+    out.grec.resize(G);
     uint64_t p = 0;
     uint32_t tile = 0;
     size_t leaf = 0;
@@ -290,19 +289,24 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
         {
             const Fan &F = fans[order[p]];
             uint32_t add = 0;
+            bool long_run = false;
             for (int s = 0; s < slots_used(F); ++s)
             {
                 const uint32_t n = slot_node(F, s);
                 if (stamp[n] != tile)
                 {
                     stamp[n] = tile;
+                    tcnt[n] = 0;
                     ++add;
                     nodes.push_back(n);
                 }
+                long_run |= ++tcnt[n] > kGroupMaxRun;
             }
-            if (nodes.size() > max_nodes)
+            if (nodes.size() > max_nodes || long_run)
             {
-                // undo this group's new nodes and close the tile before it
+                // undo this group's pushes and new nodes and close the tile before it
+                for (int s = 0; s < slots_used(F); ++s)
+                    --tcnt[slot_node(F, s)];
                 for (uint32_t k = 0; k < add; ++k)
                 {
                     stamp[nodes.back()] = ~0u;
@@ -351,18 +355,16 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
             const Fan &F = fans[g];
             const uint64_t gi = gorder.size();
             gorder.push_back(g);
-            uint32_t id[8], pos[8];
+            uint32_t id[8], ranks = 0;
             for (int s = 0; s < 8; ++s)
             {
                 id[s] = local[slot_node(F, s)];
-                pos[s] = s < slots_used(F) ? cur[id[s]]++ : 0u;
+                if (s < slots_used(F))
+                    ranks |= (cur[id[s]]++ - start[id[s]]) << (4 * s);  // < kGroupMaxRun (tile loop above)
             }
-            out.grecA[gi] = uint4{id[0] | id[1] << 8 | id[2] << 16 | id[3] << 24,
-                                  id[4] | id[5] << 8 | id[6] << 16 | id[7] << 24, (uint32_t)F.f, 0u};
-            out.grecB[gi] = uint4{pos[0] | pos[1] << 16, pos[2] | pos[3] << 16, pos[4] | pos[5] << 16,
-                                  pos[6] | pos[7] << 16};
-            if (mat)
-                out.gmat[gi] = mat[F.t[0]];
+            out.grec[gi] = uint4{id[0] | id[1] << 8 | id[2] << 16 | id[3] << 24,
+                                 id[4] | id[5] << 8 | id[6] << 16 | id[7] << 24, ranks,
+                                 (uint32_t)F.f | (mat ? mat[F.t[0]] : 0u) << 3};
         }
         const double *o = d->node_coords + 3ull * nodes[0];
         for (uint32_t i = 0; i < nn; ++i)

@@ -916,22 +916,27 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
 
 // ---- fan groups (groups.cpp) ----
 // Persistent, XCD-aware, software-pipelined like k_keff_tiles_pipe, over tiles of <= NT fan groups (one per
-// lane) and <= 2 NT nodes (two per lane). A lane loads its group's <= 8 nodes {x y z v_x}{v_y v_z} from LDS
-// once, runs the group's f <= 6 tets {a, b, r_i, r_(i+1) mod 6} through the same fp32 element body with
-// static register indices, sums the forces per node in registers and pushes one force per node to its
-// position in the tile's local CSR; the node fold, partial stores, p.Ap share and owner p store are those of
-// k_keff_tiles_pipe.
+// lane) and <= 2 NT nodes (two per lane). A lane loads its group's <= 8 nodes {x y z v_x}{v_y v_z} from LDS,
+// runs the group's f <= 6 tets {a, b, r_i, r_(i+1) mod 6} in packed fp32 (v_pk_fma_f32: tets i and i + 3 of
+// the fan side by side, so a closed Kuhn fan is three packed tet pairs), sums the forces per node in
+// registers and pushes one force per node to its position in the tile's local CSR (the node's run start,
+// kept in LDS, plus the group's 4-bit rank in the run from the 16-B record); the node fold, partial stores,
+// p.Ap share and owner p store are those of k_keff_tiles_pipe.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+
 struct GroupNext
 {
     uint2 tn[2];          // records of tile nodes threadIdx.x, threadIdx.x + NT
     uint32_t slot[2];     // their node-major partial slots
     float c[2][3];        // their tile-relative coordinates
     float v[2][3], w[2][3], m[2];  // x / p_old, z and lumped mass at them
-    uint4 ga, gb;         // record of group threadIdx.x
-    uint32_t gm;          // its material (0 when M == 1)
+    uint4 g;              // record of group threadIdx.x
 };
 
-template <int NT, bool SANITIZE, int MODE>
+template <int NT>
 __device__ __forceinline__ void group_issue_records(const DevSys &s, uint4 hd, GroupNext &n)
 {
     const DevTiles &T = s.t;
@@ -948,10 +953,7 @@ __device__ __forceinline__ void group_issue_records(const DevSys &s, uint4 hd, G
         n.c[k][1] = T.tcoord[T3 + q];
         n.c[k][2] = T.tcoord[2 * T3 + q];
     }
-    const uint32_t gi = g0 + (threadIdx.x < ng ? threadIdx.x : 0u);
-    n.ga = T.grecA[gi];
-    n.gb = T.grecB[gi];
-    n.gm = T.mat ? T.mat[gi] : 0u;
+    n.g = T.grec[g0 + (threadIdx.x < ng ? threadIdx.x : 0u)];
 }
 
 template <bool SANITIZE, int MODE>
@@ -983,167 +985,174 @@ __device__ __forceinline__ void group_issue_gather(const DevSys &s, const float 
     }
 }
 
-// stress of one tet from its strain, D and the |det| scale (the body of tet_forces_reg)
-template <bool ISO>
-__device__ __forceinline__ void fan_stress(const DevSys &s, uint32_t mi, const float *dtab, const float eps[6],
-                                           float scale, float sig[6])
+// Ring nodes k and k + 3 side by side: edge vectors d from a, values du relative to a's, w = e x d.
+struct RingPair
 {
-    constexpr int kTab = ISO ? 12 : 36;
-    if (s.M == 1)
-        stress_f32<ISO>(s.d1, eps, sig);
-    else if (mi < (uint32_t)kMaxM)
-        stress_f32<ISO>(dtab + kTab * mi, eps, sig);
-    else
+    f2 d[3], du[3], w[3];
+};
+
+__device__ __forceinline__ RingPair ring_pair(const float4 *sxp, const float2 *sq, uint32_t l0, uint32_t l1,
+                                              const float xa[3], const float ua[3], const float e[3])
+{
+    const float4 X0 = sxp[l0], X1 = sxp[l1];
+    const float2 Q0 = sq[l0], Q1 = sq[l1];
+    RingPair P;
+    P.d[0] = f2{X0.x - xa[0], X1.x - xa[0]};
+    P.d[1] = f2{X0.y - xa[1], X1.y - xa[1]};
+    P.d[2] = f2{X0.z - xa[2], X1.z - xa[2]};
+    P.du[0] = f2{X0.w - ua[0], X1.w - ua[0]};
+    P.du[1] = f2{Q0.x - ua[1], Q1.x - ua[1]};
+    P.du[2] = f2{Q0.y - ua[2], Q1.y - ua[2]};
+    P.w[0] = pk_fma(splat(e[1]), P.d[2], -(splat(e[2]) * P.d[1]));
+    P.w[1] = pk_fma(splat(e[2]), P.d[0], -(splat(e[0]) * P.d[2]));
+    P.w[2] = pk_fma(splat(e[0]), P.d[1], -(splat(e[1]) * P.d[0]));
+    return P;
+}
+
+__device__ __forceinline__ RingPair swap_pair(const RingPair &P)
+{
+    RingPair S;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
     {
-        float tab[36];
-        for (int t = 0; t < kTab; ++t)
-            tab[t] = (float)s.dmat[36u * mi + dsrc(ISO, t)];
-        stress_f32<ISO>(tab, eps, sig);
+        S.d[q] = P.d[q].yx;
+        S.du[q] = P.du[q].yx;
+        S.w[q] = P.w[q].yx;
     }
+    return S;
+}
+
+// F += B(g)^T sig (g the corner's unscaled gradient, sig the scaled stress), packed over a tet pair
+__device__ __forceinline__ void corner_acc(const f2 g[3], const f2 sig[6], f2 F[3])
+{
+    F[0] = pk_fma(g[2], sig[5], pk_fma(g[1], sig[3], pk_fma(g[0], sig[0], F[0])));
+    F[1] = pk_fma(g[2], sig[4], pk_fma(g[0], sig[3], pk_fma(g[1], sig[1], F[1])));
+    F[2] = pk_fma(g[0], sig[5], pk_fma(g[1], sig[4], pk_fma(g[2], sig[2], F[2])));
+}
+
+// Tets i (.x) and i + 3 (.y) of the fan: corners {a, b, r_i, r_j} with ring pairs I = (r_i, r_(i+3)) and
+// J = (r_j, r_(j+3)), j = i + 1. With e = x_b - x_a, d_k = x_(r_k) - x_a and w_k = e x d_k, the cofactor rows
+// (unscaled gradients) of corners b, r_i, r_j are d_i x d_j, -w_j and w_i, corner a's minus their sum, so
+// the strain is sum over {b, r_i, r_j} of B(g_k) (u_k - u_a). The stress carries s_K / (6 |det|), masked to 0
+// in a half whose tet does not exist. Forces accumulate on b (Fb), r_i (Fi) and r_j (Fj); corner a's is
+// minus the group's other forces (partition of unity), formed once per group.
+template <bool ISO>
+__device__ __forceinline__ void tet_pair(const RingPair &I, const RingPair &J, const float e[3], const float db[3],
+                                         const float *Dm, float sK6, bool vx, bool vy, f2 Fb[3], f2 Fi[3], f2 Fj[3])
+{
+    f2 g1[3];
+    g1[0] = pk_fma(I.d[1], J.d[2], -(I.d[2] * J.d[1]));
+    g1[1] = pk_fma(I.d[2], J.d[0], -(I.d[0] * J.d[2]));
+    g1[2] = pk_fma(I.d[0], J.d[1], -(I.d[1] * J.d[0]));
+    const f2 det = pk_fma(splat(e[0]), g1[0], pk_fma(splat(e[1]), g1[1], splat(e[2]) * g1[2]));
+    f2 sc = {sK6 * __builtin_amdgcn_rcpf(fabsf(det.x)), sK6 * __builtin_amdgcn_rcpf(fabsf(det.y))};
+    sc.x = vx ? sc.x : 0.f;
+    sc.y = vy ? sc.y : 0.f;
+    const f2 db0 = splat(db[0]), db1 = splat(db[1]), db2 = splat(db[2]);
+    f2 eps[6];
+    eps[0] = pk_fma(-J.w[0], I.du[0], pk_fma(I.w[0], J.du[0], g1[0] * db0));
+    eps[1] = pk_fma(-J.w[1], I.du[1], pk_fma(I.w[1], J.du[1], g1[1] * db1));
+    eps[2] = pk_fma(-J.w[2], I.du[2], pk_fma(I.w[2], J.du[2], g1[2] * db2));
+    eps[3] = pk_fma(g1[0], db1, g1[1] * db0);
+    eps[3] = pk_fma(I.w[0], J.du[1], pk_fma(I.w[1], J.du[0], eps[3]));
+    eps[3] = pk_fma(-J.w[0], I.du[1], pk_fma(-J.w[1], I.du[0], eps[3]));
+    eps[4] = pk_fma(g1[1], db2, g1[2] * db1);
+    eps[4] = pk_fma(I.w[1], J.du[2], pk_fma(I.w[2], J.du[1], eps[4]));
+    eps[4] = pk_fma(-J.w[1], I.du[2], pk_fma(-J.w[2], I.du[1], eps[4]));
+    eps[5] = pk_fma(g1[0], db2, g1[2] * db0);
+    eps[5] = pk_fma(I.w[0], J.du[2], pk_fma(I.w[2], J.du[0], eps[5]));
+    eps[5] = pk_fma(-J.w[0], I.du[2], pk_fma(-J.w[2], I.du[0], eps[5]));
 #pragma unroll
     for (int r = 0; r < 6; ++r)
-        sig[r] *= scale;
-}
-
-__device__ __forceinline__ void cross3(const float u[3], const float v[3], float w[3])
-{
-    w[0] = fmaf(u[1], v[2], -u[2] * v[1]);
-    w[1] = fmaf(u[2], v[0], -u[0] * v[2]);
-    w[2] = fmaf(u[0], v[1], -u[1] * v[0]);
-}
-
-// force on a corner with (unscaled) gradient g from the scaled stress: B(g)^T sig
-__device__ __forceinline__ void corner_force(const float g[3], const float sig[6], float f[3])
-{
-    f[0] = fmaf(g[2], sig[5], fmaf(g[1], sig[3], g[0] * sig[0]));
-    f[1] = fmaf(g[2], sig[4], fmaf(g[0], sig[3], g[1] * sig[1]));
-    f[2] = fmaf(g[0], sig[5], fmaf(g[1], sig[4], g[2] * sig[2]));
-}
-
-// One fan group around edge (a, b): tets i < f are {a, b, r_i, r_j}, j = (i + 1) mod 6. With e = x_b - x_a,
-// d_k = x_(r_k) - x_a and w_k = e x d_k, tet i's cofactor rows (tet_forces_reg's g_1..g_3 for the corner
-// order a, b, r_i, r_j) are d_i x d_j, -w_j and w_i, so each ring node's edge vector and cross product is
-// formed once for the two tets that share it. The ring is walked with a rolling window (ring node i, ring
-// node j; ring node 0 kept for the closing tet), and a ring slot's summed force is pushed as soon as its
-// last tet is done; a, b and ring 0 are pushed at the end. gb: 8 u16 push positions (slots a b r0 .. r5).
-template <bool ISO>
-__device__ __forceinline__ void group_forces(const DevSys &s, uint4 ga, uint4 gb, uint32_t mi, const float4 *sxp,
-                                             const float2 *sq, float sK6, const float *dtab, float2 *sfxy,
-                                             float *sfz)
-{
-    const auto lid = [&](int k) { return ((k < 4 ? ga.x : ga.y) >> (8 * (k & 3))) & 0xffu; };
-    const auto pos = [&](int k) {
-        const uint32_t w = k < 2 ? gb.x : k < 4 ? gb.y : k < 6 ? gb.z : gb.w;
-        return (k & 1) ? w >> 16 : w & 0xffffu;
-    };
-    const auto push = [&](int k, const float F[3]) {
-        const uint32_t q = pos(k);
-        sfxy[q] = float2{F[0], F[1]};
-        sfz[q] = F[2];
-    };
-    const int f = (int)ga.z;
-    const float4 Xa = sxp[lid(0)], Xb = sxp[lid(1)];
-    const float2 Qa = sq[lid(0)], Qb = sq[lid(1)];
-    const float e[3] = {Xb.x - Xa.x, Xb.y - Xa.y, Xb.z - Xa.z};
-    const float ua[3] = {Xa.w, Qa.x, Qa.y};
-    // relative values du_k = u_k - u_a (the strain is sum over k of g_k (x) du_k, g_a = -(g_1 + g_2 + g_3))
-    const float db[3] = {Xb.w - ua[0], Qb.x - ua[1], Qb.y - ua[2]};
-    float Fa[3] = {0.f, 0.f, 0.f}, Fb[3] = {0.f, 0.f, 0.f}, F0[3] = {0.f, 0.f, 0.f};
-    // ring node k: its edge vector from a, its value relative to a's, and e x d (ring node 0 is read again
-    // for the closing tet rather than kept live through the walk)
-    const auto ring = [&](int k, float d[3], float w[3], float du[3]) {
-        const float4 X = sxp[lid(2 + k)];
-        const float2 Q = sq[lid(2 + k)];
-        d[0] = X.x - Xa.x;
-        d[1] = X.y - Xa.y;
-        d[2] = X.z - Xa.z;
-        du[0] = X.w - ua[0];
-        du[1] = Q.x - ua[1];
-        du[2] = Q.y - ua[2];
-        cross3(e, d, w);
-    };
-    float di[3], wi[3], dui[3];
-    ring(0, di, wi, dui);
-    float Fi[3] = {0.f, 0.f, 0.f};  // ring node i's running sum (ring 0's lives in F0)
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
+        eps[r] *= sc;
+    f2 sig[6];
+    if constexpr (ISO)
     {
-        if (i >= f)
-            break;
-        const int j = (i + 1) % 6;
-        float dj[3], wj[3], duj[3];
-        ring(j, dj, wj, duj);
-        // cofactor rows (unscaled gradients) of corners b, r_i, r_j; corner a's is minus their sum
-        float g1[3];
-        cross3(di, dj, g1);
-        const float det = fmaf(e[0], g1[0], fmaf(e[1], g1[1], e[2] * g1[2]));
-        const float scale = sK6 * __builtin_amdgcn_rcpf(fabsf(det));
-        // strain = sum over k in {b, r_i, r_j} of B(g_k) (u_k - u_a): g_b = g1, g_ri = -w_j, g_rj = w_i
-        float eps[6];
-        eps[0] = fmaf(-wj[0], dui[0], fmaf(wi[0], duj[0], g1[0] * db[0]));
-        eps[1] = fmaf(-wj[1], dui[1], fmaf(wi[1], duj[1], g1[1] * db[1]));
-        eps[2] = fmaf(-wj[2], dui[2], fmaf(wi[2], duj[2], g1[2] * db[2]));
-        eps[3] = fmaf(g1[0], db[1], g1[1] * db[0]);
-        eps[3] = fmaf(wi[0], duj[1], fmaf(wi[1], duj[0], eps[3]));
-        eps[3] = fmaf(-wj[0], dui[1], fmaf(-wj[1], dui[0], eps[3]));
-        eps[4] = fmaf(g1[1], db[2], g1[2] * db[1]);
-        eps[4] = fmaf(wi[1], duj[2], fmaf(wi[2], duj[1], eps[4]));
-        eps[4] = fmaf(-wj[1], dui[2], fmaf(-wj[2], dui[1], eps[4]));
-        eps[5] = fmaf(g1[0], db[2], g1[2] * db[0]);
-        eps[5] = fmaf(wi[0], duj[2], fmaf(wi[2], duj[0], eps[5]));
-        eps[5] = fmaf(-wj[0], dui[2], fmaf(-wj[2], dui[0], eps[5]));
-        float sig[6];
-        fan_stress<ISO>(s, mi, dtab, eps, scale, sig);
-        float fb[3], fi[3], fj[3];
-        corner_force(g1, sig, fb);
-        const float mwj[3] = {-wj[0], -wj[1], -wj[2]};
-        corner_force(mwj, sig, fi);
-        corner_force(wi, sig, fj);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-        {
-            Fb[q] += fb[q];
-            Fa[q] -= fb[q] + fi[q] + fj[q];
-        }
-        if (i == 0)
-        {
+        for (int r = 0; r < 3; ++r)
+            sig[r] = pk_fma(splat(Dm[3 * r + 2]), eps[2], pk_fma(splat(Dm[3 * r + 1]), eps[1], splat(Dm[3 * r]) * eps[0]));
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
-                F0[q] += fi[q];
-        }
-        else
-        {
+        for (int r = 3; r < 6; ++r)
+            sig[r] = splat(Dm[6 + r]) * eps[r];
+    }
+    else
+    {
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
-                Fi[q] += fi[q];
-            push(2 + i, Fi);  // ring node i has had both its tets
-        }
-        if (j == 0)
+        for (int r = 0; r < 6; ++r)
         {
+            f2 acc = splat(Dm[6 * r]) * eps[0];
 #pragma unroll
-            for (int q = 0; q < 3; ++q)
-                F0[q] += fj[q];
-        }
-        else
-        {
-#pragma unroll
-            for (int q = 0; q < 3; ++q)
-            {
-                Fi[q] = fj[q];  // ring node j's first tet; its second is the next one
-                di[q] = dj[q];
-                wi[q] = wj[q];
-                dui[q] = duj[q];
-            }
+            for (int c = 1; c < 6; ++c)
+                acc = pk_fma(splat(Dm[6 * r + c]), eps[c], acc);
+            sig[r] = acc;
         }
     }
-    if (f < 6)
-        push(2 + f, Fi);  // the open fan's last ring node (or a closed fan's repeat of ring node 0)
-    push(2, F0);
-    push(0, Fa);
-    push(1, Fb);
+    const f2 mwj[3] = {-J.w[0], -J.w[1], -J.w[2]};
+    corner_acc(g1, sig, Fb);
+    corner_acc(mwj, sig, Fi);
+    corner_acc(I.w, sig, Fj);
 }
 
-template <bool ISO, bool SANITIZE, int MODE, int NT>
+// One fan group around edge (a, b). Record g: slot s (0 = a, 1 = b, 2 + k = ring node k) has local id
+// byte s of {g.x, g.y} and rank nibble s of g.z; f = g.w & 7 tets {a, b, r_i, r_(i+1)}, i < f (ring slot 6
+// is ring slot 0: a closed 6-fan; a closed fan of f < 6 repeats r_0 in ring slot f). Used slots: a, b and
+// ring slots 0 .. min(f + 1, 6) - 1.
+template <bool ISO>
+__device__ __forceinline__ void group_forces(uint4 g, const float4 *sxp, const float2 *sq, const uint16_t *sst,
+                                             float sK6, const float *Dm, float2 *sfxy, float *sfz)
+{
+    const auto lid = [&](int k) { return ((k < 4 ? g.x : g.y) >> (8 * (k & 3))) & 0xffu; };
+    const auto push = [&](int k, float fx, float fy, float fz) {
+        const uint32_t l = lid(k);
+        const uint32_t q = (uint32_t)sst[l] + ((g.z >> (4 * k)) & 15u);
+        sfxy[q] = float2{fx, fy};
+        sfz[q] = fz;
+    };
+    const int f = (int)(g.w & 7u);
+    const float4 Xa = sxp[lid(0)], Xb = sxp[lid(1)];
+    const float2 Qa = sq[lid(0)], Qb = sq[lid(1)];
+    const float xa[3] = {Xa.x, Xa.y, Xa.z};
+    const float ua[3] = {Xa.w, Qa.x, Qa.y};
+    const float e[3] = {Xb.x - Xa.x, Xb.y - Xa.y, Xb.z - Xa.z};
+    const float db[3] = {Xb.w - ua[0], Qb.x - ua[1], Qb.y - ua[2]};
+    const RingPair P0 = ring_pair(sxp, sq, lid(2), lid(5), xa, ua, e);
+    const RingPair P1 = ring_pair(sxp, sq, lid(3), lid(6), xa, ua, e);
+    f2 Fb[3] = {}, F0[3] = {}, F1[3] = {}, F2[3] = {}, F3[3] = {};
+    // pair 0: tets 0, 3 (ring pairs 0, 1)
+    tet_pair<ISO>(P0, P1, e, db, Dm, sK6, f > 0, f > 3, Fb, F0, F1);
+    const RingPair P2 = ring_pair(sxp, sq, lid(4), lid(7), xa, ua, e);
+    // pair 1: tets 1, 4 (ring pairs 1, 2); ring nodes 1 and 4 are complete after it
+    tet_pair<ISO>(P1, P2, e, db, Dm, sK6, f > 1, f > 4, Fb, F1, F2);
+    push(3, F1[0].x, F1[1].x, F1[2].x);
+    if (f >= 4)
+        push(6, F1[0].y, F1[1].y, F1[2].y);
+    // pair 2: tets 2, 5 (ring pairs 2, 3 = ring pair 0 swapped: ring slot 6 is ring slot 0)
+    tet_pair<ISO>(P2, swap_pair(P0), e, db, Dm, sK6, f > 2, f > 5, Fb, F2, F3);
+    if (f >= 2)
+        push(4, F2[0].x, F2[1].x, F2[2].x);
+    if (f >= 5)
+        push(7, F2[0].y, F2[1].y, F2[2].y);
+    // ring node 0 = F0.x + F3.y, ring node 3 = F0.y + F3.x; a = -(everything else)
+    float r0[3], r3[3], fb[3], fa[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+    {
+        r0[q] = F0[q].x + F3[q].y;
+        r3[q] = F0[q].y + F3[q].x;
+        fb[q] = Fb[q].x + Fb[q].y;
+        const f2 s12 = F1[q] + F2[q];
+        fa[q] = -(((fb[q] + r0[q]) + r3[q]) + (s12.x + s12.y));
+    }
+    push(2, r0[0], r0[1], r0[2]);
+    if (f >= 3)
+        push(5, r3[0], r3[1], r3[2]);
+    push(0, fa[0], fa[1], fa[2]);
+    push(1, fb[0], fb[1], fb[2]);
+}
+
+// MONO: one material, D from the kernel arguments (SGPR operands); otherwise the group's material selects
+// a row of the LDS table (<= 16 materials, abi.cpp)
+template <bool ISO, bool SANITIZE, int MODE, int NT, bool MONO>
 __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
                                                          const uint4 *__restrict__ hdr)
 {
@@ -1155,7 +1164,8 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
     float *sfz = lds + 2 * SP;                                // [SP]
     float4 *sxp = reinterpret_cast<float4 *>(lds + 3 * SP);  // [MS] {x, y, z, v_x}
     float2 *sq = reinterpret_cast<float2 *>(sxp + MS);       // [MS] {v_y, v_z}
-    __shared__ float dtab[kMaxM * kTab];
+    uint16_t *sst = reinterpret_cast<uint16_t *>(sq + MS);   // [MS] run start in the local CSR
+    __shared__ float dtab[MONO ? 1 : kMaxM * kTab];
     __shared__ double red[NT / 64];
     if constexpr (MODE == 1)
     {
@@ -1170,12 +1180,15 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
     uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
     if (t < t_end)
     {
-        group_issue_records<NT, SANITIZE, MODE>(s, hd, cur);
+        group_issue_records<NT>(s, hd, cur);
         group_issue_gather<SANITIZE, MODE>(s, x, pa.z, cur);
     }
-    const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
-    for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
-        dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
+    if constexpr (!MONO)
+    {
+        const uint32_t nm = s.M < kMaxM ? s.M : kMaxM;
+        for (uint32_t i = threadIdx.x; i < nm * kTab; i += NT)
+            dtab[i] = (float)s.dmat[36u * (i / kTab) + dsrc(ISO, i % kTab)];
+    }
     float beta = 0.f;
     if constexpr (MODE == 1)
     {
@@ -1203,10 +1216,10 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
                 }
                 sxp[i] = float4{cur.c[k][0], cur.c[k][1], cur.c[k][2], v0};
                 sq[i] = float2{v1, v2};
+                sst[i] = (uint16_t)(cur.tn[k].y & 0xffffu);
             }
         }
-        const uint4 ga = cur.ga, gb = cur.gb;
-        const uint32_t gm = cur.gm;
+        const uint4 gr = cur.g;
         const uint2 tn_own[2] = {cur.tn[0], cur.tn[1]};
         const uint32_t slot_own[2] = {cur.slot[0], cur.slot[1]};
         const float m_own[2] = {cur.m[0], cur.m[1]};
@@ -1215,11 +1228,14 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
         const uint32_t tn_next = t + nbx;
         const uint4 hdn = hd2;
         if (tn_next < t_end)
-            group_issue_records<NT, SANITIZE, MODE>(s, hdn, cur);
+            group_issue_records<NT>(s, hdn, cur);
         hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
         // (c) this lane's group (ablation bit 64: skipped, diagnostic timing only)
         if (threadIdx.x < ng && !(pa.abl & 64u))
-            group_forces<ISO>(s, ga, gb, gm, sxp, sq, sK6, dtab, sfxy, sfz);
+        {
+            const float *Dm = MONO ? s.d1 : dtab + kTab * (gr.w >> 3);
+            group_forces<ISO>(gr, sxp, sq, sst, sK6, Dm, sfxy, sfz);
+        }
         __syncthreads();
         // (d) next tile's gathers (ablation bit 256: skipped)
         if (tn_next < t_end && !(pa.abl & 256u))
@@ -1592,29 +1608,40 @@ void launch_pipe(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t
         k_keff_tiles_pipe<ISO, SAN, MODE, NT><<<s.t.pipe_grid, NT, lds, st>>>(s, x, pa, s.t.hdr);
 }
 
-constexpr size_t kGroupLds = sizeof(float) * 3 * kGroupSlots + 2 * kGroupThreads * (16 + 8);
+// pushed forces {f_x, f_y} + f_z per slot, then per tile node {x y z v_x} {v_y v_z} and its u16 run start
+constexpr size_t kGroupLds = sizeof(float) * 3 * kGroupSlots + 2 * kGroupThreads * (16 + 8 + 2);
 
-template <bool ISO>
+template <bool ISO, bool MONO>
 unsigned group_grid_query()
 {
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_groups_pipe<ISO, false, 1, kGroupThreads>,
-                                                       kGroupThreads, kGroupLds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &bpc, k_keff_groups_pipe<ISO, false, 1, kGroupThreads, MONO>, kGroupThreads, kGroupLds);
     unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     return g < 8u ? 8u : g - g % 8u;  // whole XCD groups
+}
+
+template <bool ISO, bool SAN, int MODE, bool MONO>
+void launch_groups_m(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0,
+                     hipEvent_t e1)
+{
+    if (e0 && e1)
+        hipExtLaunchKernelGGL(k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads, MONO>, dim3(s.t.pipe_grid),
+                              dim3(kGroupThreads), (uint32_t)kGroupLds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+    else
+        k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads, MONO><<<s.t.pipe_grid, kGroupThreads, kGroupLds, st>>>(
+            s, x, pa, s.t.hdr);
 }
 
 template <bool ISO, bool SAN, int MODE>
 void launch_groups(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
-    if (e0 && e1)
-        hipExtLaunchKernelGGL(k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads>, dim3(s.t.pipe_grid),
-                              dim3(kGroupThreads), (uint32_t)kGroupLds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+    if (s.M == 1)
+        launch_groups_m<ISO, SAN, MODE, true>(s, x, pa, st, e0, e1);
     else
-        k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads><<<s.t.pipe_grid, kGroupThreads, kGroupLds, st>>>(
-            s, x, pa, s.t.hdr);
+        launch_groups_m<ISO, SAN, MODE, false>(s, x, pa, st, e0, e1);
 }
 
 // e0/e1 (optional): hipExtLaunchKernel stamps them from the dispatch packet itself, so the timed
@@ -1658,7 +1685,8 @@ unsigned fast_pipe_grid(const DevSys &s)
 {
     if (s.t.grp)
     {
-        const unsigned g = s.iso ? group_grid_query<true>() : group_grid_query<false>();
+        const unsigned g = s.iso ? (s.M == 1 ? group_grid_query<true, true>() : group_grid_query<true, false>())
+                                 : (s.M == 1 ? group_grid_query<false, true>() : group_grid_query<false, false>());
         const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
         return g < need ? g : (need ? need : 8u);
     }
