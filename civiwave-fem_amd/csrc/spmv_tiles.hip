@@ -55,21 +55,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t whole_rsrc(const void *base)
 // 12-B store at float index 3 q; wt: write-through (sc1), so the line leaves L2 during the kernel instead of
 // in the end-of-kernel write-back the next launch waits for (the update pass's x / r / z: C2 +2.7% PCG it/s,
 // C3 neutral, same-box A/B; the tiles kernel's scattered partial / p stores measured 5% slower that way)
+// (one buffer_store_dwordx3 either way; base: the buffer the descriptor covers)
 __device__ __forceinline__ void store3(float *base, __amdgpu_buffer_rsrc_t rs, uint64_t q, float a, float b, float c,
                                        bool wt)
 {
+    (void)base;
+    const u32x3 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c)};
     if (wt)
-    {
-        const u32x3 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c)};
         __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 16);
-    }
     else
-    {
-        float *o = base + 3ull * q;
-        o[0] = a;
-        o[1] = b;
-        o[2] = c;
-    }
+        __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 0);
 }
 
 // NT-thread block sum in a fixed order; result valid in every thread. red: NT/64 doubles.
@@ -956,23 +951,30 @@ __device__ __forceinline__ void group_issue_records(const DevSys &s, uint4 hd, G
     n.g = T.grec[g0 + (threadIdx.x < ng ? threadIdx.x : 0u)];
 }
 
+// one 12-B node triple per lane in a single buffer_load_dwordx3 (three dword gathers cost three address
+// walks of the wave's 64 scattered lines)
+__device__ __forceinline__ void load3(__amdgpu_buffer_rsrc_t rs, uint32_t q, float v[3])
+{
+    const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(rs, 12u * q, 0, 0);
+    v[0] = __uint_as_float(w.x);
+    v[1] = __uint_as_float(w.y);
+    v[2] = __uint_as_float(w.z);
+}
+
 template <bool SANITIZE, int MODE>
 __device__ __forceinline__ void group_issue_gather(const DevSys &s, const float *__restrict__ x,
                                                    const float *__restrict__ z, GroupNext &n)
 {
+    const __amdgpu_buffer_rsrc_t rx = whole_rsrc(x);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
     {
         const uint32_t g = n.tn[k].x & 0x7fffffffu;  // node 0 for idle lanes (harmless, in range)
         n.m[k] = 0.f;
-        n.v[k][0] = x[3u * g + 0];
-        n.v[k][1] = x[3u * g + 1];
-        n.v[k][2] = x[3u * g + 2];
+        load3(rx, g, n.v[k]);
         if constexpr (MODE == 1)
         {
-            n.w[k][0] = z[3u * g + 0];
-            n.w[k][1] = z[3u * g + 1];
-            n.w[k][2] = z[3u * g + 2];
+            load3(whole_rsrc(z), g, n.w[k]);
             n.m[k] = s.mass[g];
         }
         else if constexpr (SANITIZE)
@@ -1263,21 +1265,11 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
                         a1 = fmaf(m, p1, a1);
                         a2 = fmaf(m, p2, a2);
                         if (pa.pnew)  // and stores the new p for the update pass
-                        {
-                            float *q = pa.pnew + 3ull * (tn.x & 0x7fffffffu);
-                            q[0] = p0;
-                            q[1] = p1;
-                            q[2] = p2;
-                        }
+                            store3(pa.pnew, whole_rsrc(pa.pnew), tn.x & 0x7fffffffu, p0, p1, p2, false);
                     }
                 }
                 if (!(pa.abl & 512u))
-                {
-                    float *o = T.part + 3ull * slot_own[k];
-                    o[0] = a0;
-                    o[1] = a1;
-                    o[2] = a2;
-                }
+                    store3(T.part, whole_rsrc(T.part), slot_own[k], a0, a1, a2, false);
                 if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
                     pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
             }

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <vector>
 namespace cwf { int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems, int corners); }
+// usage (fan groups): /tmp/tile_stats NX NY NZ MAX_NODES GROUPS_PER_TILE g  (needs groups.cpp on the build line)
 int main(int argc, char **argv)
 {
     int nx = atoi(argv[1]), ny = atoi(argv[2]), nz = atoi(argv[3]);
@@ -24,6 +25,15 @@ int main(int argc, char **argv)
     cwf_system_desc d{};
     d.element_gradients = gr.data(); d.element_volume = vol.data();
     d.node_count = N; d.element_count = E; d.element_connectivity = conn.data(); d.node_coords = xyz.data(); d.material_count = 1;
+    if (argc > 6 && argv[6][0] == 'g')
+    {
+        cwf::GroupTiles gt;
+        int st = cwf::build_group_tiles(&d, gt, me, mn, 1u << 20);
+        double T = gt.tile_nodes.size();
+        printf("groups: status %d N=%lu G=%u tiles=%u T=%.0f T/N=%.3f nn_avg=%.1f max_nn=%u max_slots=%u\n", st, N,
+               gt.ngroups, gt.ntiles, T, T / N, T / gt.ntiles, gt.max_tile_nodes, gt.max_tile_slots);
+        return 0;
+    }
     cwf::HostTiles ht;
     cwf::build_tiles(&d, ht, mn, me, 4);
     double T = ht.tile_nodes.size();
