@@ -658,9 +658,13 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             {
                 GroupTiles gt;
                 int gst = -1;
+                // 256-lane tiles (<= 256 groups, <= 512 nodes: T/N 1.59 against 1.77 on C3) where the mesh
+                // gives every resident workgroup several tiles; CWF_GROUP_NT=128|256 overrides
+                const char *gn = getenv("CWF_GROUP_NT");
+                const uint32_t gnt = gn ? (atoi(gn) == 256 ? 256u : 128u) : (E >= 4000000ull ? 256u : 128u);
                 try
                 {
-                    gst = build_group_tiles(d, gt, kGroupThreads, kGroupMaxNodes, kGroupSlots);
+                    gst = build_group_tiles(d, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt);
                 }
                 catch (const std::bad_alloc &)
                 {
@@ -714,7 +718,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     t.node_major = 1;
                     t.push = 1;
                     t.pipe = 1;
-                    t.pipe_nt = (int)kGroupThreads;
+                    t.pipe_nt = (int)gnt;
                     t.ntiles = gt.ntiles;
                     t.ngroups = gt.ngroups;
                     t.max_tile_nodes = gt.max_tile_nodes;

@@ -25,10 +25,11 @@ namespace cwf
 constexpr int kTileElems = 512;      // elements per tile (= per 256-thread workgroup)
 constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two node slots per thread)
 constexpr uint32_t kHexTileThreads = 128;  // hex8 tiles: <= 128 hexes and <= 256 nodes per 128-lane workgroup
-constexpr uint32_t kGroupThreads = 128;    // fan-group tiles: <= 128 groups (one per lane) ...
-constexpr uint32_t kGroupMaxNodes = 256;   // ... <= 256 nodes (two per lane; u8 local ids) ...
-constexpr uint32_t kGroupSlots = 1536;     // ... and <= 1536 pushed-force slots (padded runs, LDS) ...
-constexpr uint32_t kGroupMaxRun = 16;      // ... and <= 16 pushes per tile node (4-bit ranks in the record)
+// fan-group tiles of NT = 128 (meshes < 4M tets) or 256 lanes: <= NT groups (one per lane), <= 2 NT nodes
+// (two per lane; 9-bit local ids), <= kGroupSlotsPerLane NT pushed-force slots (padded runs, LDS) and <= 16
+// pushes per tile node (4-bit ranks in the record)
+constexpr uint32_t kGroupSlotsPerLane = 12;
+constexpr uint32_t kGroupMaxRun = 16;
 
 struct DevTiles
 {
@@ -55,8 +56,8 @@ struct DevTiles
     // tet fan groups (groups.cpp): k_keff_groups_pipe, one group per lane, pushes per group node
     int grp = 0;
     uint32_t ngroups = 0;
-    // [G] {u8 local node ids of slots a b r0 r1, of r2 .. r5, 8 x 4-bit ranks in the slots' runs,
-    //      tet count f | material << 3}
+    // [G] 9-bit local node ids of slots 0..7 (a b r0 .. r5), 3 per word in words 0-2 (bits 0-26), tet
+    //     count f in word 0 bits 27-29, material in word 1 bits 27-31; word 3: 8 x 4-bit ranks in the runs
     const uint4 *grec = nullptr;
     // native hex8: k_keff_hex_tiles, 128-thread persistent grid (pipe_grid), push fold
     int hex = 0;
@@ -110,8 +111,9 @@ struct GroupTiles
 {
     uint32_t ntiles = 0, ngroups = 0, max_tile_nodes = 0, max_tile_slots = 0;
     double tets_per_group = 0.0;
-    // [G] {a b r0 r1 (u8 local ids), r2 r3 r4 r5, 4-bit rank of each used slot in its node's run (push
-    // position = run start + rank), tet count f | material << 3 (groups are single-material)}
+    // [G] 9-bit local ids of slots a b r0 .. r5 (3 per word, words 0-2), f << 27 in word 0, material << 27
+    // in word 1 (groups are single-material), word 3: the 4-bit rank of each used slot in its node's run
+    // (push position = run start + rank)
     std::vector<uint4> grec;
     std::vector<uint4> hdr;                // [ntiles] {first group, #groups, first tile node, #nodes}
     std::vector<uint32_t> tile_nodes;      // [T] global node | owner bit 31
@@ -120,7 +122,7 @@ struct GroupTiles
     std::vector<uint32_t> node_part_off, tile_slot;  // [N+1] node -> slot range; [T] node-major slot
     std::vector<uint32_t> tet_group;       // [E] group of each tet (validation)
 };
-// nt: lanes per workgroup (one group per lane); max_nodes <= 256 (u8 local ids); slot_budget: LDS push slots
+// nt: lanes per workgroup (one group per lane); max_nodes <= 512 (9-bit local ids); slot_budget: LDS push slots
 int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
                       uint32_t slot_budget);
 

@@ -155,7 +155,7 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
     const uint64_t N = d->node_count, E = d->element_count;
     const uint32_t *conn = d->element_connectivity;
     const uint32_t *mat = d->material_count > 1 ? d->element_material_index : nullptr;
-    if (!d->node_coords || !E || max_nodes > 256)
+    if (!d->node_coords || !E || max_nodes > 512 || d->material_count > 32)
         return -1;
     // node -> tets, ascending tet
     std::vector<uint32_t> off(N + 1, 0), lst(4 * E);
@@ -347,6 +347,8 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
             if (padded <= slot_budget || !spread)
                 break;
         }
+        if (out.max_tile_slots > slot_budget)
+            return -3;  // cannot happen for slot_budget >= 10 nt: <= 8 pushes per group + 1 pad per node
         cur.assign(start.begin(), start.end());
         const uint32_t nb = (uint32_t)out.tile_nodes.size();
         for (uint64_t q = p0; q < p; ++q)
@@ -362,9 +364,9 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
                 if (s < slots_used(F))
                     ranks |= (cur[id[s]]++ - start[id[s]]) << (4 * s);  // < kGroupMaxRun (tile loop above)
             }
-            out.grec[gi] = uint4{id[0] | id[1] << 8 | id[2] << 16 | id[3] << 24,
-                                 id[4] | id[5] << 8 | id[6] << 16 | id[7] << 24, ranks,
-                                 (uint32_t)F.f | (mat ? mat[F.t[0]] : 0u) << 3};
+            out.grec[gi] = uint4{id[0] | id[1] << 9 | id[2] << 18 | (uint32_t)F.f << 27,
+                                 id[3] | id[4] << 9 | id[5] << 18 | (mat ? mat[F.t[0]] : 0u) << 27,
+                                 id[6] | id[7] << 9, ranks};
         }
         const double *o = d->node_coords + 3ull * nodes[0];
         for (uint32_t i = 0; i < nn; ++i)

@@ -1095,22 +1095,22 @@ __device__ __forceinline__ void tet_pair(const RingPair &I, const RingPair &J, c
     corner_acc(I.w, sig, Fj);
 }
 
-// One fan group around edge (a, b). Record g: slot s (0 = a, 1 = b, 2 + k = ring node k) has local id
-// byte s of {g.x, g.y} and rank nibble s of g.z; f = g.w & 7 tets {a, b, r_i, r_(i+1)}, i < f (ring slot 6
+// One fan group around edge (a, b). Record g: slot s (0 = a, 1 = b, 2 + k = ring node k) has the 9-bit local
+// id s % 3 of word s / 3 and rank nibble s of g.w; f = g.x >> 27 tets {a, b, r_i, r_(i+1)}, i < f (ring slot 6
 // is ring slot 0: a closed 6-fan; a closed fan of f < 6 repeats r_0 in ring slot f). Used slots: a, b and
 // ring slots 0 .. min(f + 1, 6) - 1.
 template <bool ISO>
 __device__ __forceinline__ void group_forces(uint4 g, const float4 *sxp, const float2 *sq, const uint16_t *sst,
                                              float sK6, const float *Dm, float2 *sfxy, float *sfz)
 {
-    const auto lid = [&](int k) { return ((k < 4 ? g.x : g.y) >> (8 * (k & 3))) & 0xffu; };
+    const auto lid = [&](int k) { return ((k < 3 ? g.x : k < 6 ? g.y : g.z) >> (9 * (k % 3))) & 0x1ffu; };
     const auto push = [&](int k, float fx, float fy, float fz) {
         const uint32_t l = lid(k);
-        const uint32_t q = (uint32_t)sst[l] + ((g.z >> (4 * k)) & 15u);
+        const uint32_t q = (uint32_t)sst[l] + ((g.w >> (4 * k)) & 15u);
         sfxy[q] = float2{fx, fy};
         sfz[q] = fz;
     };
-    const int f = (int)(g.w & 7u);
+    const int f = (int)((g.x >> 27) & 7u);
     const float4 Xa = sxp[lid(0)], Xb = sxp[lid(1)];
     const float2 Qa = sq[lid(0)], Qb = sq[lid(1)];
     const float xa[3] = {Xa.x, Xa.y, Xa.z};
@@ -1159,7 +1159,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
                                                          const uint4 *__restrict__ hdr)
 {
     constexpr int kTab = ISO ? 12 : 36;
-    constexpr int SP = (int)kGroupSlots, MS = 2 * NT;
+    constexpr int SP = (int)kGroupSlotsPerLane * NT, MS = 2 * NT;
     extern __shared__ float lds[];
     const DevTiles &T = s.t;
     float2 *sfxy = reinterpret_cast<float2 *>(lds);           // [SP]
@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
         // (c) this lane's group (ablation bit 64: skipped, diagnostic timing only)
         if (threadIdx.x < ng && !(pa.abl & 64u))
         {
-            const float *Dm = MONO ? s.d1 : dtab + kTab * (gr.w >> 3);
+            const float *Dm = MONO ? s.d1 : dtab + kTab * (gr.y >> 27);
             group_forces<ISO>(gr, sxp, sq, sst, sK6, Dm, sfxy, sfz);
         }
         __syncthreads();
@@ -1601,39 +1601,47 @@ void launch_pipe(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t
 }
 
 // pushed forces {f_x, f_y} + f_z per slot, then per tile node {x y z v_x} {v_y v_z} and its u16 run start
-constexpr size_t kGroupLds = sizeof(float) * 3 * kGroupSlots + 2 * kGroupThreads * (16 + 8 + 2);
+constexpr size_t group_lds(int nt) { return sizeof(float) * 3 * kGroupSlotsPerLane * nt + 2 * nt * (16 + 8 + 2); }
 
-template <bool ISO, bool MONO>
+template <bool ISO, bool MONO, int NT>
 unsigned group_grid_query()
 {
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &bpc, k_keff_groups_pipe<ISO, false, 1, kGroupThreads, MONO>, kGroupThreads, kGroupLds);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_keff_groups_pipe<ISO, false, 1, NT, MONO>, NT,
+                                                       group_lds(NT));
     unsigned g = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     return g < 8u ? 8u : g - g % 8u;  // whole XCD groups
 }
 
-template <bool ISO, bool SAN, int MODE, bool MONO>
+template <bool ISO, bool SAN, int MODE, bool MONO, int NT>
 void launch_groups_m(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0,
                      hipEvent_t e1)
 {
+    constexpr uint32_t lds = (uint32_t)group_lds(NT);
     if (e0 && e1)
-        hipExtLaunchKernelGGL(k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads, MONO>, dim3(s.t.pipe_grid),
-                              dim3(kGroupThreads), (uint32_t)kGroupLds, st, e0, e1, 0, s, x, pa, s.t.hdr);
+        hipExtLaunchKernelGGL(k_keff_groups_pipe<ISO, SAN, MODE, NT, MONO>, dim3(s.t.pipe_grid), dim3(NT), lds, st,
+                              e0, e1, 0, s, x, pa, s.t.hdr);
     else
-        k_keff_groups_pipe<ISO, SAN, MODE, kGroupThreads, MONO><<<s.t.pipe_grid, kGroupThreads, kGroupLds, st>>>(
-            s, x, pa, s.t.hdr);
+        k_keff_groups_pipe<ISO, SAN, MODE, NT, MONO><<<s.t.pipe_grid, NT, lds, st>>>(s, x, pa, s.t.hdr);
 }
 
 template <bool ISO, bool SAN, int MODE>
 void launch_groups(const DevSys &s, const float *x, const PcgArgs &pa, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
-    if (s.M == 1)
-        launch_groups_m<ISO, SAN, MODE, true>(s, x, pa, st, e0, e1);
+    if (s.t.pipe_nt == 256)
+        s.M == 1 ? launch_groups_m<ISO, SAN, MODE, true, 256>(s, x, pa, st, e0, e1)
+                 : launch_groups_m<ISO, SAN, MODE, false, 256>(s, x, pa, st, e0, e1);
     else
-        launch_groups_m<ISO, SAN, MODE, false>(s, x, pa, st, e0, e1);
+        s.M == 1 ? launch_groups_m<ISO, SAN, MODE, true, 128>(s, x, pa, st, e0, e1)
+                 : launch_groups_m<ISO, SAN, MODE, false, 128>(s, x, pa, st, e0, e1);
+}
+
+template <bool ISO, bool MONO>
+unsigned group_grid(int nt)
+{
+    return nt == 256 ? group_grid_query<ISO, MONO, 256>() : group_grid_query<ISO, MONO, 128>();
 }
 
 // e0/e1 (optional): hipExtLaunchKernel stamps them from the dispatch packet itself, so the timed
@@ -1677,8 +1685,9 @@ unsigned fast_pipe_grid(const DevSys &s)
 {
     if (s.t.grp)
     {
-        const unsigned g = s.iso ? (s.M == 1 ? group_grid_query<true, true>() : group_grid_query<true, false>())
-                                 : (s.M == 1 ? group_grid_query<false, true>() : group_grid_query<false, false>());
+        const int nt = s.t.pipe_nt;
+        const unsigned g = s.iso ? (s.M == 1 ? group_grid<true, true>(nt) : group_grid<true, false>(nt))
+                                 : (s.M == 1 ? group_grid<false, true>(nt) : group_grid<false, false>(nt));
         const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
         return g < need ? g : (need ? need : 8u);
     }
