@@ -316,6 +316,9 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         if (set.check_interval <= 0)
             batch = std::min<uint64_t>(batch * 2, kMaxBatch);
     }
+    if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
+        for (size_t i = 0; i < g.size(); ++i)
+            fast_flush_x(g[i], rhs[i], g[i]->stream);
     if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows
     {
         if (int e = comm_halo(g, &cwf_hip_system::x))
@@ -927,7 +930,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     }
     // solver scratch
     const uint64_t D = 3 * N;
-    for (float **v : {&h->x, &h->r, &h->p, &h->p2, &h->z, &h->Ap, &h->rhs, &h->tmp})
+    for (float **v : {&h->x, &h->r, &h->p, &h->p2, &h->p3, &h->p4, &h->z, &h->Ap, &h->rhs, &h->tmp})
         if (int st = dalloc(h, v, D))
             return bail(st);
     if (int st = dalloc(h, &h->inv, 9 * N))

@@ -126,7 +126,10 @@ struct GroupTiles
 int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
                       uint32_t slot_budget);
 
-constexpr uint32_t kPartOffBits = 0x1fffffffu;  // node_part_off value bits (the rest: bc_mask, off_mask)
+constexpr uint32_t kPartOffBits = 0x1fffffffu;
+// FAST PCG applies x += alpha_j p_j every kXLag iterations, from the last kXLag search directions (one p
+// buffer each, rotating), instead of re-reading x and p every iteration
+constexpr unsigned kXLag = 4;  // node_part_off value bits (the rest: bc_mask, off_mask)
 
 struct DevSys
 {
@@ -166,6 +169,7 @@ struct Ctl
     int error;       // cwf_status (0 = none)
     int error_iter;  // iteration index for the error context
     double rho2[2];  // FAST: rho by iteration parity (written by one kernel, read by the next)
+    double alpha_h[kXLag];  // FAST: alpha of iteration j at [j % kXLag] (the lazy x update, spmv_tiles.hip)
 };
 
 struct DevBuf
@@ -190,7 +194,7 @@ struct cwf_hip_system
     // solver scratch (f32 dofs) and partials
     // Ap is scratch (apply_keff staging, PARITY's K p, the prologues' K x); FAST PCG never reads it
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
-    float *p2 = nullptr;    // FAST: the search direction of odd iterations (p / p2 ping-pong, spmv_tiles.hip)
+    float *p2 = nullptr, *p3 = nullptr, *p4 = nullptr;  // FAST: p_j lives in {p, p2, p3, p4}[(j + 1) % 4]
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
@@ -277,6 +281,7 @@ void fast_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStrea
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream_t st);
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
+void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st);  // the lazy x terms still pending
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);

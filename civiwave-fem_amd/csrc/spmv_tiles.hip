@@ -35,6 +35,16 @@ namespace
 constexpr int kMaxM = 16;
 constexpr int kUpdThreads = 256;
 constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
+// CWF_UPD_U=1|2 (diagnostic): owned nodes per update-pass thread and loop trip (default 1: 2 measured 4-5%
+// slower on C2 and C3, its registers cost more occupancy than the extra loads in flight gain)
+static int upd_unroll()
+{
+    static const int v = [] {
+        const char *e = getenv("CWF_UPD_U");
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -1376,13 +1386,33 @@ __global__ __launch_bounds__(256) void k_keff_finalize(DevSys s, const float *__
     y[3u * n + 2] = (mk & 4u) ? x2 : y2;
 }
 
+// The four rotating search-direction buffers: p_j lives in p[(j + 1) % 4] (fast_p_buf)
+struct PBufs
+{
+    const float *p[4];
+};
+
+// Per-node state of the update pass, loaded in phases so that U nodes per thread have their loads in
+// flight together (the pass is latency-bound: node_part_off -> partial run is a dependent chain)
+struct UpdNode
+{
+    uint32_t n, q0, q1, mk;
+    bool ok;
+    float rv0[3], pa[3], pb[3], pv[3], m;
+    uint4 iw;
+    float xv[3], pj[kXLag][3];
+};
+
+// pcg.cpp:840-895 per owned node: Ap from the node-major partials (folded in ascending tile order),
+// r -= alpha Ap, Dirichlet, z = M^-1 r (16-B Jacobi-scaled block, blockinv_pack.hpp), r.r / r.z shares;
+// x += alpha_j p_j for the last `lag` iterations every lag-th iteration (lazy x, 1 = every iteration; the
+// FMA chain in iteration order is bitwise the eager update), fast_flush_x applies the rest after the solve.
+template <int U>
 __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, const float *__restrict__ inv9,
-    float *__restrict__ x,
-    float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold, float *__restrict__ pnew,
-    Ctl *__restrict__ ctl,
-    const double *__restrict__ part_dot, unsigned ntp, double *__restrict__ prr, double *__restrict__ prz,
-    unsigned it, int wt)
+    float *__restrict__ x, float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold,
+    float *__restrict__ pnew, Ctl *__restrict__ ctl, const double *__restrict__ part_dot, unsigned ntp,
+    double *__restrict__ prr, double *__restrict__ prz, unsigned it, int wt, PBufs pbuf, unsigned lag)
 {
     __shared__ double red[kUpdThreads / 64];
     if (!ctl->active)
@@ -1406,135 +1436,181 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         ctl->denom = denom;
         ctl->alpha = alpha_d;
         ctl->alpha_last = alpha_d;
+        ctl->alpha_h[it % kXLag] = alpha_d;
+    }
+    const bool xflush = (it + 1u) % lag == 0u;
+    float aj[kXLag];  // alpha of iteration it + 1 - lag + j
+#pragma unroll
+    for (unsigned j = 0; j < kXLag; ++j)
+    {
+        const unsigned ij = it + 1u - lag + j;
+        aj[j] = j < lag ? (float)(ij == it ? alpha_d : ctl->alpha_h[ij % kXLag]) : 0.f;
     }
     const DevTiles &T = s.t;
     const float alpha = (float)alpha_d, beta = (float)ctl->beta;
     const float sM = (float)s.sM;
+    const __amdgpu_buffer_rsrc_t rpart = whole_rsrc(T.part);
     double rr = 0.0, rz = 0.0;
-    for (uint32_t n = blockIdx.x * kUpdThreads + threadIdx.x; n < s.N; n += gridDim.x * kUpdThreads)
+    const uint32_t step = gridDim.x * kUpdThreads * U;
+    for (uint32_t base = blockIdx.x * kUpdThreads * U + threadIdx.x; base < s.Nown; base += step)
     {
-        if (n >= s.Nown)  // ghost node of a shard: only its search direction (the tiles kernel's p) is kept
+        UpdNode v[U];
+        // (1) the partial-run bounds (and the Dirichlet mask in their top bits)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
         {
+            v[u].n = base + u * kUpdThreads;
+            v[u].ok = v[u].n < s.Nown;
+            const uint32_t n = v[u].ok ? v[u].n : 0u;
+            const uint32_t o0 = T.node_part_off[n], o1 = T.node_part_off[n + 1];
+            v[u].q0 = o0 & kPartOffBits;
+            v[u].q1 = o1 & kPartOffBits;
+            v[u].mk = T.off_mask ? o0 >> 29 : s.mask[n];
+        }
+        // (2) every independent load of the U nodes
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            UpdNode &w = v[u];
+            const uint32_t n = w.ok ? w.n : 0u;
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                pnew[3u * n + k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
-            continue;
+                w.rv0[k] = r[3u * n + k];
+            w.iw = reinterpret_cast<const uint4 *>(inv)[n];
+            // first two partials unconditionally (the part buffer carries 2 padding slots)
+            if (T.node_major)
+            {
+                load3(rpart, w.q0, w.pa);
+                load3(rpart, w.q0 + 1, w.pb);
+            }
+            // a node of no element forms p_it here (Ap = m s_M p); the tiles kernel folded the mass term
+            // into every other node's owner partial
+            w.m = 0.f;
+            w.pv[0] = w.pv[1] = w.pv[2] = 0.f;
+            if (w.q0 == w.q1)
+            {
+                w.m = s.mass[n] * sM;
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    w.pv[k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
+            }
+            if (xflush)
+            {
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    w.xv[k] = x[3u * n + k];
+#pragma unroll
+                for (unsigned j = 0; j < kXLag; ++j)
+                    if (j < lag)
+                    {
+                        const float *pj = pbuf.p[(it + 2u - lag + j) % 4u];
+#pragma unroll
+                        for (int k = 0; k < 3; ++k)
+                            w.pj[j][k] = pj[3u * n + k];
+                    }
+            }
         }
-        // every independent load first: the partial run [q0, q1) (node-major: contiguous, no slot
-        // indirection) and the node's vectors are in flight together
-        const uint32_t o0 = T.node_part_off[n], q0 = o0 & kPartOffBits, q1 = T.node_part_off[n + 1] & kPartOffBits;
-        const uint32_t mk = T.off_mask ? o0 >> 29 : s.mask[n];
-        // the tiles kernel folded m s_M p into the node's first partial; a node of no element has none
-        const float m = q0 == q1 ? s.mass[n] * sM : 0.f;
-        // a node in a tile has its new p from its owner slot (k_keff_tiles*: pnew); a node of no element
-        // forms it here, with the same expression
-        float pv[3], xv[3], rv0[3];
-        if (q0 != q1)
+        // (3) fold, update, precondition, store
+#pragma unroll
+        for (int u = 0; u < U; ++u)
         {
+            UpdNode &w = v[u];
+            if (!w.ok)
+                continue;
+            const uint32_t n = w.n, mk = w.mk;
+            if (w.q0 == w.q1)
+                store3(pnew, whole_rsrc(pnew), n, w.pv[0], w.pv[1], w.pv[2], false);
+            if (xflush)  // x and the lag p_j were loaded with the rest; the FMA chain in iteration order
+            {
+#pragma unroll
+                for (unsigned j = 0; j < kXLag; ++j)
+                    if (j < lag)
+#pragma unroll
+                        for (int k = 0; k < 3; ++k)
+                            w.xv[k] = fmaf(aj[j], w.pj[j][k], w.xv[k]);
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    if (mk & (1u << k))
+                        w.xv[k] = rhs[3u * n + k];
+                store3(x, whole_rsrc(x), n, w.xv[0], w.xv[1], w.xv[2], wt);
+            }
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+            const uint32_t cnt = w.q1 - w.q0;
+            if (T.node_major)
+            {
+                if (cnt > 0)
+                {
+                    a0 = w.pa[0];
+                    a1 = w.pa[1];
+                    a2 = w.pa[2];
+                }
+                if (cnt > 1)
+                {
+                    a0 += w.pb[0];
+                    a1 += w.pb[1];
+                    a2 += w.pb[2];
+                }
+                for (uint32_t q = 2; q < cnt; ++q)
+                {
+                    float d[3];
+                    load3(rpart, w.q0 + q, d);
+                    a0 += d[0];
+                    a1 += d[1];
+                    a2 += d[2];
+                }
+            }
+            else
+                for (uint32_t q = w.q0; q < w.q1; ++q)
+                {
+                    const float *pp = T.part + 3ull * T.part_slot[q];
+                    a0 += pp[0];
+                    a1 += pp[1];
+                    a2 += pp[2];
+                }
+            const float av[3] = {a0, a1, a2};
+            float rv[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                pv[k] = pnew[3u * n + k];
-        }
-        else
-        {
+            {
+                const float apk = cnt == 0 ? w.m * w.pv[k] : av[k];
+                rv[k] = (mk & (1u << k)) ? 0.0f : fmaf(-alpha, apk, w.rv0[k]);
+            }
+            store3(r, whole_rsrc(r), n, rv[0], rv[1], rv[2], wt);
+            // symmetric block inverse {a00 a01 a02 a11 a12 a22}; a flagged block (negative scale) reads its
+            // fp32 copy instead
+            float bv[6];
+            if ((int)w.iw.x >= 0)
+                unpack_block_inverse(w.iw.y, w.iw.z, w.iw.w, __uint_as_float(w.iw.x), bv);
+            else
+            {
+                const float *a9 = inv9 + 9ull * n;
+                bv[0] = a9[0];
+                bv[1] = a9[1];
+                bv[2] = a9[2];
+                bv[3] = a9[4];
+                bv[4] = a9[5];
+                bv[5] = a9[8];
+            }
+            const float iv[9] = {bv[0], bv[1], bv[2], bv[1], bv[3], bv[4], bv[2], bv[4], bv[5]};
+            float zs[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k)
             {
-                pv[k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
-                pnew[3u * n + k] = pv[k];
+                float zk = fmaf(iv[3 * k + 2], rv[2], fmaf(iv[3 * k + 1], rv[1], iv[3 * k] * rv[0]));
+                zk = (mk & (1u << k)) ? 0.0f : zk;
+                zs[k] = zk;
+                rr += (double)rv[k] * (double)rv[k];
+                rz += (double)rv[k] * (double)zk;
             }
+            store3(z, whole_rsrc(z), n, zs[0], zs[1], zs[2], wt);
         }
+    }
+    // ghost nodes of a shard: only the search direction (the tiles kernel's p) is kept
+    for (uint32_t n = s.Nown + blockIdx.x * kUpdThreads + threadIdx.x; n < s.N; n += gridDim.x * kUpdThreads)
+    {
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-        {
-            xv[k] = x[3u * n + k];
-            rv0[k] = r[3u * n + k];
-        }
-        const uint4 iw = reinterpret_cast<const uint4 *>(inv)[n];  // 16-B record (k_sym_inverse)
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-        if (T.node_major)
-        {
-            const float *pp = T.part + 3ull * q0;
-            const uint32_t cnt = q1 - q0;
-            // first two partials unconditionally in flight (the part buffer carries 2 padding slots, so
-            // the reads stay in bounds for a node with fewer; unused values are masked below)
-            const float b0 = pp[0], b1 = pp[1], b2 = pp[2];
-            const float c0 = pp[3], c1 = pp[4], c2 = pp[5];
-            if (cnt > 0)
-            {
-                a0 = b0;
-                a1 = b1;
-                a2 = b2;
-            }
-            if (cnt > 1)
-            {
-                a0 += c0;
-                a1 += c1;
-                a2 += c2;
-            }
-            for (uint32_t q = 2; q < cnt; ++q)
-            {
-                a0 += pp[3 * q + 0];
-                a1 += pp[3 * q + 1];
-                a2 += pp[3 * q + 2];
-            }
-        }
-        else
-            for (uint32_t q = q0; q < q1; ++q)
-            {
-                const float *pp = T.part + 3ull * T.part_slot[q];
-                a0 += pp[0];
-                a1 += pp[1];
-                a2 += pp[2];
-            }
-        const float av[3] = {a0, a1, a2};
-        float rv[3], xs[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-        {
-            const uint32_t d = 3u * n + k;
-            const float pk = pv[k];
-            const float apk = (mk & (1u << k)) ? pk : (q0 == q1 ? m * pk : av[k]);
-            float xn = fmaf(alpha, pk, xv[k]);
-            float rw = fmaf(-alpha, apk, rv0[k]);
-            if (mk & (1u << k))
-            {
-                xn = rhs[d];
-                rw = 0.0f;
-            }
-            xs[k] = xn;
-            rv[k] = rw;
-        }
-        store3(x, whole_rsrc(x), n, xs[0], xs[1], xs[2], wt);
-        store3(r, whole_rsrc(r), n, rv[0], rv[1], rv[2], wt);
-        // symmetric block inverse {a00 a01 a02 a11 a12 a22} from the 16-B Jacobi-scaled record
-        // (blockinv_pack.hpp); a flagged block (negative scale) reads its fp32 copy instead
-        float bv[6];
-        if ((int)iw.x >= 0)
-            unpack_block_inverse(iw.y, iw.z, iw.w, __uint_as_float(iw.x), bv);
-        else
-        {
-            const float *a9 = inv9 + 9ull * n;
-            bv[0] = a9[0];
-            bv[1] = a9[1];
-            bv[2] = a9[2];
-            bv[3] = a9[4];
-            bv[4] = a9[5];
-            bv[5] = a9[8];
-        }
-        const float b00 = bv[0], b01 = bv[1], b02 = bv[2], b11 = bv[3], b12 = bv[4], b22 = bv[5];
-        const float iv[9] = {b00, b01, b02, b01, b11, b12, b02, b12, b22};
-        float zs[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-        {
-            float zk = fmaf(iv[3 * k + 2], rv[2], fmaf(iv[3 * k + 1], rv[1], iv[3 * k] * rv[0]));
-            zk = (mk & (1u << k)) ? 0.0f : zk;
-            zs[k] = zk;
-            rr += (double)rv[k] * (double)rv[k];
-            rz += (double)rv[k] * (double)zk;
-        }
-        store3(z, whole_rsrc(z), n, zs[0], zs[1], zs[2], wt);
+            pnew[3u * n + k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
     }
     const double t0 = block_sum<kUpdThreads>(rr, red);
     const double t1 = block_sum<kUpdThreads>(rz, red);
@@ -1705,11 +1781,14 @@ unsigned fast_update_blocks(const DevSys &s)
         int dev = 0, bpc = 0, cus = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles, kUpdThreads, 0);
+        if (upd_unroll() == 2)
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<2>, kUpdThreads, 0);
+        else
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<1>, kUpdThreads, 0);
         const unsigned r = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
         return r < kMaxUpdateBlocks ? r : kMaxUpdateBlocks;
     }();
-    const unsigned g = grid_for(s.N, kUpdThreads);
+    const unsigned g = grid_for(s.N, kUpdThreads * (unsigned)upd_unroll());
     return g < resident ? (g ? g : 1u) : resident;
 }
 
@@ -1746,10 +1825,59 @@ void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, cons
         k_keff_finalize<false><<<g, 256, 0, st>>>(s, x, y);
 }
 
-// FAST search directions ping-pong by iteration parity between p and p2: iteration `it` reads p_old
-// from one and writes the new p to the other (the prologue's p is in p)
-inline float *fast_p_old(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p2 : h->p; }
-inline float *fast_p_new(cwf_hip_system *h, unsigned it) { return (it & 1u) ? h->p : h->p2; }
+// FAST search directions rotate over four buffers: p_j (iteration j's) lives in {p, p2, p3, p4}[(j + 1) % 4],
+// so iteration `it` reads p_old from [it % 4] (the prologue's p is in p) and writes the new p to
+// [(it + 1) % 4], and the last kXLag directions stay readable for the lazy x update
+inline float *fast_p_buf(cwf_hip_system *h, unsigned k)
+{
+    float *const b[4] = {h->p, h->p2, h->p3, h->p4};
+    return b[k % 4u];
+}
+inline float *fast_p_old(cwf_hip_system *h, unsigned it) { return fast_p_buf(h, it); }
+inline float *fast_p_new(cwf_hip_system *h, unsigned it) { return fast_p_buf(h, it + 1u); }
+static_assert(kXLag <= 4, "p_(it - lag + 1) .. p_it must still be in the four rotating buffers");
+inline PBufs fast_p_bufs(cwf_hip_system *h) { return PBufs{{h->p, h->p2, h->p3, h->p4}}; }
+
+// CWF_XLAG=1..4 (diagnostic): iterations per lazy x update (default kXLag)
+static unsigned x_lag()
+{
+    static const unsigned v = [] {
+        const char *e = getenv("CWF_XLAG");
+        const int k = e ? atoi(e) : (int)kXLag;
+        return (unsigned)(k < 1 ? 1 : k > (int)kXLag ? (int)kXLag : k);
+    }();
+    return v;
+}
+
+// the lazy x terms of the iterations after the last flush: j = n - n % lag .. n - 1, n = completed
+// iterations (the device control block's count, so the host needs no iteration count)
+__global__ __launch_bounds__(256) void k_x_flush(DevSys s, const float *__restrict__ rhs, float *__restrict__ x,
+                                                 const Ctl *__restrict__ ctl, PBufs pb, unsigned lag)
+{
+    const unsigned n_it = (unsigned)ctl->iterations, j0 = n_it - n_it % lag;
+    if (j0 == n_it)
+        return;
+    for (uint32_t n = blockIdx.x * 256 + threadIdx.x; n < s.Nown; n += gridDim.x * 256)
+    {
+        float xv[3] = {x[3u * n + 0], x[3u * n + 1], x[3u * n + 2]};
+        for (unsigned j = j0; j < n_it; ++j)
+        {
+            const float *pj = pb.p[(j + 1u) % 4u];
+            const float a = (float)ctl->alpha_h[j % kXLag];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                xv[k] = fmaf(a, pj[3u * n + k], xv[k]);
+        }
+        const uint32_t mk = s.mask[n];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+        {
+            if (mk & (1u << k))
+                xv[k] = rhs[3u * n + k];
+            x[3u * n + k] = xv[k];
+        }
+    }
+}
 
 // CWF_WT=0 (diagnostic): plain x / r / z stores in the update pass instead of write-through
 static bool update_write_through()
@@ -1788,10 +1916,20 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
 {
     const DevSys &s = h->ds;
     const bool direct = fast_direct_fold(h);
-    k_pcg_update_tiles<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
+    const auto k = upd_unroll() == 2 ? k_pcg_update_tiles<2> : k_pcg_update_tiles<1>;
+    k<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
-        direct ? h->part0 : h->g_pap,
-        direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it, update_write_through());
+        direct ? h->part0 : h->g_pap, direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it,
+        update_write_through(), fast_p_bufs(h), x_lag());
+}
+
+void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st)
+{
+    const DevSys &s = h->ds;
+    if (!s.Nown)
+        return;
+    const unsigned g = std::min<unsigned>(grid_for(s.Nown, 256), 2048u);
+    k_x_flush<<<g, 256, 0, st>>>(s, rhs, h->x, h->ctl, fast_p_bufs(h), x_lag());
 }
 
 // diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
