@@ -1141,7 +1141,14 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)
         return "k_keff_parity";
-    return t.grp ? "k_keff_groups_pipe" : t.hex ? "k_keff_hex_tiles" : t.pipe ? "k_keff_tiles_pipe" : "k_keff_tiles";
+    if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
+    {
+        static thread_local char name[96];
+        snprintf(name, sizeof name, "k_keff_groups_pipe<%s, false, 1, %d, %s>", h->ds.iso ? "true" : "false",
+                 t.pipe_nt, h->ds.M == 1 ? "true" : "false");
+        return name;
+    }
+    return t.hex ? "k_keff_hex_tiles" : t.pipe ? "k_keff_tiles_pipe" : "k_keff_tiles";
 }
 
 int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_kind, float *elements,
