@@ -202,6 +202,21 @@ std::vector<uint32_t> morton_node_order(const double *X, uint64_t N)
     return perm;
 }
 
+// CWF_GROUPS=0 (diagnostic): the per-tet tiles instead of the fan groups
+bool groups_enabled()
+{
+    const char *gv = getenv("CWF_GROUPS");
+    return !(gv && gv[0] == '0');
+}
+
+// fan-group tile lanes: 256 (<= 256 groups, <= 512 nodes: T/N 1.59 against 1.77 on C3) where the mesh gives
+// every resident workgroup several tiles, else 128; CWF_GROUP_NT=128|256 overrides
+uint32_t group_lanes(uint64_t E)
+{
+    const char *gn = getenv("CWF_GROUP_NT");
+    return gn ? (atoi(gn) == 256 ? 256u : 128u) : (E >= 4000000ull ? 256u : 128u);
+}
+
 std::string pcg_error_message(int code, int iter, std::string *ctx)
 {
     if (code == CWF_ERR_DENOM_ZERO)
@@ -461,9 +476,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                           !(d->reserved & CWF_DESC_KEEP_NODE_ORDER) && !(rn && rn[0] == '0');
     if (renumber)
     {
-        try
-        {
-            r_perm = morton_node_order(d->node_coords, N);
+        const auto apply_perm = [&]() {
             std::vector<uint32_t> inv(N);
             for (uint64_t i = 0; i < N; ++i)
                 inv[r_perm[i]] = (uint32_t)i;
@@ -481,6 +494,44 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 r_mask[i] = d->bc_mask[n];
                 for (int k = 0; k < 3; ++k)
                     r_coords[3 * i + k] = d->node_coords[3 * n + k];
+            }
+        };
+        try
+        {
+            r_perm = morton_node_order(d->node_coords, N);
+            apply_perm();
+            // fan-group meshes: renumber again by (owner tile, Morton) so every tile's owned nodes are one
+            // contiguous id range (whole-line owner p / partial stores, coalesced owned gathers). The groups
+            // and tiles are built from coordinates and tet order only, so the rebuild after this renumbering
+            // gives the same partition.
+            const char *ot = getenv("CWF_OWNER_ORDER");
+            if (!hex && d->material_count <= 16 && !(ot && ot[0] == '0') && groups_enabled())
+            {
+                cwf_system_desc md = *d;
+                md.element_connectivity = r_conn.data();
+                md.lumped_mass = r_mass.data();
+                md.bc_mask = r_mask.data();
+                md.node_coords = r_coords.data();
+                GroupTiles gt;
+                const uint32_t gnt = group_lanes(E);
+                if (build_group_tiles(&md, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt) == 0 &&
+                    gt.tets_per_group >= 3.0)
+                {
+                    std::vector<uint32_t> own(N, 0xFFFFFFFFu);
+                    for (uint32_t tl = 0; tl < gt.ntiles; ++tl)
+                        for (uint32_t q = gt.hdr[tl].z; q < gt.hdr[tl].z + gt.hdr[tl].w; ++q)
+                            if (gt.tile_nodes[q] & 0x80000000u)
+                                own[gt.tile_nodes[q] & 0x7fffffffu] = tl;
+                    std::vector<uint32_t> order(N);
+                    std::iota(order.begin(), order.end(), 0u);
+                    std::stable_sort(order.begin(), order.end(),
+                                     [&](uint32_t a, uint32_t b) { return own[a] < own[b]; });
+                    std::vector<uint32_t> p2(N);
+                    for (uint64_t i = 0; i < N; ++i)
+                        p2[i] = r_perm[order[i]];
+                    r_perm.swap(p2);
+                    apply_perm();
+                }
             }
         }
         catch (const std::bad_alloc &)
@@ -656,15 +707,11 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         // CWF_GROUPS=0: the per-tet tiles below
         bool grouped = false;
         {
-            const char *gv = getenv("CWF_GROUPS");
-            if (!hex && t.pipe && !(gv && gv[0] == '0') && d->material_count <= 16)
+            if (!hex && t.pipe && groups_enabled() && d->material_count <= 16)
             {
                 GroupTiles gt;
                 int gst = -1;
-                // 256-lane tiles (<= 256 groups, <= 512 nodes: T/N 1.59 against 1.77 on C3) where the mesh
-                // gives every resident workgroup several tiles; CWF_GROUP_NT=128|256 overrides
-                const char *gn = getenv("CWF_GROUP_NT");
-                const uint32_t gnt = gn ? (atoi(gn) == 256 ? 256u : 128u) : (E >= 4000000ull ? 256u : 128u);
+                const uint32_t gnt = group_lanes(E);
                 try
                 {
                     gst = build_group_tiles(d, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt);

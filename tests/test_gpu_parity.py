@@ -293,6 +293,41 @@ def test_fast_stepper_with_partial_masks():
     assert np.linalg.norm(uf - ur) <= 1e-4 * np.linalg.norm(ur)
 
 
+_LAZY_X_SCRIPT = r"""
+import hashlib, sys, numpy as np
+sys.path[:0] = sys.argv[1:3]
+from cwf import _lib, pcg, scenarios
+case = scenarios.block_case(7, 6, 5, h=0.1, jitter=True, tol=1e-6, max_iterations=600)
+s0, m0 = case.scalars()
+s = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, s0, m0, mode=_lib.MODE_FAST)
+rhs = case.static_rhs()
+out = []
+for it in (5, 6, 7, 8, 600):
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(it, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    out += [hashlib.sha256(x.tobytes()).hexdigest(), str(t.iterations)]
+print(" ".join(out))
+"""
+
+
+def test_fast_lazy_x_is_bitwise_the_eager_update():
+    """FAST PCG applies x += alpha_j p_j every 4th iteration (k_pcg_update_tiles) and flushes the rest
+    after the solve (k_x_flush); the FMA chain in iteration order is bitwise the per-iteration update
+    (CWF_XLAG=1). Solves stopping at every iteration count mod 4 (max_iterations 5..8) and a converged one."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [sys.executable, "-c", _LAZY_X_SCRIPT, os.path.join(root, "civiwave-fem_amd"), os.path.join(root, "tests")]
+    runs = {}
+    for lag in ("4", "1"):
+        env = dict(os.environ, CWF_XLAG=lag)
+        r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        runs[lag] = r.stdout.split()
+    assert runs["4"] == runs["1"]
+
+
 def test_cpp_mirror_single_tet_reference_outputs(tmp_path):
     """tests/cpp/pcg_api_test.cpp: the reference's single-tet fixture through include/cwf_hip.hpp."""
     import subprocess
