@@ -1417,49 +1417,21 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     __shared__ double red[kUpdThreads / 64];
     if (!ctl->active)
         return;
-    // pcg.cpp:840-852: alpha = rho / (p . Ap)
-    const double denom = fold_all<kUpdThreads>(part_dot, ntp, red);
-    if (fabs(denom) < 1.0e-18)
-    {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-        {
-            ctl->denom = denom;
-            ctl->error = CWF_ERR_DENOM_ZERO;
-            ctl->error_iter = (int)it;
-            ctl->active = 0;
-        }
-        return;
-    }
-    const double alpha_d = ctl->rho2[it & 1u] / denom;
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-    {
-        ctl->denom = denom;
-        ctl->alpha = alpha_d;
-        ctl->alpha_last = alpha_d;
-        ctl->alpha_h[it % kXLag] = alpha_d;
-    }
-    const bool xflush = (it + 1u) % lag == 0u;
-    float aj[kXLag];  // alpha of iteration it + 1 - lag + j
-#pragma unroll
-    for (unsigned j = 0; j < kXLag; ++j)
-    {
-        const unsigned ij = it + 1u - lag + j;
-        aj[j] = j < lag ? (float)(ij == it ? alpha_d : ctl->alpha_h[ij % kXLag]) : 0.f;
-    }
     const DevTiles &T = s.t;
-    const float alpha = (float)alpha_d, beta = (float)ctl->beta;
+    const float beta = (float)ctl->beta;  // this iteration's (the tiles kernel's residual step wrote it)
     const float sM = (float)s.sM;
     const __amdgpu_buffer_rsrc_t rpart = whole_rsrc(T.part);
-    double rr = 0.0, rz = 0.0;
+    const bool xflush = (it + 1u) % lag == 0u;
     const uint32_t step = gridDim.x * kUpdThreads * U;
-    for (uint32_t base = blockIdx.x * kUpdThreads * U + threadIdx.x; base < s.Nown; base += step)
-    {
-        UpdNode v[U];
-        // (1) the partial-run bounds (and the Dirichlet mask in their top bits)
+    uint32_t base = blockIdx.x * kUpdThreads * U + threadIdx.x;
+    UpdNode v[U];
+    // (1) + (2): every load of the U nodes that does not need alpha (issued for the first trip before the
+    // p.Ap fold below, so its latency hides under the fold's)
+    const auto load_nodes = [&](uint32_t b0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u)  // the partial-run bounds (and the Dirichlet mask in their top bits)
         {
-            v[u].n = base + u * kUpdThreads;
+            v[u].n = b0 + u * kUpdThreads;
             v[u].ok = v[u].n < s.Nown;
             const uint32_t n = v[u].ok ? v[u].n : 0u;
             const uint32_t o0 = T.node_part_off[n], o1 = T.node_part_off[n + 1];
@@ -1467,7 +1439,6 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             v[u].q1 = o1 & kPartOffBits;
             v[u].mk = T.off_mask ? o0 >> 29 : s.mask[n];
         }
-        // (2) every independent load of the U nodes
 #pragma unroll
         for (int u = 0; u < U; ++u)
         {
@@ -1510,6 +1481,43 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
                     }
             }
         }
+    };
+    if (base < s.Nown)
+        load_nodes(base);
+    // pcg.cpp:840-852: alpha = rho / (p . Ap)
+    const double denom = fold_all<kUpdThreads>(part_dot, ntp, red);
+    if (fabs(denom) < 1.0e-18)
+    {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+        {
+            ctl->denom = denom;
+            ctl->error = CWF_ERR_DENOM_ZERO;
+            ctl->error_iter = (int)it;
+            ctl->active = 0;
+        }
+        return;
+    }
+    const double alpha_d = ctl->rho2[it & 1u] / denom;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+    {
+        ctl->denom = denom;
+        ctl->alpha = alpha_d;
+        ctl->alpha_last = alpha_d;
+        ctl->alpha_h[it % kXLag] = alpha_d;
+    }
+    float aj[kXLag];  // alpha of iteration it + 1 - lag + j
+#pragma unroll
+    for (unsigned j = 0; j < kXLag; ++j)
+    {
+        const unsigned ij = it + 1u - lag + j;
+        aj[j] = j < lag ? (float)(ij == it ? alpha_d : ctl->alpha_h[ij % kXLag]) : 0.f;
+    }
+    const float alpha = (float)alpha_d;
+    double rr = 0.0, rz = 0.0;
+    for (; base < s.Nown; base += step)
+    {
+        if (base != blockIdx.x * kUpdThreads * U + threadIdx.x)
+            load_nodes(base);
         // (3) fold, update, precondition, store
 #pragma unroll
         for (int u = 0; u < U; ++u)
