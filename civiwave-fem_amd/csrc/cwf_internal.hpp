@@ -101,7 +101,7 @@ uint64_t spread21(uint64_t v);  // 21-bit Morton spread (one axis of a 63-bit ke
 // recursive coordinate bisection of order's items (centroids c[3 id], mean extents ext) into leaves of at most
 // max_elems, cut between layers (tiles.cpp); leaf_end receives each leaf's end in `order`
 void rcb_partition(const std::vector<double> &c, const double ext[3], std::vector<uint32_t> &order,
-                   uint64_t max_elems, std::vector<uint64_t> &leaf_end);
+                   uint64_t max_elems, std::vector<uint64_t> &leaf_end, int tdiv = 16, int wdiv = 16);
 
 // FAST tet "fan groups" (groups.cpp): tets grouped around a shared edge (a, b) -- a closed or open fan of
 // up to 6 tets {a, b, r_i, r_{(i+1) mod 6}} -- so one lane computes a group with its <= 8 nodes in

@@ -40,16 +40,17 @@ uint64_t spread21(uint64_t v)
 namespace
 {
 
-// Recursive coordinate bisection of the elements into leaves of at most max_elems (target ~7/8 of it).
-// Each range is cut along the longest axis of its centroid box near the count n * L1 / L (L leaves,
-// L1 = L / 2), at the widest gap between consecutive centroid coordinates within +-n/16 of that count.
+// Recursive coordinate bisection of the elements into leaves of at most max_elems (target max_elems
+// (1 - 1/tdiv), tdiv = 0: max_elems). Each range is cut along the longest axis of its centroid box near the
+// count n * L1 / L (L leaves, L1 = L / 2), at the widest gap between consecutive centroid coordinates within
+// +-n/wdiv of that count.
 // A cut through such a gap runs between element layers instead of through them, so the two sides share
 // one node layer rather than the nodes of a whole sliced layer: for a Kuhn block the tile halo (T / N)
 // drops from ~2.5 (Morton-curve segments) to ~1.8. The leaves come out in k-d-tree order, so consecutive
 // tiles are neighbours. c: centroids [3E]; lo/hi: per-element min/max node coordinate [3E] (extent);
 // leaf_end receives each leaf's end in `order`.
 void rcb(const std::vector<double> &c, const double ext[3], std::vector<uint32_t> &order, uint64_t b, uint64_t e,
-         uint64_t max_elems, std::vector<uint64_t> &leaf_end)
+         uint64_t max_elems, std::vector<uint64_t> &leaf_end, int tdiv = 16, int wdiv = 16)
 {
     const uint64_t n = e - b;
     if (n <= max_elems)
@@ -58,7 +59,7 @@ void rcb(const std::vector<double> &c, const double ext[3], std::vector<uint32_t
             leaf_end.push_back(e);
         return;
     }
-    const uint64_t target = std::max<uint64_t>(1, max_elems - max_elems / 16);
+    const uint64_t target = std::max<uint64_t>(1, tdiv > 0 ? max_elems - max_elems / (uint64_t)tdiv : max_elems);
     const uint64_t Lr = std::max<uint64_t>((n + target - 1) / target, 2);
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     for (uint64_t i = b; i < e; ++i)
@@ -77,7 +78,7 @@ void rcb(const std::vector<double> &c, const double ext[3], std::vector<uint32_t
     };
     const uint64_t L1 = Lr / 2;
     const uint64_t m = b + (n * L1 + Lr / 2) / Lr;
-    const uint64_t w = n / 16;
+    const uint64_t w = n / (uint64_t)(wdiv > 0 ? wdiv : 16);
     uint64_t cut = m;
     std::nth_element(order.begin() + b, order.begin() + m, order.begin() + e, less);
     if (w >= 2)
@@ -105,15 +106,15 @@ void rcb(const std::vector<double> &c, const double ext[3], std::vector<uint32_t
         }
     }
     cut = std::min(std::max(cut, b + 1), e - 1);  // both sides non-empty (n > max_elems >= 1)
-    rcb(c, ext, order, b, cut, max_elems, leaf_end);
-    rcb(c, ext, order, cut, e, max_elems, leaf_end);
+    rcb(c, ext, order, b, cut, max_elems, leaf_end, tdiv, wdiv);
+    rcb(c, ext, order, cut, e, max_elems, leaf_end, tdiv, wdiv);
 }
 }  // namespace
 
 void rcb_partition(const std::vector<double> &c, const double ext[3], std::vector<uint32_t> &order,
-                   uint64_t max_elems, std::vector<uint64_t> &leaf_end)
+                   uint64_t max_elems, std::vector<uint64_t> &leaf_end, int tdiv, int wdiv)
 {
-    rcb(c, ext, order, 0, order.size(), max_elems, leaf_end);
+    rcb(c, ext, order, 0, order.size(), max_elems, leaf_end, tdiv, wdiv);
 }
 
 int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, uint32_t max_elems, int corners)
