@@ -230,7 +230,7 @@ int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::
     for (size_t i = 0; i < g.size(); ++i)
     {
         fast_update_pcg(g[i], rhs[i], it, g[i]->stream);
-        fast_fold_rrz(g[i], g[i]->stream);
+        fast_fold_rrz(g[i], it, g[i]->stream);
     }
     if (int st = comm_allgather(g, &cwf_hip_system::g_rrz, 2))
         return st;

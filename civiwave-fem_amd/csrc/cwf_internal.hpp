@@ -285,13 +285,13 @@ void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st);  // the 
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
-unsigned fast_update_blocks(const DevSys &s);
+unsigned fast_update_blocks(const DevSys &s, bool flush);  // grid of update pass (lazy-x iteration or not)
 // sharded FAST PCG (comm.cpp orchestrates, spmv_tiles.hip / kernels_fast.hip launch)
 // post.hip: derived fields (derived_fields.cpp:139-211) -> f32 [13 E] / [13 N] (either may be NULL)
 void derived_fields(cwf_hip_system *h, const float *u, float *elem_out, float *node_out, hipStream_t st);
 bool fast_direct_fold(const cwf_hip_system *h);  // unsharded: consumers fold per-workgroup shares
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> g_pap[rank]
-void fast_fold_rrz(cwf_hip_system *h, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
+void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
 void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st);
 void fast_block_inverse(cwf_hip_system *h, hipStream_t st);  // parity BJ, symmetrised + packed to inv6
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st);

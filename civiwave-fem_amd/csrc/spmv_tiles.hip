@@ -1407,7 +1407,7 @@ struct UpdNode
 // r -= alpha Ap, Dirichlet, z = M^-1 r (16-B Jacobi-scaled block, blockinv_pack.hpp), r.r / r.z shares;
 // x += alpha_j p_j for the last `lag` iterations every lag-th iteration (lazy x, 1 = every iteration; the
 // FMA chain in iteration order is bitwise the eager update), fast_flush_x applies the rest after the solve.
-template <int U>
+template <int U, bool XF>
 __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, const float *__restrict__ inv9,
     float *__restrict__ x, float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold,
@@ -1421,7 +1421,9 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     const float beta = (float)ctl->beta;  // this iteration's (the tiles kernel's residual step wrote it)
     const float sM = (float)s.sM;
     const __amdgpu_buffer_rsrc_t rpart = whole_rsrc(T.part);
-    const bool xflush = (it + 1u) % lag == 0u;
+    // XF: this iteration applies the lazy x update (a separate instantiation, so the three iterations in four
+    // that do not keep the registers of the update pass's occupancy)
+    constexpr bool xflush = XF;
     const uint32_t step = gridDim.x * kUpdThreads * U;
     uint32_t base = blockIdx.x * kUpdThreads * U + threadIdx.x;
     UpdNode v[U];
@@ -1783,21 +1785,27 @@ unsigned fast_pipe_grid(const DevSys &s)
 }
 // the update pass is grid-stride: at most one resident wave of workgroups (occupancy x CUs), so no
 // workgroup waits for a slot behind the others' whole node ranges
-unsigned fast_update_blocks(const DevSys &s)
+template <int U, bool XF>
+unsigned update_resident()
 {
-    static const unsigned resident = [] {
-        int dev = 0, bpc = 0, cus = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (upd_unroll() == 2)
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<2>, kUpdThreads, 0);
-        else
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<1>, kUpdThreads, 0);
-        const unsigned r = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
-        return r < kMaxUpdateBlocks ? r : kMaxUpdateBlocks;
-    }();
+    int dev = 0, bpc = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<U, XF>, kUpdThreads, 0);
+    const unsigned r = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
+    return r < kMaxUpdateBlocks ? r : kMaxUpdateBlocks;
+}
+
+// flush: the grid of the lazy-x instantiation (its own occupancy); the consumers of the update's r.r / r.z
+// shares ask with the flag of the iteration that produced them
+unsigned fast_update_blocks(const DevSys &s, bool flush)
+{
+    static const unsigned resident[2][2] = {
+        {update_resident<1, false>(), update_resident<1, true>()},
+        {update_resident<2, false>(), update_resident<2, true>()}};
+    const unsigned res = resident[upd_unroll() == 2][flush ? 1 : 0];
     const unsigned g = grid_for(s.N, kUpdThreads * (unsigned)upd_unroll());
-    return g < resident ? (g ? g : 1u) : resident;
+    return g < res ? (g ? g : 1u) : res;
 }
 
 static int tile_threads()
@@ -1857,6 +1865,9 @@ static unsigned x_lag()
     return v;
 }
 
+// iteration j's update applies the lazy x terms
+inline bool x_flush_iter(unsigned j) { return (j + 1u) % x_lag() == 0u; }
+
 // the lazy x terms of the iterations after the last flush: j = n - n % lag .. n - 1, n = completed
 // iterations (the device control block's count, so the host needs no iteration count)
 __global__ __launch_bounds__(256) void k_x_flush(DevSys s, const float *__restrict__ rhs, float *__restrict__ x,
@@ -1911,7 +1922,8 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e
     // directly; a shard reads the all-gathered per-rank pairs
     PcgArgs pa = fast_direct_fold(h)
                      ? PcgArgs{h->z, h->ctl, h->part0, h->part1, h->part2,
-                               fast_update_blocks(s), 1u, it, h->hist, abl, fast_p_new(h, it)}
+                               fast_update_blocks(s, it && x_flush_iter(it - 1u)), 1u, it, h->hist, abl,
+                               fast_p_new(h, it)}
                      : PcgArgs{h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
                                (unsigned)h->nranks, 2u, it, h->hist, abl, fast_p_new(h, it)};
     if (s.iso)
@@ -1924,8 +1936,10 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
 {
     const DevSys &s = h->ds;
     const bool direct = fast_direct_fold(h);
-    const auto k = upd_unroll() == 2 ? k_pcg_update_tiles<2> : k_pcg_update_tiles<1>;
-    k<<<fast_update_blocks(s), kUpdThreads, 0, st>>>(
+    const bool xf = x_flush_iter(it);
+    const auto k = upd_unroll() == 2 ? (xf ? k_pcg_update_tiles<2, true> : k_pcg_update_tiles<2, false>)
+                                     : (xf ? k_pcg_update_tiles<1, true> : k_pcg_update_tiles<1, false>);
+    k<<<fast_update_blocks(s, xf), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
         direct ? h->part0 : h->g_pap, direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it,
         update_write_through(), fast_p_bufs(h), x_lag());
@@ -1953,7 +1967,8 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
     if (fast_direct_fold(h))
-        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->part1, h->part2, fast_update_blocks(h->ds), 1u, it, h->hist);
+        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->part1, h->part2,
+                                       fast_update_blocks(h->ds, it && x_flush_iter(it - 1u)), 1u, it, h->hist);
     else
         k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
 }
@@ -1992,11 +2007,11 @@ void fast_fold_pap(cwf_hip_system *h, hipStream_t st)
     fold_pair(h->part0, nullptr, fast_tile_blocks(h->ds), h->g_pap + h->rank, st);
 }
 
-void fast_fold_rrz(cwf_hip_system *h, hipStream_t st)
+void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
     if (fast_direct_fold(h))
         return;
-    fold_pair(h->part1, h->part2, fast_update_blocks(h->ds), h->g_rrz + 2 * h->rank, st);
+    fold_pair(h->part1, h->part2, fast_update_blocks(h->ds, x_flush_iter(it)), h->g_rrz + 2 * h->rank, st);
 }
 
 void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st)
