@@ -500,28 +500,45 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         {
             r_perm = morton_node_order(d->node_coords, N);
             apply_perm();
-            // fan-group meshes: renumber again by (owner tile, Morton) so every tile's owned nodes are one
+            // fan-group and hex8 meshes: renumber again by (owner tile, Morton) so every tile's owned nodes are one
             // contiguous id range (whole-line owner p / partial stores, coalesced owned gathers). The groups
             // and tiles are built from coordinates and tet order only, so the rebuild after this renumbering
             // gives the same partition.
             const char *ot = getenv("CWF_OWNER_ORDER");
-            if (!hex && d->material_count <= 16 && !(ot && ot[0] == '0') && groups_enabled())
+            if (!(ot && ot[0] == '0') && (hex || (d->material_count <= 16 && groups_enabled())))
             {
                 cwf_system_desc md = *d;
                 md.element_connectivity = r_conn.data();
                 md.lumped_mass = r_mass.data();
                 md.bc_mask = r_mask.data();
                 md.node_coords = r_coords.data();
-                GroupTiles gt;
-                const uint32_t gnt = group_lanes(E);
-                if (build_group_tiles(&md, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt) == 0 &&
-                    gt.tets_per_group >= 3.0)
+                std::vector<uint32_t> own;
+                if (hex)  // the hex tiles (tiles.cpp, 8 corners): the same owner = first tile of the node
                 {
-                    std::vector<uint32_t> own(N, 0xFFFFFFFFu);
-                    for (uint32_t tl = 0; tl < gt.ntiles; ++tl)
-                        for (uint32_t q = gt.hdr[tl].z; q < gt.hdr[tl].z + gt.hdr[tl].w; ++q)
-                            if (gt.tile_nodes[q] & 0x80000000u)
-                                own[gt.tile_nodes[q] & 0x7fffffffu] = tl;
+                    HostTiles ht;
+                    build_tiles(&md, ht, 2u * kHexTileThreads, kHexTileThreads, 8);
+                    own.assign(N, 0xFFFFFFFFu);
+                    for (uint32_t tl = 0; tl < ht.ntiles; ++tl)
+                        for (uint32_t q = ht.tile_node_off[tl]; q < ht.tile_node_off[tl + 1]; ++q)
+                            if (ht.tile_nodes[q] & 0x80000000u)
+                                own[ht.tile_nodes[q] & 0x7fffffffu] = tl;
+                }
+                else
+                {
+                    GroupTiles gt;
+                    const uint32_t gnt = group_lanes(E);
+                    if (build_group_tiles(&md, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt) == 0 &&
+                        gt.tets_per_group >= 3.0)
+                    {
+                        own.assign(N, 0xFFFFFFFFu);
+                        for (uint32_t tl = 0; tl < gt.ntiles; ++tl)
+                            for (uint32_t q = gt.hdr[tl].z; q < gt.hdr[tl].z + gt.hdr[tl].w; ++q)
+                                if (gt.tile_nodes[q] & 0x80000000u)
+                                    own[gt.tile_nodes[q] & 0x7fffffffu] = tl;
+                    }
+                }
+                if (!own.empty())
+                {
                     std::vector<uint32_t> order(N);
                     std::iota(order.begin(), order.end(), 0u);
                     std::stable_sort(order.begin(), order.end(),
