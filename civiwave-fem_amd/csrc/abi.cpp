@@ -786,6 +786,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     t.push = 1;
                     t.pipe = 1;
                     t.pipe_nt = (int)gnt;
+                    {
+                        const char *wt = getenv("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
+                        t.wt_part = wt ? (wt[0] == '1') : (gnt == 128);
+                    }
                     t.ntiles = gt.ntiles;
                     t.ngroups = gt.ngroups;
                     t.max_tile_nodes = gt.max_tile_nodes;

@@ -72,6 +72,10 @@ struct DevTiles
     // are the contiguous run part[3 node_part_off[n] .. 3 node_part_off[n+1]) and part_slot is not read
     const uint32_t *tslot = nullptr;
     int node_major = 0;
+    // fan groups: partials stored write-through (sc1), so their lines leave L2 during the kernel instead of in
+    // the end-of-kernel write-back the update pass waits for; only pays while the working set stays in the
+    // MALL (abi.cpp: 128-lane tiles, < 4M tets)
+    int wt_part = 0;
     float *part = nullptr;                    // [3*total] tile-node partial sums, node-major (scratch)
 };
 

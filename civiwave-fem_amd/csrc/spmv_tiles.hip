@@ -1279,7 +1279,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
                     }
                 }
                 if (!(pa.abl & 512u))
-                    store3(T.part, whole_rsrc(T.part), slot_own[k], a0, a1, a2, false);
+                    store3(T.part, whole_rsrc(T.part), slot_own[k], a0, a1, a2, T.wt_part != 0);
                 if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
                     pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
             }
