@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--keff-sample", type=int, default=4,
                     help="hipEvent-time every k-th K_eff launch of the timed steps (1 = all)")
     ap.add_argument("--cpu-iterations", type=int, default=40)
+    ap.add_argument("--no-hbm-roofline", action="store_true",
+                    help="skip the live configs[2] K_eff roofline (N=1 runs of configs other than c3 add it)")
     ap.add_argument("--traffic", default="auto",
                     help="PMC summary json for roofline.traffic; 'auto' = newest profiles/r*_<config>_<mode>_pmc.json")
     return ap.parse_args()
@@ -67,6 +69,48 @@ def cpu_baseline(case, sK, sM, iters):
     return dict(value=case.packing.dof_count * it / dt, unit="DOF-it/s", cores=1, kind="port",
                 sample=f"{case.name}: oracle solve_pcg (block-Jacobi setup + {it} PCG iterations), "
                        f"{dt:.2f} s, 1 thread, {os.cpu_count()} host CPUs visible")
+
+
+def hbm_roofline(L, device, key="c3", iters=200, sample=4):
+    """The same PCG-mode K_eff kernel, live, on the configs[2] block (C2's working set sits in
+    the 256 MB MALL, so its roofline is not an HBM figure; C3 moves 0.38 GB per launch). A FAST solve of
+    `iters` iterations from x = 0 on the static load, every `sample`-th launch hipEvent-timed (as in the
+    Newmark steps) on the handle's stream;
+    the first solve is an untimed warm-up. Outside the timed Newmark steps, so it changes no other field."""
+    import ctypes as C
+
+    import numpy as np
+
+    from cwf import _lib, pcg, scenarios
+
+    case = scenarios.config_case(key)
+    P = case.packing
+    sK, sM = case.scalars()
+    sysm = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=_lib.MODE_FAST, device=device)
+    rhs = case.static_rhs()
+    h = sysm.handle()
+    out = None
+    for timed in (False, True):
+        x = np.zeros(P.dof_count, np.float32)
+        r = np.zeros(P.dof_count, np.float32)
+        L.cwf_hip_system_set_timing(h, sample if timed else 0)
+        res = pcg.solve_pcg(sysm, rhs, pcg.PcgSettings(iters, 1e-12, False), pcg.PcgVectors(x, r))
+        if not res.has_value():
+            raise SystemExit(f"hbm roofline solve failed: {res.error()}")
+        if timed:
+            ms, n = C.c_double(), C.c_uint64()
+            L.cwf_hip_system_timing(h, C.byref(ms), C.byref(n))
+            lay_b, ref_b = C.c_uint64(), C.c_uint64()
+            L.cwf_hip_system_keff_traffic(h, C.byref(lay_b), C.byref(ref_b))
+            avg = ms.value / max(1, n.value)
+            ach = lay_b.value / (avg * 1e-3) / 1e9
+            out = {"bound": "hbm", "workload": case.name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": ach / HBM_PEAK_GBS, "kernel": (L.cwf_hip_system_keff_kernel(h) or b"").decode(),
+                   "avg_launch_ms": avg, "launches": int(n.value), "algorithmic_bytes_per_launch": float(lay_b.value),
+                   "reference_layout_equiv_gbs": ref_b.value / (avg * 1e-3) / 1e9}
+    L.cwf_hip_system_set_timing(h, 0)
+    sysm.close()
+    return out
 
 
 def stream_copy_gbs(L, device, nbytes=2 << 30, reps=20):
@@ -197,6 +241,23 @@ def main():
             traffic_src = os.path.relpath(tpath, ROOT)
     result = None
     copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
+    stepper.close()
+    stepper.system.close()
+    hbm = None
+    if (rank == 0 and world == 1 and not args.no_hbm_roofline and args.mode == "fast" and args.element == "tet4"
+            and args.config != "c3"):
+        hbm = hbm_roofline(L, device)
+        if copy_gbs:
+            hbm["frac_of_measured_copy"] = hbm["achieved"] / copy_gbs
+        hbm["traffic"], hbm["traffic_source"] = None, None
+        import glob
+
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_fast_pmc.json")))
+        if cands:
+            pmc = json.load(open(cands[-1]))
+            if any(hbm["kernel"] in k for k in pmc.get("kernels", {})):
+                hbm["traffic"] = pmc.get("hbm_bytes_per_launch")
+                hbm["traffic_source"] = os.path.relpath(cands[-1], ROOT)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1 and args.element == "tet4":  # rank 0 at N=1 only
@@ -235,10 +296,9 @@ def main():
                          "measured_copy_gbs": copy_gbs,
                          "frac_of_measured_copy": (achieved / copy_gbs) if achieved and copy_gbs else None},
             "cpu_baseline": cpu,
+            "roofline_hbm": hbm,
         }
         print(json.dumps(result), flush=True)
-    stepper.close()
-    stepper.system.close()
     if comm is not None:
         comm.close()
     if dist is not None:

@@ -131,6 +131,7 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
                       uint32_t slot_budget);
 
 constexpr uint32_t kPartOffBits = 0x1fffffffu;
+constexpr uint64_t kMaxFirstBatch = 4096;  // PCG iterations enqueued before the first control-block read-back
 // FAST PCG applies x += alpha_j p_j every kXLag iterations, from the last kXLag search directions (one p
 // buffer each, rotating), instead of re-reading x and p every iteration
 constexpr unsigned kXLag = 4;  // node_part_off value bits (the rest: bc_mask, off_mask)
@@ -213,6 +214,7 @@ struct cwf_hip_system
     double *hist = nullptr;        // device residual history
     uint64_t hist_cap = 0;
     uint64_t hist_count = 0;
+    uint64_t last_iters = 0;  // iterations of the previous solve on this handle (the first batch's size)
     std::string err, ctx;
     // live K_eff timing (cwf_hip_system_set_timing)
     int timing = 0;
