@@ -240,13 +240,14 @@ def main():
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(tpath, ROOT)
     result = None
-    copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
     stepper.close()
     stepper.system.close()
     hbm = None
     if (rank == 0 and world == 1 and not args.no_hbm_roofline and args.mode == "fast" and args.element == "tet4"
             and args.config != "c3"):
         hbm = hbm_roofline(L, device)
+    copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
+    if hbm:
         if copy_gbs:
             hbm["frac_of_measured_copy"] = hbm["achieved"] / copy_gbs
         hbm["traffic"], hbm["traffic_source"] = None, None

@@ -1312,6 +1312,8 @@ int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64
         return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
                          "required=" + std::to_string(req) + " available=" + std::to_string(n));
     float *dst = kind == CWF_PTR_DEVICE && !h->perm ? inv_out : h->inv;
+    if (dst == h->inv)
+        h->inv_fast = false;  // overwritten with the unsymmetrised reference inverse
     if (h->ds.hex)
         hex_block_jacobi(h, dst, h->stream);
     else

@@ -202,6 +202,11 @@ struct cwf_hip_system
     float *p2 = nullptr, *p3 = nullptr, *p4 = nullptr;  // FAST: p_j lives in {p, p2, p3, p4}[(j + 1) % 4]
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
+    // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's
+    // immutable element data and mask and on the two scalars, so a FAST solve with unchanged scalars (every
+    // fixed-step Newmark step) reuses it instead of rebuilding it (pcg.cpp:749 rebuilds per solve; same values)
+    bool inv_fast = false;
+    double inv_sK = 0.0, inv_sM = 0.0;
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
     uint64_t part_cap = 0;
     // FAST-mode internal node renumbering (Morton order of the coordinates): perm[i] = caller's node of

@@ -861,6 +861,7 @@ void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
     const DevSys &s = h->ds;
     const uint32_t chunks = parity_chunk_count(h);
     parity_block_jacobi(h, h->inv, st);
+    h->inv_fast = false;  // inv now holds the PARITY inverse (not symmetrised, no inv6)
     parity_keff(h, h->x, h->Ap, true, nullptr, st);
     k_init_residual<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->Ap, h->x, h->r);
     parity_dot_partials(h, rhs, rhs, nullptr, h->part0, nullptr, nullptr, st);

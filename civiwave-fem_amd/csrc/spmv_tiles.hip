@@ -1975,6 +1975,11 @@ void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 
 void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
 {
+    if (h->inv_fast && h->inv_sK == h->ds.sK && h->inv_sM == h->ds.sM)
+        return;  // built for these scalars (C2: one 350-us fp64 setup per Newmark step saved)
+    h->inv_fast = true;
+    h->inv_sK = h->ds.sK;
+    h->inv_sM = h->ds.sM;
     if (h->ds.hex)
         hex_block_jacobi(h, h->inv, st);
     else

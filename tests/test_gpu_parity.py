@@ -227,6 +227,36 @@ def test_fast_mode_solve_close(case):
     assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
 
 
+def test_fast_block_inverse_reused_only_for_unchanged_scalars(case):
+    """A FAST handle keeps its block inverse while (s_K, s_M) are unchanged and rebuilds it when they change
+    or when the reference inverse was exported through it: every solve is bitwise the same solve on a fresh
+    handle with the same scalars (FAST is deterministic: fixed fold orders, no atomics)."""
+    sK, sM = case.scalars()
+    rhs = case.static_rhs()
+
+    def solve(s):
+        x, r = np.zeros_like(rhs), np.zeros_like(rhs)
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(40, 1e-12), pcg.PcgVectors(x, r)).value()
+        return x, r, t.residual_norm
+
+    def same(a, b):
+        assert_bitwise(a[0], b[0], "x")
+        assert_bitwise(a[1], b[1], "r")
+        assert a[2] == b[2]
+
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    first = solve(s)
+    same(solve(s), first)  # the second solve reuses the inverse
+    s.stiffness_scale, s.mass_factor = 1.5 * sK, 0.5 * sM + 1.0
+    changed = solve(s)
+    same(changed, solve(gpu_system(case, mode=_lib.MODE_FAST, sK=1.5 * sK, sM=0.5 * sM + 1.0)))
+    ref_inv = np.zeros(9 * case.packing.node_count, np.float32)
+    assert pcg.build_block_jacobi_inverse(s, None, ref_inv).has_value()  # overwrites the handle's copy
+    same(solve(s), changed)
+    s.stiffness_scale, s.mass_factor = sK, sM
+    same(solve(s), first)
+
+
 def _upper_sym(inv9):
     b = inv9.reshape(-1, 3, 3)
     return np.stack([b[:, 0, 0], b[:, 0, 1], b[:, 0, 2], b[:, 1, 1], b[:, 1, 2], b[:, 2, 2]], 1)

@@ -12,7 +12,7 @@ timeout -k 10 300 python -u bench.py > $O/${TAG}_bench_c2.log 2>&1 && tail -1 $O
 timeout -k 10 300 python -u bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_c3.log 2>&1 && tail -1 $O/${TAG}_bench_c3.log > $O/${TAG}_bench_c3_fast.json &&
 timeout -k 10 300 python -u bench.py --element hex8 --no-cpu-baseline > $O/${TAG}_bench_c2hex.log 2>&1 && tail -1 $O/${TAG}_bench_c2hex.log > $O/${TAG}_bench_c2_hex8_fast.json &&
 timeout -k 10 300 python -u bench.py --element hex8 --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/${TAG}_bench_c3hex.log 2>&1 && tail -1 $O/${TAG}_bench_c3hex.log > $O/${TAG}_bench_c3_hex8_fast.json &&
-bash tools/profile.sh c2 --steps 5 --warmup 1 --no-cpu-baseline > $O/${TAG}_profile_c2.log 2>&1 &&
+bash tools/profile.sh c2 --steps 5 --warmup 1 --no-cpu-baseline --no-hbm-roofline > $O/${TAG}_profile_c2.log 2>&1 &&
 python3 tools/pmc_summary.py gpurun_out/prof_c2 --kernel "$K" --json $O/${TAG}_c2_fast_pmc.json > $O/${TAG}_c2_fast_summary.txt &&
 cp gpurun_out/prof_c2/kt/kt_kernel_stats.csv $O/${TAG}_c2_fast_kernel_stats.csv && grep "^{\"metric" gpurun_out/prof_c2/bench_kt.log > $O/${TAG}_c2_bench_under_rocprof.json &&
 bash tools/profile.sh c3 --config c3 --steps 2 --warmup 1 --no-cpu-baseline > $O/${TAG}_profile_c3.log 2>&1 &&
