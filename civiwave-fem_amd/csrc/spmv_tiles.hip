@@ -33,7 +33,10 @@ namespace cwf
 namespace
 {
 constexpr int kMaxM = 16;
-constexpr int kUpdThreads = 256;
+#ifndef CWF_UPD_THREADS
+#define CWF_UPD_THREADS 256
+#endif
+constexpr int kUpdThreads = CWF_UPD_THREADS;  // update-pass workgroup size (its per-workgroup shares are refolded by every consumer workgroup)
 constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
 // CWF_UPD_U=1|2 (diagnostic): owned nodes per update-pass thread and loop trip (default 1: 2 measured 4-5%
 // slower on C2 and C3, its registers cost more occupancy than the extra loads in flight gain)
@@ -1775,6 +1778,12 @@ unsigned fast_pipe_grid(const DevSys &s)
         const unsigned g = s.iso ? (s.M == 1 ? group_grid<true, true>(nt) : group_grid<true, false>(nt))
                                  : (s.M == 1 ? group_grid<false, true>(nt) : group_grid<false, false>(nt));
         const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
+        static const bool all = [] {  // CWF_GROUP_GRID=all: one tile per workgroup (diagnostic)
+            const char *e = getenv("CWF_GROUP_GRID");
+            return e && std::string(e) == "all";
+        }();
+        if (all)
+            return need ? need : 8u;
         return g < need ? g : (need ? need : 8u);
     }
     if (s.t.hex)
@@ -1805,6 +1814,12 @@ unsigned fast_update_blocks(const DevSys &s, bool flush)
         {update_resident<2, false>(), update_resident<2, true>()}};
     const unsigned res = resident[upd_unroll() == 2][flush ? 1 : 0];
     const unsigned g = grid_for(s.N, kUpdThreads * (unsigned)upd_unroll());
+    static const bool all = [] {  // CWF_UPD_GRID=all: one node per thread, no grid stride (diagnostic)
+        const char *e = getenv("CWF_UPD_GRID");
+        return e && std::string(e) == "all";
+    }();
+    if (all)
+        return g ? g : 1u;
     return g < res ? (g ? g : 1u) : res;
 }
 
