@@ -153,28 +153,20 @@ __global__ __launch_bounds__(kBlock) void k_perm_copy(const uint32_t *__restrict
 // STREAM-like copy for the bandwidth probe: 16-B loads/stores per lane, four loads in flight per lane
 // before their stores, nontemporal (each byte is touched once)
 typedef float v4f __attribute__((ext_vector_type(4)));
+// one 16-B element per thread, one pass (no grid stride): the fastest copy form measured on MI355X
+// (tools/copy_probe.hip: 6.2-6.3 TB/s read + write; persistent grid-stride and blocked copies, plain or
+// nontemporal, 4.4-5.3 TB/s; one-pass with 2 / 4 / 8 rows per workgroup 5.8 / 5.6 / 4.3 TB/s)
 __global__ __launch_bounds__(256) void k_copy16(const v4f *__restrict__ a, v4f *__restrict__ b, uint64_t n)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride)
-    {
-        v4f v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            v[u] = __builtin_nontemporal_load(a + i + u * stride);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            __builtin_nontemporal_store(v[u], b + i + u * stride);
-    }
-    for (; i < n; i += stride)
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n)
         b[i] = a[i];
 }
 
 void copy16(const void *a, void *b, uint64_t bytes, hipStream_t st)
 {
     const uint64_t n = bytes / 16;
-    k_copy16<<<256 * 8, 256, 0, st>>>(static_cast<const v4f *>(a), static_cast<v4f *>(b), n);
+    k_copy16<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(static_cast<const v4f *>(a), static_cast<v4f *>(b), n);
 }
 
 void perm_gather(const uint32_t *perm, const float *src, float *dst, uint32_t N, int w, hipStream_t st)
