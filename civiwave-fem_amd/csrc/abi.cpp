@@ -543,7 +543,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 {
                     GroupTiles gt;
                     const uint32_t gnt = group_lanes(E);
-                    if (build_group_tiles(&md, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt) == 0 &&
+                    if (build_group_tiles(&md, gt, gnt, 2 * gnt, kGroupSlotsPerLane * gnt, false) == 0 &&
                         gt.tets_per_group >= 3.0)
                     {
                         own.assign(N, 0xFFFFFFFFu);

@@ -127,8 +127,9 @@ struct GroupTiles
     std::vector<uint32_t> tet_group;       // [E] group of each tet (validation)
 };
 // nt: lanes per workgroup (one group per lane); max_nodes <= 512 (9-bit local ids); slot_budget: LDS push slots
+// order_lanes: bank-aware lane order within each tile (groups.cpp); off where only the tiles' node sets matter
 int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
-                      uint32_t slot_budget);
+                      uint32_t slot_budget, bool order_lanes = true);
 
 constexpr uint32_t kPartOffBits = 0x1fffffffu;
 constexpr uint64_t kMaxFirstBatch = 4096;  // PCG iterations enqueued before the first control-block read-back

@@ -148,10 +148,97 @@ Fan walk_fan(const uint32_t *conn, const std::vector<uint32_t> &off, const std::
         F.t[i] = TT[head + i];
     return F;
 }
+
+// ds_read_b128 lane groups of a wave64 access (MI355X_MICROARCH.md §LDS): {0-3, 12-15, 20-27},
+// {4-11, 16-19, 28-31}, and the same two + 32
+inline uint32_t lane_group128(uint32_t l)
+{
+    const uint32_t h = (l & 63u) >= 32u ? 2u : 0u;
+    l &= 31u;
+    const bool g0 = l < 4u || (l >= 12u && l < 16u) || (l >= 20u && l < 28u);
+    return h + (g0 ? 0u : 1u);
+}
+
+// The fan kernel reads every group's 8 slot nodes from LDS by local id, all lanes in lockstep per slot:
+// {x y z v_x} by ds_read_b128 (bank 4 lid mod 64: conflict-free when the 16 lanes of a lane group have
+// distinct lid mod 16), {v_y v_z} by ds_read_b64 (32-lane groups, lid mod 32) and the u16 run start
+// (32-lane groups, (lid / 2) mod 32); then it pushes one force per used slot, {f_x, f_y} by ds_write_b64
+// (16-lane groups, bank 2 q mod 32) and f_z by ds_write_b32 (32-lane groups, q mod 32) at q = the node's run
+// start + the group's rank in the run. In RCB order those addresses collide often: the C2 kernel's group
+// phase spent 1.16M extra LDS cycles per launch on bank conflicts (tools/lds_ablate.sh; tools/tile_stats.cpp
+// models the same count: 0.51M from the reads, 0.63M from the pushes). Greedy, lane by lane: take, among the
+// next W unplaced groups, the one adding the fewest same-bank accesses to its lane groups (ranks follow the
+// placement order, so a candidate's push positions are known; ties: the earliest, so RCB order is the
+// fallback). The fold order follows the new lane order.
+template <typename SlotNode, typename SlotsUsed>
+void order_lanes_by_bank(const std::vector<Fan> &fans, const SlotNode &slot_node, const SlotsUsed &slots_used,
+                         const std::vector<uint32_t> &local, const std::vector<uint32_t> &start,
+                         std::vector<uint32_t> &placed, uint32_t *grp, uint32_t ng)
+{
+    constexpr uint32_t W = 32;
+    const uint32_t nw = (ng + 63u) / 64u;
+    std::vector<uint8_t> c128(nw * 4u * 8u * 16u, 0), c64(nw * 2u * 8u * 32u, 0), c16(nw * 2u * 8u * 32u, 0);
+    std::vector<uint8_t> cw64(nw * 4u * 8u * 16u, 0), cw32(nw * 2u * 8u * 32u, 0);
+    uint32_t lid[8], q[8];
+    const auto slots = [&](const Fan &F) {  // local ids and push positions of F placed next
+        const int su = slots_used(F);
+        for (int s = 0; s < 8; ++s)
+        {
+            lid[s] = local[slot_node(F, s)];
+            uint32_t dup = 0;  // a closing repeat pushes to r_0 twice
+            for (int r = 0; r < s; ++r)
+                dup += r < su && lid[r] == lid[s];
+            q[s] = s < su ? start[lid[s]] + placed[lid[s]] + dup : ~0u;
+        }
+    };
+    for (uint32_t L = 0; L < ng; ++L)
+    {
+        const uint32_t w = L / 64u, g128 = lane_group128(L), g32 = (L & 63u) >> 5, g16 = (L & 63u) >> 4;
+        uint8_t *a = &c128[(w * 4u + g128) * 8u * 16u];
+        uint8_t *b = &c64[(w * 2u + g32) * 8u * 32u];
+        uint8_t *c = &c16[(w * 2u + g32) * 8u * 32u];
+        uint8_t *d = &cw64[(w * 4u + g16) * 8u * 16u];
+        uint8_t *e = &cw32[(w * 2u + g32) * 8u * 32u];
+        uint32_t best = L, best_cost = ~0u;
+        const uint32_t end = std::min(ng, L + W);
+        for (uint32_t k = L; k < end && best_cost; ++k)
+        {
+            slots(fans[grp[k]]);
+            uint32_t cost = 0;
+            for (int s = 0; s < 8; ++s)
+            {
+                cost += a[s * 16 + (lid[s] & 15u)] + b[s * 32 + (lid[s] & 31u)] + c[s * 32 + ((lid[s] >> 1) & 31u)];
+                if (q[s] != ~0u)
+                    cost += d[s * 16 + (q[s] & 15u)] + e[s * 32 + (q[s] & 31u)];
+            }
+            if (cost < best_cost)
+            {
+                best_cost = cost;
+                best = k;
+            }
+        }
+        std::rotate(grp + L, grp + best, grp + best + 1);
+        slots(fans[grp[L]]);
+        for (int s = 0; s < 8; ++s)
+        {
+            ++a[s * 16 + (lid[s] & 15u)];
+            ++b[s * 32 + (lid[s] & 31u)];
+            ++c[s * 32 + ((lid[s] >> 1) & 31u)];
+            if (q[s] != ~0u)
+            {
+                ++d[s * 16 + (q[s] & 15u)];
+                ++e[s * 32 + (q[s] & 31u)];
+            }
+        }
+        for (int s = 0; s < 8; ++s)
+            if (q[s] != ~0u)
+                ++placed[lid[s]];
+    }
+}
 }  // namespace
 
 int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
-                      uint32_t slot_budget)
+                      uint32_t slot_budget, bool order_lanes)
 {
     out = GroupTiles{};
     const uint64_t N = d->node_count, E = d->element_count;
@@ -277,8 +364,12 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
         sscanf(rv, "%d,%d", &tdiv, &wdiv);
     rcb_partition(cen, gext, order, nt, leaf_end, tdiv, wdiv);
 
+    // lanes of a tile ordered against LDS bank conflicts (order_lanes_by_bank; CWF_GROUP_LANES=0 keeps the
+    // RCB order, diagnostic)
+    const char *gl = getenv("CWF_GROUP_LANES");
+    const bool lanes_by_bank = order_lanes && !(gl && gl[0] == '0');
     // tiles: each RCB leaf, split greedily while its node list would exceed max_nodes
-    std::vector<uint32_t> stamp(N, ~0u), local(N, 0), tcnt(N, 0);
+    std::vector<uint32_t> stamp(N, ~0u), local(N, 0), tcnt(N, 0), placed;
     std::vector<uint32_t> nodes, cnt, cur;
     out.hdr.clear();
     out.grec.resize(G);
@@ -359,6 +450,11 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
         if (out.max_tile_slots > slot_budget)
             return -3;  // cannot happen for slot_budget >= 10 nt: <= 8 pushes per group + 1 pad per node
         cur.assign(start.begin(), start.end());
+        if (lanes_by_bank)
+        {
+            placed.assign(nn, 0);
+            order_lanes_by_bank(fans, slot_node, slots_used, local, start, placed, order.data() + p0, ng);
+        }
         const uint32_t nb = (uint32_t)out.tile_nodes.size();
         for (uint64_t q = p0; q < p; ++q)
         {
