@@ -209,12 +209,16 @@ bool groups_enabled()
     return !(gv && gv[0] == '0');
 }
 
-// fan-group tile lanes: 256 (<= 256 groups, <= 512 nodes: T/N 1.59 against 1.77 on C3) where the mesh gives
-// every resident workgroup several tiles, else 128; CWF_GROUP_NT=128|256 overrides
+// fan-group tile lanes: 256 (<= 256 groups, <= 512 nodes: T/N 1.59 against 1.77 on C3, 1.60 against 1.76 on
+// C2). 128-lane tiles give C2's resident workgroups two tiles each instead of 1.7, but twice the workgroups
+// whose per-workgroup p.Ap shares every update workgroup refolds: with write-through partials C2 runs +2.3%
+// on 256 lanes (same-box A/B, two passes; 128 had been +6% before the partials were written through).
+// CWF_GROUP_NT=128|256 overrides
 uint32_t group_lanes(uint64_t E)
 {
+    (void)E;
     const char *gn = getenv("CWF_GROUP_NT");
-    return gn ? (atoi(gn) == 256 ? 256u : 128u) : (E >= 4000000ull ? 256u : 128u);
+    return gn && atoi(gn) == 128 ? 128u : 256u;
 }
 
 std::string pcg_error_message(int code, int iter, std::string *ctx)
@@ -804,7 +808,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     t.pipe_nt = (int)gnt;
                     {
                         const char *wt = getenv("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
-                        t.wt_part = wt ? (wt[0] == '1') : (gnt == 128);
+                        t.wt_part = wt ? (wt[0] == '1') : (E < 4000000ull);
                     }
                     t.ntiles = gt.ntiles;
                     t.ngroups = gt.ngroups;

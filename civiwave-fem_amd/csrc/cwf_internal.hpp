@@ -74,7 +74,7 @@ struct DevTiles
     int node_major = 0;
     // fan groups: partials stored write-through (sc1), so their lines leave L2 during the kernel instead of in
     // the end-of-kernel write-back the update pass waits for; only pays while the working set stays in the
-    // MALL (abi.cpp: 128-lane tiles, < 4M tets)
+    // MALL (abi.cpp: < 4M tets)
     int wt_part = 0;
     float *part = nullptr;                    // [3*total] tile-node partial sums, node-major (scratch)
 };

@@ -214,6 +214,19 @@ def test_fast_mode_apply_keff_close(case):
     assert np.max(np.abs(y - ref)) <= 2e-5 * np.max(np.abs(ref))
 
 
+def test_fast_mode_128_lane_tiles_close(case, monkeypatch):
+    """The 128-lane fan-group tiles (CWF_GROUP_NT=128, no longer the default) keep the FAST tolerance."""
+    monkeypatch.setenv("CWF_GROUP_NT", "128")
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rng = np.random.Generator(np.random.PCG64(5))
+    x = rng.uniform(-1, 1, case.packing.dof_count).astype(np.float32)
+    y = np.zeros_like(x)
+    pcg.apply_keff(s, x, y).value()
+    ref = o.apply_keff(x).astype(np.float64)
+    assert np.max(np.abs(y - ref)) <= 2e-5 * np.max(np.abs(ref))
+
+
 def test_fast_mode_solve_close(case):
     s = gpu_system(case, mode=_lib.MODE_FAST)
     o = oracle_system(case.packing, case.materials, *case.scalars())
