@@ -38,6 +38,18 @@ int hip_fail(cwf_hip_system *h, hipError_t e, const char *what)
     return set_error(h, CWF_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e), hipGetErrorName(e));
 }
 
+// hex8 tile lanes: 256 (<= 256 hexes, <= 512 nodes) from 1M hexes up, else 128. The per-workgroup p.Ap shares
+// every update workgroup refolds (and the r.r / r.z shares every hex workgroup refolds) halve with the
+// workgroup count: C3 hex8 +2.5-3.9% on 256 lanes, C2 hex8 -2.0-2.5% (same-box A/B, two passes).
+// CWF_HEX_NT=128|256 overrides
+uint32_t hex_tile_lanes(uint64_t hexes)
+{
+    const char *e = getenv("CWF_HEX_NT");
+    if (e)
+        return atoi(e) == 256 ? 256u : 128u;
+    return hexes >= 1000000ull ? 256u : 128u;
+}
+
 }  // namespace cwf
 
 using namespace cwf;
@@ -536,7 +548,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 if (hex)  // the hex tiles (tiles.cpp, 8 corners): the same owner = first tile of the node
                 {
                     HostTiles ht;
-                    build_tiles(&md, ht, 2u * kHexTileThreads, kHexTileThreads, 8);
+                    build_tiles(&md, ht, 2u * hex_tile_lanes(E), hex_tile_lanes(E), 8);
                     own.assign(N, 0xFFFFFFFFu);
                     for (uint32_t tl = 0; tl < ht.ntiles; ++tl)
                         for (uint32_t q = ht.tile_node_off[tl]; q < ht.tile_node_off[tl + 1]; ++q)
@@ -729,9 +741,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         // when the desc carries coordinates that reproduce its gradients (CWF_GEO=0 forces the records)
         const char *ge = getenv("CWF_GEO");
         t.geo = hex || ((!ge || ge[0] != '0') && d->node_coords && N && geometry_matches(d)) ? 1 : 0;
-        if (hex)  // k_keff_hex_tiles: kHexTileThreads lanes, one hex and two tile nodes per lane, push fold
+        if (hex)  // k_keff_hex_tiles: hex_nt lanes, one hex and two tile nodes per lane, push fold
         {
             t.hex = 1;
+            t.hex_nt = (int)hex_tile_lanes(E);
             t.push = 1;
         }
         else
@@ -833,7 +846,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 t.push = 1;  // the pipelined kernel folds pushed forces (epos), not local-CSR entries
             }
             if (hex)
-                build_tiles(d, ht, 2u * kHexTileThreads, kHexTileThreads, 8);
+                build_tiles(d, ht, 2u * (uint32_t)t.hex_nt, (uint32_t)t.hex_nt, 8);
             else
                 build_tiles(d, ht, t.pipe ? (uint32_t)t.pipe_nt : (uint32_t)kMaxTileNodes,
                             t.pipe ? 2u * (uint32_t)t.pipe_nt : (uint32_t)kTileElems);

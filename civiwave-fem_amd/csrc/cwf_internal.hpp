@@ -24,7 +24,8 @@ namespace cwf
 // FAST-mode element tiles (tiles.cpp): element-centric K_eff with deterministic LDS folds
 constexpr int kTileElems = 512;      // elements per tile (= per 256-thread workgroup)
 constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two node slots per thread)
-constexpr uint32_t kHexTileThreads = 128;  // hex8 tiles: <= 128 hexes and <= 256 nodes per 128-lane workgroup
+// hex8 tiles: <= NT hexes and <= 2 NT nodes per NT-lane workgroup, NT = hex_tile_lanes(E) (abi.cpp)
+uint32_t hex_tile_lanes(uint64_t hexes);
 // fan-group tiles of NT = 128 (meshes < 4M tets) or 256 lanes: <= NT groups (one per lane), <= 2 NT nodes
 // (two per lane; 9-bit local ids), <= kGroupSlotsPerLane NT pushed-force slots (padded runs, LDS) and <= 16
 // pushes per tile node (4-bit ranks in the record)
@@ -62,6 +63,7 @@ struct DevTiles
     // native hex8: k_keff_hex_tiles, 128-thread persistent grid (pipe_grid), push fold
     int hex = 0;
     int hex_all_affine = 0;        // every hex tile is a parallelepiped tile (affine-only kernel variant)
+    int hex_nt = 128;              // lanes per hex tile / workgroup (128 or 256)
     const uint4 *eid8 = nullptr;   // [E] 8 u16 local corner ids (Gmsh corner order)
     const uint4 *epos8 = nullptr;  // [E] 8 u16 local-CSR positions
     const uint32_t *node_part_off = nullptr;  // [N+1] node -> range of its tile slots (ascending tile); with

@@ -173,6 +173,32 @@ def test_gpu_hex8_apply_keff_matches_oracle(hcase):
 
 
 @pytest.mark.gpu
+def test_gpu_hex8_256_lane_tiles_apply_and_solve(hcase, monkeypatch):
+    """The 256-lane hex tiles (the default from 1M hexes; CWF_HEX_NT=256 forces them here) keep the apply
+    tolerance and the PCG solution of the 128-lane tiles."""
+    monkeypatch.setenv("CWF_HEX_NT", "256")
+    s = gpu_hex_system(hcase)
+    P = hcase.packing
+    sK, sM = hcase.scalars()
+    rng = np.random.Generator(np.random.PCG64(12))
+    x = rng.uniform(-1, 1, P.dof_count).astype(np.float32)
+    y = np.zeros_like(x)
+    pcg.apply_keff(s, x, y).value()
+    ref = O.hex8_apply(hcase.mesh.coords, hcase.mesh.tets, P.material_index, D_STEEL, sK, sM, P.lumped_mass,
+                       P.bc_mask, x).astype(np.float64)
+    assert np.max(np.abs(y - ref)) <= 2e-5 * np.max(np.abs(ref))
+    rhs = hcase.static_rhs()
+    x256 = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(2000, 1e-6), pcg.PcgVectors(x256, np.zeros_like(rhs))).value()
+    assert t.converged
+    monkeypatch.setenv("CWF_HEX_NT", "128")
+    x128 = np.zeros_like(rhs)
+    pcg.solve_pcg(gpu_hex_system(hcase), rhs, pcg.PcgSettings(2000, 1e-6),
+                  pcg.PcgVectors(x128, np.zeros_like(rhs))).value()
+    assert np.linalg.norm(x256 - x128) <= 1e-4 * np.linalg.norm(x128)
+
+
+@pytest.mark.gpu
 def test_gpu_hex8_block_jacobi_matches_oracle(hcase):
     s = gpu_hex_system(hcase)
     P = hcase.packing
