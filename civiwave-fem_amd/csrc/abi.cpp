@@ -745,6 +745,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         {
             t.hex = 1;
             t.hex_nt = (int)hex_tile_lanes(E);
+            const char *wt = getenv("CWF_TILES_WT");  // 0|1: write-through hex partials (diagnostic)
+            t.wt_part = wt && wt[0] == '1';
             t.push = 1;
         }
         else
