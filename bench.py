@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", help="BASELINE config key (c1..c5)")
     ap.add_argument("--mode", default="fast", choices=["fast", "parity"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = the config's block per GPU (N stacked copies), strong = the config's block "
+                         "split over the N GPUs (SURVEY 8e: C3's fixed 10.1M DOF at 1/2/4/8 GPUs). Unstructured "
+                         "configs (c4) always scale strong over an RCB node partition")
     ap.add_argument("--element", default="tet4", choices=["tet4", "hex8"],
                     help="tet4: the Kuhn expansion the reference runs (the headline); hex8: native hexes "
                          "(SURVEY 8f4, FAST only, parity unpinned)")
@@ -56,21 +60,56 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
 def cpu_baseline(case, sK, sM, iters):
-    """Oracle restatement of pcg.cpp solve_pcg, 1 thread, bounded: block-Jacobi setup + `iters` iterations."""
+    """The bit-exact CPU restatement (ours, oracle/cwf_oracle.c) of the reference's single-threaded solve_pcg,
+    pinned to one core of this host for the CPU leg only (os.sched_setaffinity on this thread, restored
+    afterwards): block-Jacobi setup + `iters` PCG iterations on the bench workload, plus a
+    full C1 solve to its tolerance. The restatement omits the reference's per-call validate_system and its unused
+    fp64 D*B product (pcg.cpp:82-139, 592-604), so it runs ~3x faster than the reference itself (the survey
+    measured 5.25 M DOF-it/s on C2)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from helpers import oracle_system  # noqa: E402
 
-    s = oracle_system(case.packing, case.materials, sK, sM)
-    rhs = case.static_rhs()
-    t0 = time.perf_counter()
-    out = s.solve_pcg(rhs, iters, 1e-30)
-    dt = time.perf_counter() - t0
-    it = out["telemetry"].iterations
+    from cwf import scenarios
+
+    prev = os.sched_getaffinity(0)
+    core = min(prev)
+    os.sched_setaffinity(0, {core})
+    try:
+        s = oracle_system(case.packing, case.materials, sK, sM)
+        rhs = case.static_rhs()
+        t0 = time.perf_counter()
+        out = s.solve_pcg(rhs, iters, 1e-30)
+        dt = time.perf_counter() - t0
+        it = out["telemetry"].iterations
+        c1 = scenarios.config_case("c1")
+        s1 = oracle_system(c1.packing, c1.materials, *c1.scalars())
+        t1 = time.perf_counter()
+        o1 = s1.solve_pcg(c1.static_rhs(), c1.cfg.solver.max_iterations, c1.cfg.solver.runtime_tolerance)
+        d1 = time.perf_counter() - t1
+    finally:
+        os.sched_setaffinity(0, prev)
+    it1 = o1["telemetry"].iterations
     return dict(value=case.packing.dof_count * it / dt, unit="DOF-it/s", cores=1, kind="port",
-                sample=f"{case.name}: oracle solve_pcg (block-Jacobi setup + {it} PCG iterations), "
-                       f"{dt:.2f} s, 1 thread, {os.cpu_count()} host CPUs visible")
+                label="bit-exact restatement (ours), not the reference binary",
+                cpu_model=cpu_model(), core=core, host_cpus=os.cpu_count(),
+                sample=f"{case.name}: oracle solve_pcg (block-Jacobi setup + {it} PCG iterations), {dt:.2f} s, "
+                       f"1 thread pinned to core {core}",
+                c1_full_solve={"iterations": int(it1), "seconds": d1, "pcg_iterations_per_sec": it1 / d1,
+                               "dof_it_per_sec": c1.packing.dof_count * it1 / d1,
+                               "converged": bool(o1["telemetry"].converged)})
 
 
 def hbm_roofline(L, device, key="c3", iters=200, sample=5):
@@ -115,6 +154,17 @@ def hbm_roofline(L, device, key="c3", iters=200, sample=5):
     return out
 
 
+def same_kernel(kname: str, profiled: str) -> bool:
+    """rocprofv3 names a kernel 'ns::name<args>' (optionally with its parameter list): the base name and the
+    template arguments must both match, so 'k_keff_tiles' is not taken for 'k_keff_tiles_pipe<...>'."""
+    def split(k):
+        k = k.split("(")[0].replace(" ", "")
+        base, _, args = k.partition("<")
+        return base.split("::")[-1], args
+
+    return split(kname) == split(profiled)
+
+
 def stream_copy_gbs(L, device, nbytes=2 << 30, reps=20):
     """STREAM-like 16-B-lane device copy measured on this GPU: read + write bytes / time."""
     import ctypes as C
@@ -153,6 +203,10 @@ def main():
     device = local_rank % ngpu if world > 1 else 0
     mode = _lib.MODE_FAST if args.mode == "fast" else _lib.MODE_PARITY
     comm = None
+    unstructured = bool(scenarios.meshgen.CONFIGS[args.config].get("jitter"))
+    strong = args.scaling == "strong" or unstructured
+    load_pattern = None  # (base, pattern) f64 in the stepper's node order, for a curve-scaled (harmonic) load
+    halo_nodes = 0
     if world == 1:
         case = scenarios.config_case(args.config, max_iterations=args.max_iterations, element=args.element)
         P = case.packing
@@ -160,10 +214,17 @@ def main():
         stepper = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode,
                           device=device)
         owned_dofs, local_nodes, local_tets = P.dof_count, P.node_count, P.element_count
+        if case.load_curve is not None:
+            load_pattern = case.load_pattern()
     else:
         if mode != _lib.MODE_FAST or args.element != "tet4":
-            raise SystemExit("multi-GPU runs the FAST tet4 path only")
-        case, node_global, begin = scenarios.slab_case(args.config, world, rank, max_iterations=args.max_iterations)
+            raise SystemExit("the multi-GPU bench runs the FAST tet4 path (the bit-exact sharded PARITY solve is "
+                             "the parity gate in tests/test_gpu_shard.py)")
+        if unstructured:  # C4: the whole mesh, RCB node partition, renumbered part after part
+            case, node_global, begin = scenarios.rcb_case(args.config, world, max_iterations=args.max_iterations)
+        else:
+            case, node_global, begin = scenarios.slab_case(args.config, world, rank,
+                                                           max_iterations=args.max_iterations, strong=strong)
         P = case.packing
         sK, sM = case.scalars()
         src = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=mode)  # host arrays only
@@ -183,11 +244,24 @@ def main():
         stepper = Stepper(_LocalPacking, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=mode,
                           device=device, system=system)
         owned_dofs, local_nodes, local_tets = 3 * sh.owned_nodes, sh.local_nodes, sh.local_elements
+        halo_nodes = sh.local_nodes - sh.owned_nodes
+        if case.load_curve is not None:
+            base, pattern = case.load_pattern()
+            load_pattern = (sh.local_dofs(base), sh.local_dofs(pattern))
+        del src
+    if load_pattern is not None:  # the harmonic tip load (C4), rewritten on the device before every step
+        stepper.set_load_pattern(*load_pattern)
+
+    def step(t):
+        if load_pattern is not None:
+            stepper.set_load_scale(case.load_scale(t))
+        return stepper.step(t).value()
+
     L = _lib.load()
     h = stepper.system.handle()
     t_sim = 0.0
     for w in range(args.warmup):
-        stepper.step(t_sim).value()
+        step(t_sim)
         t_sim += case.cfg.time.initial_dt
     import ctypes as C
 
@@ -197,7 +271,7 @@ def main():
     total_iters = 0
     t0 = time.perf_counter()
     for k in range(args.steps):
-        tel = stepper.step(t_sim).value()
+        tel = step(t_sim)
         total_iters += tel.pcg.iterations
         t_sim += case.cfg.time.initial_dt
     torch.cuda.synchronize()
@@ -208,7 +282,12 @@ def main():
     L.cwf_hip_system_set_timing(h, 0)
     D = owned_dofs
     local = np.array([elapsed, D * total_iters, total_iters, D], np.float64)
+    per_rank = [{"owned_dofs": int(D), "local_tets": int(local_tets), "halo_nodes": int(halo_nodes),
+                 "halo_bytes_per_exchange": 12 * int(halo_nodes), "seconds": elapsed}]
     if dist is not None:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank[0])
+        per_rank = gathered
         t = torch.from_numpy(local.copy())
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -238,7 +317,7 @@ def main():
     if tpath and os.path.exists(tpath):
         pmc = json.load(open(tpath))
         # only a profile of the same kernel counts (a committed profile of an older kernel is not this one's)
-        if any(kname in k for k in pmc.get("kernels", {})):
+        if any(same_kernel(kname, k) for k in pmc.get("kernels", {})):
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(tpath, ROOT)
     result = None
@@ -258,7 +337,7 @@ def main():
         cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_fast_pmc.json")))
         if cands:
             pmc = json.load(open(cands[-1]))
-            if any(hbm["kernel"] in k for k in pmc.get("kernels", {})):
+            if any(same_kernel(hbm["kernel"], k) for k in pmc.get("kernels", {})):
                 hbm["traffic"] = pmc.get("hbm_bytes_per_launch")
                 hbm["traffic_source"] = os.path.relpath(cands[-1], ROOT)
     if rank == 0:
@@ -275,16 +354,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if (strong and world > 1) or args.scaling == "strong" else "weak",
             "vs_baseline": None,
             "dtype": "f32" if args.mode == "fast" else "f64",
-            "data": "synthetic (structured hex block -> Kuhn tets, gravity + tip load)" if args.element == "tet4"
-                    else "synthetic (structured native hex8 block, gravity + tip load)",
+            "data": ("synthetic (native hex8 block, gravity + tip load)" if args.element == "hex8" else
+                     "synthetic (jittered + permuted hex block -> Kuhn tets, gravity + harmonic tip load "
+                     "F0 sin(2 pi 5 t) from a 64-point curve, rewritten on the device every step)"
+                     if load_pattern is not None else
+                     "synthetic (structured hex block -> Kuhn tets, gravity + tip load)"),
             "config": {"workload": case.name, "nodes_per_gpu": local_nodes,
                        ("hexes_per_gpu" if args.element == "hex8" else "tets_per_gpu"): local_tets,
                        "dofs": int(dofs_sum), "mode": args.mode,
-                       "parallelism": f"node-range shards x{world} (RCCL halo + all-gather)" if world > 1
-                       else "single"},
+                       "parallelism": (f"{'RCB' if unstructured else 'slab'} node-range shards x{world} "
+                                       f"(RCCL halo + all-gather, {'strong' if strong else 'weak'} scaling)")
+                       if world > 1 else "single"},
+            "ranks": per_rank if world > 1 else None,
             "pcg_iterations": int(iters_sum),
             "pcg_iterations_per_sec": iters_sum / world / elapsed,
             "dof_updates_per_sec": dofs_sum * args.steps / elapsed,

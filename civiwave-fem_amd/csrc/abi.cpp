@@ -258,10 +258,12 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     if (set.max_iterations == 0)
         return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
     const bool sharded = h->sharded();
-    if (sharded && h->mode != CWF_MODE_FAST)
-        return set_error(h, CWF_ERR_UNSUPPORTED, "sharded systems run in FAST mode only");
     if (!sharded && g.size() != 1)
         return set_error(h, CWF_ERR_ARGUMENT, "a group needs attached shards");
+    for (cwf_hip_system *m : g)
+        if (m->mode != h->mode)
+            return set_error(m, CWF_ERR_ARGUMENT, "every rank of a sharded solve runs in the same mode",
+                             "rank=" + std::to_string(m->rank));
     for (cwf_hip_system *m : g)
         if (m->hist_cap < set.max_iterations + 1)
         {
@@ -281,7 +283,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     const bool fast = h->mode == CWF_MODE_FAST;
     if (sharded)
     {
-        if (int e = sharded_pcg_init(g, rhs, set.relative_tolerance))
+        if (int e = fast ? sharded_pcg_init(g, rhs, set.relative_tolerance)
+                         : sharded_parity_init(g, rhs, set.relative_tolerance))
             return e;
     }
     else if (fast)
@@ -294,14 +297,17 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     uint64_t batch = set.check_interval > 0 ? std::min<uint64_t>((uint64_t)set.check_interval, kMaxBatch) : 4;
     // Batches end in a control-block read-back (a host round trip with the GPU idle) and overshoot the
     // converging iteration by up to a batch of no-op launches. Consecutive solves on one handle (warm-started
-    // Newmark steps) take similar iteration counts, so with no check interval set the first batch runs up to
-    // 24 short of the previous solve's count and the doubling restarts from 8 there: C2 steps ~17 read-backs
-    // and ~50 no-op iterations -> ~4 and <= 8 (the first solve of a handle doubles from 4). Every rank of a
-    // sharded solve has the same history (identical scalars), so their enqueued counts stay equal.
+    // Newmark steps) take similar iteration counts, so with no check interval set and the handle's last two
+    // solves within 25% of each other, the first batch runs up to 24 short of the smaller count and the
+    // doubling restarts from 4 there: C2 steps ~17 read-backs and ~50 no-op iterations -> ~4 and <= 8. A
+    // handle whose counts moved (its first solves, a static solve before Newmark steps, a changed tolerance)
+    // doubles from 4, so a solve that converges early never waits on a long queue of no-op launches. Every
+    // rank of a sharded solve has the same history (identical scalars), so their enqueued counts stay equal.
     uint64_t first = batch;
-    if (set.check_interval <= 0 && h->last_iters > 40)
+    const uint64_t lo = std::min(h->last_iters, h->prev_iters), hi = std::max(h->last_iters, h->prev_iters);
+    if (set.check_interval <= 0 && lo > 40 && 4 * hi <= 5 * lo)
     {
-        first = std::min<uint64_t>(h->last_iters - 24, kMaxFirstBatch);
+        first = std::min<uint64_t>(lo - 24, kMaxFirstBatch);
         batch = 4;
     }
     if (h->timing && h->ev.size() < 2 * std::max(first, kMaxBatch))
@@ -347,6 +353,11 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
                 if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
                     return e;
             }
+            else if (sharded)
+            {
+                if (int e = sharded_parity_iteration(g, rhs, e0, e1))
+                    return e;
+            }
             else
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
@@ -374,6 +385,7 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     for (cwf_hip_system *m : g)
     {
         m->hist_count = c.iterations + 1;
+        m->prev_iters = m->last_iters;
         m->last_iters = c.iterations;
     }
     if (tel)
@@ -460,7 +472,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     // validate_system (pcg.cpp:82-139)
     if (d->dof_count != N * 3)
         return set_error(nullptr, CWF_ERR_SIZE, "dof count mismatch (expected node_count * 3)",
-                         "node_count=" + std::to_string(N) + " dof_count=" + std::to_string(d->dof_count));
+                         "node_count=" + std::to_string(N) + "\ndof_count=" + std::to_string(d->dof_count));
     if (d->material_count == 0 || !d->material_stiffness)
         return set_error(nullptr, CWF_ERR_MATERIALS, "materials table is empty");
     if (d->reduction_block == 0)
@@ -473,7 +485,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         return set_error(nullptr, CWF_ERR_ARGUMENT, "null system array");
     if (N * 3 >= (1ull << 32) || E >= (1ull << 30))
         return set_error(nullptr, CWF_ERR_UNSUPPORTED, "mesh too large for one handle (shard it)",
-                         "nodes=" + std::to_string(N) + " elements=" + std::to_string(E));
+                         "nodes=" + std::to_string(N) + "\nelements=" + std::to_string(E));
     // hex8: all 8 connectivity slots used; tet4 pads slots 4..7 with UINT32_MAX
     const bool hex = E && d->element_connectivity[4] != 0xFFFFFFFFu;
     const int K = hex ? 8 : 4;
@@ -487,7 +499,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (d->element_material_index[e] >= d->material_count)
             return set_error(nullptr, CWF_ERR_MATERIAL_RANGE, "element references material out of range",
                              "element=" + std::to_string(e) +
-                                 " material_index=" + std::to_string(d->element_material_index[e]));
+                                 "\nmaterial_index=" + std::to_string(d->element_material_index[e]));
         if ((d->element_connectivity[e * 8 + 4] != 0xFFFFFFFFu) != hex)
             return set_error(nullptr, CWF_ERR_UNSUPPORTED, "mixed tet4/hex8 meshes are not supported",
                              "element=" + std::to_string(e));
@@ -495,7 +507,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             if (d->element_connectivity[e * 8 + a] >= N)
                 return set_error(nullptr, CWF_ERR_NODE_RANGE, "element connectivity references node out of range",
                                  "element=" + std::to_string(e) +
-                                     " node=" + std::to_string(d->element_connectivity[e * 8 + a]));
+                                     "\nnode=" + std::to_string(d->element_connectivity[e * 8 + a]));
     }
     // FAST handles renumber their nodes along a Morton curve (cwf_hip.h CWF_DESC_KEEP_NODE_ORDER): the
     // rest of create then sees a desc in internal order; perm converts at the boundary
@@ -699,7 +711,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             std::memcpy(off.data(), d->adjacency_offsets, (N + 1) * sizeof(uint32_t));
             if (off[N] != E * K)
                 return bail(set_error(h, CWF_ERR_SIZE, "adjacency size mismatch",
-                                      "expected=" + std::to_string(E * K) + " actual=" + std::to_string(off[N])));
+                                      "expected=" + std::to_string(E * K) + "\nactual=" + std::to_string(off[N])));
             for (uint64_t j = 0; j < E * K; ++j)
                 inc[j] = (d->adjacency_elements[j] << sh) | (d->adjacency_local[j] & (uint32_t)(K - 1));
         }
@@ -1263,7 +1275,7 @@ int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_
         return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
     if (n != h->ds.D)
         return set_error(h, CWF_ERR_SIZE, "displacement span size mismatch",
-                         "input=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+                         "input=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
     const float *uin = nullptr;
     if (int st = stage_vec(h, u, h->tmp, u_kind, 3, &uin))
         return st;
@@ -1306,7 +1318,7 @@ int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, 
         return st;
     if (n != h->ds.D)
         return set_error(h, CWF_ERR_SIZE, "input/output span size mismatch",
-                         "input=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+                         "input=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
     const float *xin = nullptr;
     if (int st = stage_vec(h, x, h->tmp, kind, 3, &xin))
         return st;
@@ -1329,7 +1341,7 @@ int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64
     const uint64_t req = 9ull * h->ds.N;
     if (n < req)
         return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
-                         "required=" + std::to_string(req) + " available=" + std::to_string(n));
+                         "required=" + std::to_string(req) + "\navailable=" + std::to_string(n));
     float *dst = kind == CWF_PTR_DEVICE && !h->perm ? inv_out : h->inv;
     if (dst == h->inv)
         h->inv_fast = false;  // overwritten with the unsymmetrised reference inverse
@@ -1352,7 +1364,7 @@ int cwf_hip_fast_block_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, in
     const uint64_t N = h->ds.N, req = 9ull * N;
     if (n < req)
         return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
-                         "required=" + std::to_string(req) + " available=" + std::to_string(n));
+                         "required=" + std::to_string(req) + "\navailable=" + std::to_string(n));
     if (h->mode != CWF_MODE_FAST)
         return set_error(h, CWF_ERR_ARGUMENT, "FAST-mode operator requested on a PARITY handle");
     fast_block_inverse(h, h->stream);
@@ -1405,7 +1417,7 @@ int cwf_hip_dot(cwf_hip_system *h, const float *a, const float *b, uint64_t n, i
         return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
     if (n != h->ds.D)
         return set_error(h, CWF_ERR_SIZE, "dot product span size mismatch",
-                         "lhs=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+                         "lhs=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
     const float *da = nullptr, *db = nullptr;
     if (int st = stage_in(h, a, h->tmp, n, kind, &da))
         return st;
@@ -1461,7 +1473,7 @@ int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_setting
         std::memset(telemetry, 0, sizeof *telemetry);
     if (n != h->ds.D)
         return set_error(h, CWF_ERR_SIZE, "rhs span size mismatch",
-                         "rhs=" + std::to_string(n) + " dofs=" + std::to_string(h->ds.D));
+                         "rhs=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
     if (settings->max_iterations == 0)
         return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
     const float *drhs = nullptr;
@@ -1481,8 +1493,8 @@ int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_setting
 }
 
 int cwf_hip_solve_pcg_group(cwf_hip_system *const *members, int32_t count, const float *const *rhs,
-                            const cwf_pcg_settings *settings, float *const *x_inout, int kind,
-                            cwf_pcg_telemetry *telemetry)
+                            const cwf_pcg_settings *settings, float *const *x_inout, float *const *residual_out,
+                            int kind, cwf_pcg_telemetry *telemetry)
 {
     if (!members || count < 1 || !rhs || !settings || !x_inout)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
@@ -1519,6 +1531,8 @@ int cwf_hip_solve_pcg_group(cwf_hip_system *const *members, int32_t count, const
     {
         cwf_hip_system *h = g[i];
         HIPTRY(h, hipMemcpyAsync(x_inout[i], h->x, h->ds.D * sizeof(float), back, h->stream));
+        if (residual_out && residual_out[i])
+            HIPTRY(h, hipMemcpyAsync(residual_out[i], h->r, h->ds.D * sizeof(float), back, h->stream));
         HIPTRY(h, hipStreamSynchronize(h->stream));
     }
     return st;
@@ -1551,6 +1565,7 @@ struct cwf_hip_stepper
     int warm_start = 1;
     float *u = nullptr, *v = nullptr, *a = nullptr, *up = nullptr, *vp = nullptr, *f = nullptr, *bcv = nullptr,
           *damp = nullptr, *kd = nullptr, *srhs = nullptr;
+    double *lbase = nullptr, *lpat = nullptr;  // cwf_hip_stepper_set_load_pattern: f64 [3N] each (internal order)
     std::vector<void *> owned;
 };
 
@@ -1723,7 +1738,12 @@ int cwf_hip_stepper_get_state(cwf_hip_stepper *t, int which, float *out, uint64_
         return st;
     if (n != h->ds.D)
         return set_error(h, CWF_ERR_SIZE, "state span size mismatch");
-    const float *src = which == 0 ? t->u : which == 1 ? t->v : which == 2 ? t->a : which == 3 ? h->x : nullptr;
+    const float *src = which == 0   ? t->u
+                       : which == 1 ? t->v
+                       : which == 2 ? t->a
+                       : which == 3 ? h->x
+                       : which == 4 ? t->f  // nodes.external_force (after set_load_scale / set_external_force)
+                                    : nullptr;
     if (!src)
         return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
     if (int st = vec_out(h, src, out, kind, 3))
@@ -1762,6 +1782,49 @@ int cwf_hip_stepper_set_external_force(cwf_hip_stepper *t, const float *f, uint6
     if (int st = vec_in(h, f, t->f, kind, 3))
         return st;
     HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_stepper_set_load_pattern(cwf_hip_stepper *t, const double *base, const double *pattern, uint64_t n)
+{
+    if (!t || !base || !pattern)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    cwf_hip_system *h = t->sys;
+    if (int st = check_ready(h))
+        return st;
+    if (n != h->ds.D)
+        return set_error(h, CWF_ERR_SIZE, "load pattern span size mismatch",
+                         "input=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
+    if (!t->lbase)
+    {
+        void *q = nullptr;
+        if (hipMalloc(&q, std::max<uint64_t>(2 * n, 2) * sizeof(double)) != hipSuccess)
+            return set_error(h, CWF_ERR_ALLOC, "failed to allocate stepper buffers");
+        t->owned.push_back(q);
+        t->lbase = static_cast<double *>(q);
+        t->lpat = t->lbase + n;
+    }
+    // a node's 3 f64 = 6 floats: the node-order conversion moves them as 6-float records
+    if (int st = vec_in(h, reinterpret_cast<const float *>(base), reinterpret_cast<float *>(t->lbase), CWF_PTR_HOST, 6))
+        return st;
+    if (int st = vec_in(h, reinterpret_cast<const float *>(pattern), reinterpret_cast<float *>(t->lpat), CWF_PTR_HOST,
+                        6))
+        return st;
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int cwf_hip_stepper_set_load_scale(cwf_hip_stepper *t, double scale)
+{
+    if (!t)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
+    cwf_hip_system *h = t->sys;
+    if (int st = check_ready(h))
+        return st;
+    if (!t->lbase)
+        return set_error(h, CWF_ERR_ARGUMENT, "no load pattern set", "cwf_hip_stepper_set_load_pattern");
+    stepper_scaled_load(h->ds.D, t->lbase, t->lpat, scale, t->f, h->stream);  // ordered before the next step
+    HIPTRY(h, hipGetLastError());
     return 0;
 }
 

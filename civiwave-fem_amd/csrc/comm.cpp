@@ -108,53 +108,60 @@ int nccl_fail(cwf_hip_system *h, ncclResult_t e, const char *what)
 
 }  // namespace
 
-// in-place all-gather of `count` doubles per rank: slot r of buf is [r * count, (r + 1) * count)
-int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count)
+// One exchange step of a sharded solve: in-place all-gathers of per-rank double slots (slot r of buf is
+// [r * count, (r + 1) * count)) and, optionally, the halo of one vector (ghost rows <- the owners' values). Over
+// RCCL every operation of the step is one ncclGroupStart/End, so the all-gathers and the halo send/recv pairs
+// of an iteration go out as one launch.
+int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
+                  float *cwf_hip_system::*vec)
 {
     cwf_hip_system *h0 = g[0];
-    if (h0->nranks == 1)
-        return 0;
-    if (h0->comm->kind == 1)
-    {
-        const Rccl *r = rccl(nullptr);
-        double *b = h0->*buf;
-        NCCLTRY(h0, r->AllGather(b + (size_t)h0->rank * count, b, count, ncclFloat64,
-                                 static_cast<ncclComm_t>(h0->comm->nccl), h0->stream));
-        return 0;
-    }
-    for (cwf_hip_system *dst : g)
-        for (cwf_hip_system *src : g)
-            if (dst != src)
-                HIPTRY(dst, hipMemcpyAsync(dst->*buf + (size_t)src->rank * count, src->*buf + (size_t)src->rank * count,
-                                           count * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
-    return 0;
-}
-
-// ghost rows of `vec` <- the owners' values
-int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec)
-{
-    for (cwf_hip_system *h : g)
-        halo_pack(h, h->*vec, h->stream);
-    cwf_hip_system *h0 = g[0];
+    if (vec)
+        for (cwf_hip_system *h : g)
+            halo_pack(h, h->*vec, h->stream);
+    const bool gather = h0->nranks > 1;
     if (h0->comm && h0->comm->kind == 1)
     {
+        if (!gather && !vec)
+            return 0;
         const Rccl *r = rccl(nullptr);
         ncclComm_t c = static_cast<ncclComm_t>(h0->comm->nccl);
-        float *v = h0->*vec;
         NCCLTRY(h0, r->GroupStart());
-        for (size_t k = 0; k < h0->nbr.size(); ++k)
+        if (gather)
+            for (const Gather &q : gathers)
+            {
+                double *b = h0->*(q.buf);
+                NCCLTRY(h0, r->AllGather(b + (size_t)h0->rank * q.count, b, q.count, ncclFloat64, c, h0->stream));
+            }
+        if (vec)
         {
-            const size_t ns = h0->send_off[k + 1] - h0->send_off[k], nr = h0->recv_off[k + 1] - h0->recv_off[k];
-            if (ns)
-                NCCLTRY(h0, r->Send(h0->sendbuf + 3 * h0->send_off[k], 3 * ns, ncclFloat32, h0->nbr[k], c, h0->stream));
-            if (nr)
-                NCCLTRY(h0, r->Recv(v + 3 * ((size_t)h0->ds.Nown + h0->recv_off[k]), 3 * nr, ncclFloat32, h0->nbr[k], c,
-                                    h0->stream));
+            float *v = h0->*vec;
+            for (size_t k = 0; k < h0->nbr.size(); ++k)
+            {
+                const size_t ns = h0->send_off[k + 1] - h0->send_off[k], nr = h0->recv_off[k + 1] - h0->recv_off[k];
+                if (ns)
+                    NCCLTRY(h0, r->Send(h0->sendbuf + 3 * h0->send_off[k], 3 * ns, ncclFloat32, h0->nbr[k], c,
+                                        h0->stream));
+                if (nr)
+                    NCCLTRY(h0, r->Recv(v + 3 * ((size_t)h0->ds.Nown + h0->recv_off[k]), 3 * nr, ncclFloat32,
+                                        h0->nbr[k], c, h0->stream));
+            }
         }
         NCCLTRY(h0, r->GroupEnd());
         return 0;
     }
-    // LOCAL: member m's ghosts from q = q's send segment for m
+    // LOCAL (every rank in this process, one shared stream): device copies
+    if (gather)
+        for (const Gather &q : gathers)
+            for (cwf_hip_system *dst : g)
+                for (cwf_hip_system *src : g)
+                    if (dst != src)
+                        HIPTRY(dst, hipMemcpyAsync(dst->*(q.buf) + (size_t)src->rank * q.count,
+                                                   src->*(q.buf) + (size_t)src->rank * q.count,
+                                                   q.count * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+    if (!vec)
+        return 0;
+    // member m's ghosts from q = q's send segment for m
     for (cwf_hip_system *m : g)
         for (size_t k = 0; k < m->nbr.size(); ++k)
         {
@@ -166,13 +173,23 @@ int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*ve
             const size_t nr = m->recv_off[k + 1] - m->recv_off[k], ns = q->send_off[j + 1] - q->send_off[j];
             if (nr != ns)
                 return set_error(m, CWF_ERR_COMM, "halo plans disagree",
-                                 "rank=" + std::to_string(m->rank) + " peer=" + std::to_string(q->rank));
+                                 "rank=" + std::to_string(m->rank) + "\npeer=" + std::to_string(q->rank));
             if (nr)
                 HIPTRY(m, hipMemcpyAsync((m->*vec) + 3 * ((size_t)m->ds.Nown + m->recv_off[k]),
                                          q->sendbuf + 3 * q->send_off[j], 3 * nr * sizeof(float),
                                          hipMemcpyDeviceToDevice, m->stream));
         }
     return 0;
+}
+
+int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count)
+{
+    return comm_exchange(g, {Gather{buf, count}}, nullptr);
+}
+
+int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec)
+{
+    return comm_exchange(g, {}, vec);
 }
 
 // solve_pcg prologue (pcg.cpp:744-828) for a sharded system: owned-row dots, gathered scalars, halos
@@ -217,7 +234,8 @@ int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<c
     return 0;
 }
 
-// one FAST PCG iteration of every member (a single unsharded handle is the group {h} with one rank)
+// one FAST PCG iteration of every member (a single unsharded handle is the group {h} with one rank): two
+// exchange steps, p.Ap after the tiles kernel and {r.r, r.z} + the z halo (one RCCL group) after the update
 int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
                              unsigned it, hipEvent_t e0, hipEvent_t e1)
 {
@@ -232,9 +250,152 @@ int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::
         fast_update_pcg(g[i], rhs[i], it, g[i]->stream);
         fast_fold_rrz(g[i], it, g[i]->stream);
     }
-    if (int st = comm_allgather(g, &cwf_hip_system::g_rrz, 2))
+    return comm_exchange(g, {Gather{&cwf_hip_system::g_rrz, 2}}, g[0]->sharded() ? &cwf_hip_system::z : nullptr);
+}
+
+// ---- sharded PARITY (SURVEY.md 8e parity gate): the reference's fold orders across ranks --------------------
+// Each rank's owned nodes are one contiguous range of global node ids, ascending by rank from node 0, and every
+// rank but the last owns a whole number of reduction chunks (3 * owned % reduction_block == 0). Then a rank's
+// k-th local chunk is global chunk (3 begin / B) + k, and the all-gathered per-rank chunk partials, folded
+// rank after rank, are the global chunk partials folded in pcg.cpp:170-207 order (a rank's slot is padded with
+// +0.0 past its own chunks; a sequential fp64 sum that starts at +0.0 is never -0.0, so adding +0.0 is exact).
+// Owned K_eff / block-Jacobi rows are complete node gathers over the rank's elements in ascending global
+// element order, bitwise the single-handle rows. Ghost rows of x / r / z are never read; p is refreshed on the
+// ghosts by one halo after each p update. So every scalar, the residual history and every owned vector entry
+// equal the single-handle PARITY solve bit for bit.
+namespace
+{
+int parity_setup(const std::vector<cwf_hip_system *> &g)
+{
+    cwf_hip_system *h0 = g[0];
+    const int n = h0->nranks;
+    // (first global node, owned nodes) of every rank, gathered through the init-scalar slots
+    for (cwf_hip_system *h : g)
+    {
+        const double v[2] = {(double)h->gbegin, (double)h->ds.Nown};
+        HIPTRY(h, hipMemcpyAsync(h->g_init + 2 * h->rank, v, sizeof v, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::g_init, 2))
         return st;
-    return g[0]->sharded() ? comm_halo(g, &cwf_hip_system::z) : 0;
+    std::vector<double> ranges(2 * (size_t)n);
+    HIPTRY(h0, hipStreamSynchronize(h0->stream));
+    HIPTRY(h0, hipMemcpy(ranges.data(), h0->g_init, ranges.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const uint64_t B = h0->reduction_block ? h0->reduction_block : 1;
+    uint64_t next = 0, stride = 1;
+    for (int r = 0; r < n; ++r)
+    {
+        const uint64_t begin = (uint64_t)ranges[2 * r], owned = (uint64_t)ranges[2 * r + 1];
+        if (begin != next || (r + 1 < n && (3 * owned) % B != 0))
+            return set_error(h0, CWF_ERR_UNSUPPORTED,
+                             "sharded PARITY needs contiguous owned node ranges, ascending by rank from node 0, "
+                             "each but the last a whole number of reduction blocks",
+                             "rank=" + std::to_string(r) + "\nfirst_node=" + std::to_string(begin) +
+                                 "\nowned_nodes=" + std::to_string(owned));
+        next = begin + owned;
+        stride = std::max<uint64_t>(stride, (3 * owned + B - 1) / B);
+    }
+    for (cwf_hip_system *h : g)
+    {
+        if (!h->owned_contiguous)
+            return set_error(h, CWF_ERR_UNSUPPORTED, "sharded PARITY needs the rank's owned nodes in ascending "
+                                                     "contiguous global order", "rank=" + std::to_string(h->rank));
+        if (h->pstride == stride && h->gp0)
+            continue;
+        void *q = nullptr;
+        const size_t bytes = 2 * (size_t)n * stride * sizeof(double);
+        if (hipMalloc(&q, bytes) != hipSuccess)
+            return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer", "bytes=" + std::to_string(bytes));
+        h->owned.push_back(q);
+        h->bytes += bytes;
+        h->gp0 = static_cast<double *>(q);
+        h->gp1 = h->gp0 + (size_t)n * stride;
+        HIPTRY(h, hipMemset(h->gp0, 0, bytes));  // the +0.0 padding of every slot
+        h->pstride = (uint32_t)stride;
+    }
+    return 0;
+}
+
+inline uint32_t owned_dofs(const cwf_hip_system *h) { return 3u * h->ds.Nown; }
+inline uint32_t block_of(const cwf_hip_system *h) { return (uint32_t)(h->reduction_block ? h->reduction_block : 1); }
+}  // namespace
+
+int sharded_parity_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+{
+    if (int st = parity_setup(g))
+        return st;
+    const uint32_t S = g[0]->pstride, total = (uint32_t)g[0]->nranks * S;
+    for (cwf_hip_system *h : g)
+    {
+        parity_block_jacobi(h, h->inv, h->stream);
+        h->inv_fast = false;
+    }
+    if (int st = comm_halo(g, &cwf_hip_system::x))  // warm start: ghost x from the owners
+        return st;
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        cwf_hip_system *h = g[i];
+        const size_t slot = (size_t)h->rank * S;
+        parity_keff(h, h->x, h->Ap, true, nullptr, h->stream);
+        launch_init_residual(h, rhs[i], h->stream);
+        parity_dot_partials_n(owned_dofs(h), block_of(h), rhs[i], rhs[i], nullptr, h->gp0 + slot, nullptr, nullptr,
+                              h->stream);
+        parity_dot_partials_n(owned_dofs(h), block_of(h), h->r, h->r, nullptr, h->gp1 + slot, nullptr, nullptr,
+                              h->stream);
+    }
+    if (int st = comm_exchange(g, {Gather{&cwf_hip_system::gp0, S}, Gather{&cwf_hip_system::gp1, S}}, nullptr))
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        parity_init_scalars(h, h->gp0, h->gp1, total, rel_tol, h->stream);
+        launch_precond(h, h->ctl, h->stream);
+        parity_dot_partials_n(owned_dofs(h), block_of(h), h->r, h->z, nullptr, h->gp0 + (size_t)h->rank * S, nullptr,
+                              h->ctl, h->stream);
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::gp0, S))
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        parity_init_rho(h, h->gp0, total, h->stream);
+        launch_p_init(h, h->stream);
+    }
+    return comm_halo(g, &cwf_hip_system::p);
+}
+
+int sharded_parity_iteration(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
+                             hipEvent_t e0, hipEvent_t e1)
+{
+    const uint32_t S = g[0]->pstride, total = (uint32_t)g[0]->nranks * S;
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        cwf_hip_system *h = g[i];
+        if (i == 0 && e0)
+            (void)hipEventRecord(e0, h->stream);
+        parity_keff(h, h->p, h->Ap, false, h->ctl, h->stream);
+        if (i == 0 && e1)
+            (void)hipEventRecord(e1, h->stream);
+        parity_dot_partials_n(owned_dofs(h), block_of(h), h->p, h->Ap, nullptr, h->gp0 + (size_t)h->rank * S, nullptr,
+                              h->ctl, h->stream);
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::gp0, S))
+        return st;
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        cwf_hip_system *h = g[i];
+        const size_t slot = (size_t)h->rank * S;
+        parity_alpha(h, h->gp0, total, h->stream);
+        parity_update(h, rhs[i], h->stream);
+        parity_dot_partials_n(owned_dofs(h), block_of(h), h->r, h->r, h->z, h->gp0 + slot, h->gp1 + slot, h->ctl,
+                              h->stream);
+    }
+    if (int st = comm_exchange(g, {Gather{&cwf_hip_system::gp0, S}, Gather{&cwf_hip_system::gp1, S}}, nullptr))
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        parity_beta(h, h->gp0, h->gp1, total, h->stream);
+        parity_p_update(h, h->stream);
+    }
+    return comm_halo(g, &cwf_hip_system::p);
 }
 
 }  // namespace cwf
@@ -359,7 +520,7 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         return set_error(h, CWF_ERR_ARGUMENT, "communicator and handle are on different devices");
     if (plan->local_nodes != h->ds.N || plan->owned_nodes > h->ds.N)
         return set_error(h, CWF_ERR_SIZE, "halo plan does not match the handle",
-                         "local_nodes=" + std::to_string(plan->local_nodes) + " handle_nodes=" + std::to_string(h->ds.N));
+                         "local_nodes=" + std::to_string(plan->local_nodes) + "\nhandle_nodes=" + std::to_string(h->ds.N));
     const uint32_t K = plan->neighbor_count;
     if (K && (!plan->neighbor_ranks || !plan->send_offsets || !plan->recv_offsets ||
               (plan->send_offsets[K] && !plan->send_nodes)))
@@ -410,10 +571,19 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         h->recv_off.assign(1, 0);
     }
     h->ds.Nown = (uint32_t)plan->owned_nodes;
+    h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
+    h->owned_contiguous = true;  // PARITY shards fold chunk partials in global order (comm.cpp parity_setup)
+    if (plan->node_global)
+        for (uint64_t i = 1; i < plan->owned_nodes; ++i)
+            if (plan->node_global[i] != h->gbegin + i)
+            {
+                h->owned_contiguous = false;
+                break;
+            }
+    h->pstride = 0;
     h->comm = cm;
     h->rank = rank;
     h->nranks = n;
-    h->mode = CWF_MODE_FAST;
     if (cm->kind == 0)
     {
         HIPTRY(h, hipStreamSynchronize(h->stream));

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -26,7 +27,7 @@ constexpr int kTileElems = 512;      // elements per tile (= per 256-thread work
 constexpr int kMaxTileNodes = 512;  // distinct nodes per tile (LDS bound; two node slots per thread)
 // hex8 tiles: <= NT hexes and <= 2 NT nodes per NT-lane workgroup, NT = hex_tile_lanes(E) (abi.cpp)
 uint32_t hex_tile_lanes(uint64_t hexes);
-// fan-group tiles of NT = 128 (meshes < 4M tets) or 256 lanes: <= NT groups (one per lane), <= 2 NT nodes
+// fan-group tiles of NT = 256 lanes (group_lanes(), abi.cpp; 128 on request): <= NT groups (one per lane), <= 2 NT nodes
 // (two per lane; 9-bit local ids), <= kGroupSlotsPerLane NT pushed-force slots (padded runs, LDS) and <= 16
 // pushes per tile node (4-bit ranks in the record)
 constexpr uint32_t kGroupSlotsPerLane = 12;
@@ -133,11 +134,13 @@ struct GroupTiles
 int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
                       uint32_t slot_budget, bool order_lanes = true);
 
-constexpr uint32_t kPartOffBits = 0x1fffffffu;
-constexpr uint64_t kMaxFirstBatch = 4096;  // PCG iterations enqueued before the first control-block read-back
+constexpr uint32_t kPartOffBits = 0x1fffffffu;  // node_part_off value bits (the rest: bc_mask, off_mask)
+// cap of the first batch of PCG iterations enqueued before the first control-block read-back (abi.cpp: sized from
+// the handle's last two solves when they agree)
+constexpr uint64_t kMaxFirstBatch = 2048;
 // FAST PCG applies x += alpha_j p_j every kXLag iterations, from the last kXLag search directions (one p
 // buffer each, rotating), instead of re-reading x and p every iteration
-constexpr unsigned kXLag = 4;  // node_part_off value bits (the rest: bc_mask, off_mask)
+constexpr unsigned kXLag = 4;
 
 struct DevSys
 {
@@ -222,7 +225,7 @@ struct cwf_hip_system
     double *hist = nullptr;        // device residual history
     uint64_t hist_cap = 0;
     uint64_t hist_count = 0;
-    uint64_t last_iters = 0;  // iterations of the previous solve on this handle (the first batch's size)
+    uint64_t last_iters = 0, prev_iters = 0;  // iterations of the last two solves on this handle (first batch size)
     std::string err, ctx;
     // live K_eff timing (cwf_hip_system_set_timing)
     int timing = 0;
@@ -243,6 +246,13 @@ struct cwf_hip_system
     double *g_rrz = nullptr;   // [2 nranks]    {r.r, r.z}
     double *g_init = nullptr;  // [2 nranks]    {rhs.rhs, r0.r0}
     double *g_rz0 = nullptr;   // [nranks]      r0.z0
+    // sharded PARITY: every rank's 256-DOF chunk partials all-gathered into slot [r * pstride, (r+1) * pstride)
+    // (zero-padded past the rank's own chunk count) and folded in that order on every rank = the global chunk
+    // order of pcg.cpp:170-207, since the owned node ranges are ascending by rank and aligned to whole chunks
+    double *gp0 = nullptr, *gp1 = nullptr;
+    uint32_t pstride = 0;
+    uint64_t gbegin = 0;            // global id of the first owned node (cwf_hip_system_attach)
+    bool owned_contiguous = false;  // owned local i = global gbegin + i
     bool sharded() const { return nranks > 1 || comm != nullptr; }
 };
 
@@ -270,7 +280,16 @@ void parity_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st);
 void hex_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st);  // hex8 diagonal blocks -> inverse
 void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b, const float *c, double *pab,
                          double *pac, const Ctl *ctl, hipStream_t st);
+void parity_dot_partials_n(uint32_t D, uint32_t B, const float *a, const float *b, const float *c, double *pab,
+                           double *pac, const Ctl *ctl, hipStream_t st);
 void parity_fold(const double *part, uint32_t count, double *out, hipStream_t st);
+void parity_init_scalars(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count, double rel_tol,
+                         hipStream_t st);
+void parity_init_rho(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st);
+void parity_alpha(cwf_hip_system *h, const double *p_pap, uint32_t count, hipStream_t st);
+void parity_update(cwf_hip_system *h, const float *rhs, hipStream_t st);
+void parity_beta(cwf_hip_system *h, const double *p_rr, const double *p_rz, uint32_t count, hipStream_t st);
+void parity_p_update(cwf_hip_system *h, hipStream_t st);
 void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
 void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
@@ -313,9 +332,19 @@ void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const dou
                                uint32_t stride, double rel_tol, hipStream_t st);
 void fast_rho_from(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st);
 // comm.cpp
+struct Gather
+{
+    double *cwf_hip_system::*buf;
+    size_t count;
+};
+int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
+                  float *cwf_hip_system::*vec);
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);
 int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec);
 int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
+int sharded_parity_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
+int sharded_parity_iteration(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
+                             hipEvent_t e0, hipEvent_t e1);
 int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
                              unsigned it, hipEvent_t e0, hipEvent_t e1);
 
@@ -328,5 +357,7 @@ void stepper_rhs_damping(uint32_t D, float *rhs, const float *kd, float bf, hipS
 void stepper_clamp(uint32_t N, const uint32_t *mask, const float *bcv, const float *u, float *rhs, hipStream_t st);
 void stepper_update(uint32_t D, const float *x, const float *up, const float *vp, float *u, float *v, float *a,
                     float ib, float gob, hipStream_t st);
+void stepper_scaled_load(uint32_t D, const double *base, const double *pattern, double scale, float *f,
+                         hipStream_t st);
 
 }  // namespace cwf

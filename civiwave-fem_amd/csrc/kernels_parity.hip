@@ -810,11 +810,11 @@ void parity_block_jacobi(const cwf_hip_system *h, float *inv, hipStream_t st)
     k_block_jacobi_parity<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, inv);
 }
 
-void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b, const float *c, double *pab,
-                         double *pac, const Ctl *ctl, hipStream_t st)
+void parity_dot_partials_n(uint32_t D, uint32_t B, const float *a, const float *b, const float *c, double *pab,
+                           double *pac, const Ctl *ctl, hipStream_t st)
 {
-    const uint32_t D = h->ds.D, B = (uint32_t)(h->reduction_block ? h->reduction_block : 1);
-    const uint32_t chunks = parity_chunk_count(h);
+    B = B ? B : 1;
+    const uint32_t chunks = (uint32_t)(((uint64_t)D + B - 1) / B);
     if (chunks == 0)
         return;
     if (B == 256)
@@ -833,6 +833,12 @@ void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b
             k_dot_chunks_generic<1><<<grid_for(chunks, kBlock), kBlock, 0, st>>>(a, b, c, D, B, chunks, pab, pac,
                                                                                 ctl);
     }
+}
+
+void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b, const float *c, double *pab,
+                         double *pac, const Ctl *ctl, hipStream_t st)
+{
+    parity_dot_partials_n(h->ds.D, (uint32_t)h->reduction_block, a, b, c, pab, pac, ctl, st);
 }
 
 void parity_fold(const double *part, uint32_t count, double *out, hipStream_t st)
@@ -871,6 +877,39 @@ void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
     parity_dot_partials(h, h->r, h->z, nullptr, h->part0, nullptr, h->ctl, st);
     k_pcg_init_rho<<<1, 1, 0, st>>>(h->ctl, h->part0, chunks);
     k_p_init<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
+}
+
+// ---- the scalar and node phases of solve_pcg, for the sharded PARITY schedule (comm.cpp), which folds the
+// all-gathered chunk partials of every rank in global chunk order ----
+void parity_init_scalars(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count, double rel_tol,
+                         hipStream_t st)
+{
+    k_pcg_init_scalars<<<1, 1, 0, st>>>(h->ctl, p_rhs, p_rr, count, rel_tol, h->hist);
+}
+
+void parity_init_rho(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st)
+{
+    k_pcg_init_rho<<<1, 1, 0, st>>>(h->ctl, p_rz, count);
+}
+
+void parity_alpha(cwf_hip_system *h, const double *p_pap, uint32_t count, hipStream_t st)
+{
+    k_pcg_alpha<<<1, 1, 0, st>>>(h->ctl, p_pap, count);
+}
+
+void parity_update(cwf_hip_system *h, const float *rhs, hipStream_t st)
+{
+    k_update<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl);
+}
+
+void parity_beta(cwf_hip_system *h, const double *p_rr, const double *p_rz, uint32_t count, hipStream_t st)
+{
+    k_pcg_beta<<<1, 1, 0, st>>>(h->ctl, p_rr, p_rz, count, h->hist);
+}
+
+void parity_p_update(cwf_hip_system *h, hipStream_t st)
+{
+    k_p_update<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, h->z, h->p, h->ctl);
 }
 
 // one PCG iteration (pcg.cpp:830-915); no-op once ctl->active == 0

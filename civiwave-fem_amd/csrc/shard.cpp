@@ -50,7 +50,7 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
                          "hex8 (SURVEY 8f4) runs on one handle");
     if (nranks < 1 || rank < 0 || rank >= nranks)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "rank out of range",
-                         "nranks=" + std::to_string(nranks) + " rank=" + std::to_string(rank));
+                         "nranks=" + std::to_string(nranks) + "\nrank=" + std::to_string(rank));
     for (int32_t q = 0; q < nranks; ++q)
         if (rank_node_begin[q + 1] < rank_node_begin[q])
             return set_error(nullptr, CWF_ERR_ARGUMENT, "rank node ranges must be non-decreasing",
@@ -74,7 +74,7 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
             {
                 delete s;
                 return set_error(nullptr, CWF_ERR_NODE_RANGE, "node outside every rank's range",
-                                 "node=" + std::to_string(n) + " global=" + std::to_string(g));
+                                 "node=" + std::to_string(n) + "\nglobal=" + std::to_string(g));
             }
             owner[n] = (int32_t)(std::upper_bound(rank_node_begin, rank_node_begin + nranks + 1, g) -
                                  rank_node_begin) - 1;
@@ -91,7 +91,7 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
                 {
                     delete s;
                     return set_error(nullptr, CWF_ERR_NODE_RANGE, "element connectivity references node out of range",
-                                     "element=" + std::to_string(e) + " node=" + std::to_string(c[a]));
+                                     "element=" + std::to_string(e) + "\nnode=" + std::to_string(c[a]));
                 }
                 mine |= owner[c[a]] == rank;
             }

@@ -92,6 +92,30 @@ __global__ __launch_bounds__(kBlock) void k_state_update(uint32_t D, const float
     a[i] = ib * dx;
     v[i] = vp[i] + gob * dx;
 }
+
+// external_force = safe_cast(base + scale * pattern) (loads.cpp:87-174 with one curve-scaled load pattern,
+// then pack.cpp:41-57): the per-step rewrite of nodes.external_force the viewer does on the host
+// (viewer.cpp:262-266), on the device
+__global__ __launch_bounds__(kBlock) void k_scaled_load(uint32_t D, const double *__restrict__ base,
+                                                        const double *__restrict__ pattern, double scale,
+                                                        float *__restrict__ f)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= D)
+        return;
+    const double v = base[i] + scale * pattern[i];
+    const double fmax = 3.4028234663852886e38;  // FLT_MAX
+    float out;
+    if (!isfinite(v))
+        out = v > 0.0 ? __int_as_float(0x7f800000) : v < 0.0 ? __int_as_float((int)0xff800000u) : __int_as_float(0x7fc00000);
+    else if (v > fmax)
+        out = 3.4028234663852886e38f;
+    else if (v < -fmax)
+        out = -3.4028234663852886e38f;
+    else
+        out = (float)v;
+    f[i] = out;
+}
 }  // namespace
 
 void stepper_predictor(uint32_t D, const float *u, const float *v, const float *a, float *up, float *vp, double dt,
@@ -129,6 +153,12 @@ void stepper_update(uint32_t D, const float *x, const float *up, const float *vp
 {
     if (D)
         k_state_update<<<grid_for(D), kBlock, 0, st>>>(D, x, up, vp, u, v, a, ib, gob);
+}
+
+void stepper_scaled_load(uint32_t D, const double *base, const double *pattern, double scale, float *f, hipStream_t st)
+{
+    if (D)
+        k_scaled_load<<<grid_for(D), kBlock, 0, st>>>(D, base, pattern, scale, f);
 }
 
 }  // namespace cwf

@@ -150,6 +150,8 @@ def load() -> C.CDLL:
         "cwf_hip_stepper_set_state": ([P, i32, P, u64, i32], i32),
         "cwf_hip_stepper_set_external_force": ([P, P, u64, i32], i32),
         "cwf_hip_stepper_set_warm_start": ([P, i32], i32),
+        "cwf_hip_stepper_set_load_pattern": ([P, P, P, u64], i32),
+        "cwf_hip_stepper_set_load_scale": ([P, C.c_double], i32),
         "cwf_hip_stepper_time": ([P, P, P], i32),
         "cwf_shard_build": ([P, P, P, i32, i32, P], i32),
         "cwf_shard_get": ([P, P, P], i32),
@@ -159,7 +161,7 @@ def load() -> C.CDLL:
         "cwf_hip_comm_create_local": ([i32, i32, P], i32),
         "cwf_hip_comm_destroy": ([P], None),
         "cwf_hip_system_attach": ([P, P, i32, P], i32),
-        "cwf_hip_solve_pcg_group": ([P, i32, P, P, P, i32, P], i32),
+        "cwf_hip_solve_pcg_group": ([P, i32, P, P, P, P, i32, P], i32),
         "cwf_preprocess_tets": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),
         "cwf_preprocess_hex8": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),
         "cwf_hip_derived_fields": ([P, P, u64, i32, P, P, i32], i32),

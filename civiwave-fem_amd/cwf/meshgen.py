@@ -158,8 +158,8 @@ CONFIGS = {
                tol=3e-4),
     "c3": dict(name="cube 149^3 hex (Kuhn tets), 10.1M DOF, Rayleigh", shape=(149, 149, 149), h=0.1, xi=0.05,
                w=(10.0, 100.0), tol=3e-4),
-    "c4": dict(name="jittered/permuted 118^3 hex (Kuhn tets), 5.06M DOF", shape=(118, 118, 118), h=0.1, xi=0.02,
-               w=(5.0, 50.0), tol=3e-4, jitter=True),
+    "c4": dict(name="jittered/permuted 118^3 hex (Kuhn tets), 5.06M DOF, harmonic tip load", shape=(118, 118, 118),
+               h=0.1, xi=0.02, w=(5.0, 50.0), tol=3e-4, jitter=True, harmonic=5.0),
     "c5": dict(name="slab 800x400x50 hex (Kuhn tets), 49.1M DOF", shape=(800, 400, 50), h=0.1, xi=0.02,
                w=(5.0, 50.0), tol=3e-4),
 }

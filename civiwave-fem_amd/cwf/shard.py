@@ -30,6 +30,54 @@ def slab_ranges(node_count: int, nranks: int, align: int = 1) -> np.ndarray:
     return np.asarray(b, np.uint64)
 
 
+def _morton_keys(c: np.ndarray) -> np.ndarray:
+    lo, hi = c.min(0), c.max(0)
+    q = np.floor((c - lo) / max(float((hi - lo).max()), 1e-300) * ((1 << 20) - 1)).astype(np.uint64)
+
+    def spread(v):
+        v = v & np.uint64(0x1FFFFF)
+        v = (v | v << np.uint64(32)) & np.uint64(0x1F00000000FFFF)
+        v = (v | v << np.uint64(16)) & np.uint64(0x1F0000FF0000FF)
+        v = (v | v << np.uint64(8)) & np.uint64(0x100F00F00F00F00F)
+        v = (v | v << np.uint64(4)) & np.uint64(0x10C30C30C30C30C3)
+        v = (v | v << np.uint64(2)) & np.uint64(0x1249249249249249)
+        return v
+
+    return spread(q[:, 0]) | spread(q[:, 1]) << np.uint64(1) | spread(q[:, 2]) << np.uint64(2)
+
+
+def rcb_node_ranges(coords: np.ndarray, nranks: int):
+    """Recursive coordinate bisection of the nodes into `nranks` parts of near-equal size (the
+    C4 mesh is randomly numbered, so contiguous ranges of its own ids would make every shard's halo most of the
+    mesh). A range of parts is split along its longest extent at the node count proportional to its two halves'
+    part counts (ties broken by node id, so every rank computes the same partition). Nodes are then numbered
+    part after part, along a Morton curve inside a part (the locality the shard's tiles gather with).
+    Returns (global id per input node u64 [N], rank_node_begin u64 [nranks + 1]) for cwf_shard_build."""
+    c = np.asarray(coords, np.float64).reshape(-1, 3)
+    N = c.shape[0]
+    part = np.empty(N, np.int64)
+    stack = [(np.arange(N, dtype=np.int64), 0, nranks)]
+    while stack:
+        idx, p0, n = stack.pop()
+        if n == 1 or idx.size == 0:
+            part[idx] = p0
+            continue
+        sub = c[idx]
+        axis = int(np.argmax(sub.max(0) - sub.min(0)))
+        nl = n // 2
+        cut = (idx.size * nl) // n
+        order = np.lexsort((idx, sub[:, axis]))  # by coordinate, then node id
+        stack.append((idx[order[:cut]], p0, nl))
+        stack.append((idx[order[cut:]], p0 + nl, n - nl))
+    key = _morton_keys(c)
+    order = np.lexsort((np.arange(N), key, part))  # part, then Morton, then id
+    gid = np.empty(N, np.uint64)
+    gid[order] = np.arange(N, dtype=np.uint64)
+    counts = np.bincount(part, minlength=nranks)
+    begin = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    return gid, begin
+
+
 @dataclass
 class Shard:
     rank: int
@@ -64,11 +112,13 @@ class Shard:
         v = np.asarray(global_vec).reshape(-1, 3)
         return np.ascontiguousarray(v[self.node_source.astype(np.int64)].reshape(-1))
 
-    def system(self, materials, stiffness_scale=1.0, mass_factor=0.0, device=0) -> MatrixFreeSystem:
+    def system(self, materials, stiffness_scale=1.0, mass_factor=0.0, device=0, mode=_lib.MODE_FAST) -> MatrixFreeSystem:
+        """The shard's local handle (its node order is the halo plan's). mode=MODE_PARITY gives the bit-exact
+        sharded solve; it needs slab_ranges(..., align=256) ranges (cwf_hip.h cwf_hip_system_attach)."""
         return MatrixFreeSystem(self.connectivity, self.gradients, self.volume, self.material_index, materials,
                                 self.lumped_mass, self.bc_mask, self.local_nodes, self.local_elements,
                                 3 * self.local_nodes, stiffness_scale, mass_factor, 256, None, None,
-                                _lib.MODE_FAST, device, self.node_coords, keep_node_order=True)
+                                mode, device, self.node_coords, keep_node_order=True)
 
     def close(self):
         if self._c is not None:
@@ -165,17 +215,19 @@ class Comm:
 
 
 def solve_pcg_group(systems: list, rhs: list, settings: PcgSettings, solutions: list,
-                    check_interval: int = 0) -> Expected:
-    """solve_pcg over every rank of a LOCAL communicator (systems in rank order)."""
+                    check_interval: int = 0, residuals: list | None = None) -> Expected:
+    """solve_pcg over every rank of a LOCAL communicator (systems in rank order); `residuals` (optional)
+    receives each rank's local r."""
     n = len(systems)
     hs = (C.c_void_p * n)(*[s.handle().value for s in systems])
     rp = (C.c_void_p * n)(*[_lib.ptr(r).value for r in rhs])
     xp = (C.c_void_p * n)(*[_lib.ptr(x).value for x in solutions])
+    resp = (C.c_void_p * n)(*[_lib.ptr(r).value for r in residuals]) if residuals is not None else None
     kind = _lib.PTR_HOST if isinstance(rhs[0], np.ndarray) else _lib.PTR_DEVICE
     s = _lib.PcgSettingsC(settings.max_iterations, settings.relative_tolerance, int(settings.warm_start),
                           check_interval)
     tel = _lib.PcgTelemetryC()
-    st = _lib.load().cwf_hip_solve_pcg_group(hs, n, rp, C.byref(s), xp, kind, C.byref(tel))
+    st = _lib.load().cwf_hip_solve_pcg_group(hs, n, rp, C.byref(s), xp, resp, kind, C.byref(tel))
     if st:
         msg, ctx = _lib.last_error(systems[0]._h)
         return Expected(error=PcgError(msg, ctx))

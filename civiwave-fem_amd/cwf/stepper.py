@@ -45,7 +45,7 @@ class StepTelemetry:
 class Stepper:
     """Stepper(packing, materials, rayleigh, solver_settings, time_settings, adaptive_policy)."""
 
-    DISPLACEMENT, VELOCITY, ACCELERATION, SOLUTION = 0, 1, 2, 3
+    DISPLACEMENT, VELOCITY, ACCELERATION, SOLUTION, EXTERNAL_FORCE = 0, 1, 2, 3, 4
 
     def __init__(self, packing, materials, rayleigh: RayleighCoefficients, solver_settings: SolverSettings,
                  time_settings: TimeSettings, adaptive_policy: AdaptivePolicy | None = None,
@@ -117,6 +117,21 @@ class Stepper:
         if isinstance(force, np.ndarray):
             force = np.ascontiguousarray(force, np.float32)
         rc = _lib.load().cwf_hip_stepper_set_external_force(self._st, _lib.ptr(force), self.dof_count, kind)
+        if rc:
+            raise RuntimeError(_lib.last_error(self.system._h))
+
+    def set_load_pattern(self, base: np.ndarray, pattern: np.ndarray):
+        """Device-side time-varying load (cwf_hip_stepper_set_load_pattern): f64 [3N] loads no curve scales and
+        the point-load values one curve scales; set_load_scale(c) then packs f32(base + c * pattern)."""
+        self._lbase = np.ascontiguousarray(base, np.float64)
+        self._lpat = np.ascontiguousarray(pattern, np.float64)
+        rc = _lib.load().cwf_hip_stepper_set_load_pattern(self._st, _lib.ptr(self._lbase), _lib.ptr(self._lpat),
+                                                          self.dof_count)
+        if rc:
+            raise RuntimeError(_lib.last_error(self.system._h))
+
+    def set_load_scale(self, scale: float):
+        rc = _lib.load().cwf_hip_stepper_set_load_scale(self._st, float(scale))
         if rc:
             raise RuntimeError(_lib.last_error(self.system._h))
 

@@ -231,11 +231,23 @@ int cwf_hip_stepper_create(cwf_hip_system *system, const cwf_stepper_desc *desc,
 void cwf_hip_stepper_destroy(cwf_hip_stepper *st);
 /* Stepper::step(simulation_time_seconds, paused_mode) */
 int cwf_hip_stepper_step(cwf_hip_stepper *st, double simulation_time, int paused, cwf_step_telemetry *tel);
-/* which: 0 = displacement, 1 = velocity, 2 = acceleration; out [3N] */
+/* which: 0 = displacement, 1 = velocity, 2 = acceleration, 3 = the last PCG solution x, 4 = external force
+ * (get only); out [3N] */
 int cwf_hip_stepper_get_state(cwf_hip_stepper *st, int which, float *out, uint64_t n, int ptr_kind);
 int cwf_hip_stepper_set_state(cwf_hip_stepper *st, int which, const float *in, uint64_t n, int ptr_kind);
 /* rewrite nodes.external_force between steps (viewer.cpp:262-266) */
 int cwf_hip_stepper_set_external_force(cwf_hip_stepper *st, const float *f, uint64_t n, int ptr_kind);
+/* Time-varying loads on the device (loads.cpp:87-174 evaluated for one curve-scaled pattern, cast as
+ * pack.cpp:41-57): set_load_pattern uploads base = the loads no curve scales (gravity, unscaled tractions and
+ * point loads) and pattern = the point-load values one curve scales, f64 [3N] host arrays in the caller's node
+ * order; each set_load_scale(c) then writes external_force = safe_cast(base + c * pattern) on the handle's
+ * stream, where c = evaluate_curve(curve, t) (loads.cpp:63-85). For point loads (at most one scaled group per
+ * node) that is bitwise the external_force assemble_load_vector at t packs (loads.cpp:163-172 adds
+ * scale * value[axis] after gravity); a scaled traction rounds as (area * scale / n) * value there and is not
+ * covered. This is the viewer's per-step rewrite of nodes.external_force (viewer.cpp:262-266) without the
+ * host round trip. */
+int cwf_hip_stepper_set_load_pattern(cwf_hip_stepper *st, const double *base, const double *pattern, uint64_t n);
+int cwf_hip_stepper_set_load_scale(cwf_hip_stepper *st, double scale);
 int cwf_hip_stepper_set_warm_start(cwf_hip_stepper *st, int enabled);
 int cwf_hip_stepper_time(const cwf_hip_stepper *st, double *current_time, double *time_step);
 
@@ -286,17 +298,23 @@ int cwf_hip_comm_create_rccl(int32_t nranks, int32_t rank, const uint8_t *id, in
 int cwf_hip_comm_create_local(int32_t nranks, int device, cwf_hip_comm **out);
 void cwf_hip_comm_destroy(cwf_hip_comm *comm); /* after every attached handle is destroyed */
 
-/* Make `h` (created from a shard's local desc) rank `rank` of `comm` with the shard's halo plan.
- * Afterwards solve_pcg / stepper_step are collective: scalars are all-gathered and folded in rank
- * order on every rank (identical control flow everywhere), ghost DOFs are refreshed by the halo
- * exchange, and vectors are local [3 * local_nodes] with only the owned rows meaningful on output
- * (x is halo-consistent). FAST mode only. */
+/* Make `h` (created from a shard's local desc with CWF_DESC_KEEP_NODE_ORDER) rank `rank` of `comm` with the
+ * shard's halo plan. Afterwards solve_pcg / stepper_step are collective: scalars are all-gathered and folded
+ * in rank order on every rank (identical control flow everywhere), ghost DOFs are refreshed by the halo
+ * exchange, and vectors are local [3 * local_nodes] with only the owned rows meaningful on output (x is
+ * halo-consistent). Both modes: FAST all-gathers one fp64 per rank per scalar (p.Ap; r.r and r.z with the z
+ * halo in one RCCL group). PARITY all-gathers every rank's 256-DOF chunk partials and folds them in global
+ * chunk order (pcg.cpp:170-207), so x, r and the residual history equal one handle's PARITY solve bit for
+ * bit; it requires owned ranges that are contiguous, ascending by rank from node 0, and (all but the last)
+ * whole reduction blocks: 3 * owned_nodes % reduction_block == 0 (cwf/shard.py slab_ranges(align=256)),
+ * else CWF_ERR_UNSUPPORTED at the first solve. */
 int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *comm, int32_t rank, const cwf_shard_info *plan);
 /* solve_pcg over all ranks of a LOCAL communicator (members in rank order); for RCCL call
- * cwf_hip_solve_pcg on each rank's handle. Telemetry is identical on every rank. */
+ * cwf_hip_solve_pcg on each rank's handle. Telemetry is identical on every rank. residual_out (nullable, or
+ * NULL entries) receives each member's local r (owned rows meaningful). */
 int cwf_hip_solve_pcg_group(cwf_hip_system *const *members, int32_t count, const float *const *rhs,
-                            const cwf_pcg_settings *settings, float *const *x_inout, int ptr_kind,
-                            cwf_pcg_telemetry *telemetry);
+                            const cwf_pcg_settings *settings, float *const *x_inout, float *const *residual_out,
+                            int ptr_kind, cwf_pcg_telemetry *telemetry);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side preprocessing (no GPU needed): tet gradients/volume/lumped mass/CSR exactly as

@@ -84,6 +84,22 @@ int main()
     EXPECT(g9(u[11]) == "-7.85199674e-08");  // from rest: u = u_pred + x = x
     auto s2 = stepper.step(stepper.current_time(), true);
     EXPECT(s2.has_value() && s2->paused_mode && s2->applied_tolerance == 1.0e-5);
+
+    // two-entry breadcrumbs come back as two entries (pcg.cpp:566-570, 609-613), so a caller rebuilds a
+    // PcgError equal to the reference's
+    const std::vector<uint32_t> bad_mat = {1};
+    pcg::MatrixFreeSystem sys_m{conn, grads, vol, bad_mat, mats, mass32, bc, 4, 1, 12, 1.0, 0.0, 256, 1};
+    pcg::MatrixFreeWorkspace ws_m;
+    auto em = pcg::apply_keff(sys_m, in, out, ws_m);
+    EXPECT(!em.has_value() && em.error().message == "element references material out of range");
+    EXPECT(!em.has_value() && em.error().context == std::vector<std::string>({"element=0", "material_index=1"}));
+    std::vector<uint32_t> bad_conn = conn;
+    bad_conn[2] = 9;
+    pcg::MatrixFreeSystem sys_n{bad_conn, grads, vol, mat, mats, mass32, bc, 4, 1, 12, 1.0, 0.0, 256, 1};
+    pcg::MatrixFreeWorkspace ws_n;
+    auto en = pcg::apply_keff(sys_n, in, out, ws_n);
+    EXPECT(!en.has_value() && en.error().message == "element connectivity references node out of range");
+    EXPECT(!en.has_value() && en.error().context == std::vector<std::string>({"element=0", "node=9"}));
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
     return failures ? 1 : 0;
 }

@@ -380,3 +380,29 @@ def test_cpp_mirror_single_tet_reference_outputs(tmp_path):
     exe = _build_cpp_test(tmp_path)
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_fast_short_solve_after_long_solves_matches_fresh_handle():
+    """The first PCG batch is sized from the handle's last two solves when they agree (abi.cpp run_pcg_group);
+    a short warm-started solve after two long ones must still stop at its own convergence: x, r, the
+    iteration count and the fp64 residual history equal a fresh handle's (which batches from 4), bit for bit,
+    including the lazy x flush of an iteration count that is not a multiple of 4."""
+    case = CASES["jitter"]()
+    rhs = case.static_rhs()
+    s = gpu_system(case, mode=_lib.MODE_FAST)
+    for _ in range(2):
+        x_long = np.zeros_like(rhs)
+        t_long = pcg.solve_pcg(s, rhs, pcg.PcgSettings(600, 1e-6), pcg.PcgVectors(x_long, np.zeros_like(rhs))).value()
+        assert t_long.converged and t_long.iterations > 60
+    rhs2 = (1.01 * rhs).astype(np.float32)
+    out = []
+    for h in (s, gpu_system(case, mode=_lib.MODE_FAST)):
+        x, r = x_long.copy(), np.zeros_like(rhs)
+        t = pcg.solve_pcg(h, rhs2, pcg.PcgSettings(600, 1e-3, True), pcg.PcgVectors(x, r)).value()
+        out.append((x, r, t, pcg.residual_history(h)))
+    (x1, r1, t1, h1), (x2, r2, t2, h2) = out
+    assert t1.converged and 0 < t1.iterations < t_long.iterations // 2
+    assert (t1.iterations, t1.residual_norm) == (t2.iterations, t2.residual_norm)
+    assert_bitwise(x1, x2, "x")
+    assert_bitwise(r1, r2, "r")
+    assert np.array_equal(h1, h2)

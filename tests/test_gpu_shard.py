@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from cwf import _lib, pcg, scenarios, shard
-from helpers import oracle_system
+from helpers import assert_bitwise, oracle_system
 
 pytestmark = pytest.mark.gpu
 
@@ -103,3 +103,92 @@ def test_rccl_single_rank_sharded_schedule():
     assert np.linalg.norm(xg.reshape(-1) - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
     s.close()
     comm.close()
+
+
+def _parity_sharded(glob, nranks, ranges=None, from_slabs=None, rel_tol=1e-6, max_iterations=800, warm=None):
+    """LOCAL PARITY solve over `nranks` shards -> (telemetry or error, global x, global r, members' histories)."""
+    sK, sM = glob.scalars()
+    P = glob.packing
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs, rs = [], [], [], [], []
+    for k in range(nranks):
+        if from_slabs:
+            case, node_global, begin = scenarios.slab_case_shape(from_slabs, nranks, k, tol=rel_tol)
+            src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_PARITY)
+            sh = shard.build_shard(src, begin, k, node_global)
+            rhs.append(sh.local_dofs(case.static_rhs()))
+        else:
+            src = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_PARITY)
+            sh = shard.build_shard(src, ranges, k)
+            rhs.append(sh.local_dofs(glob.static_rhs()))
+        s = sh.system(glob.materials, sK, sM, mode=_lib.MODE_PARITY)
+        comm.attach(s, sh)
+        systems.append(s)
+        shards.append(sh)
+        xs.append(sh.local_dofs(warm) if warm is not None else np.zeros(3 * sh.local_nodes, np.float32))
+        rs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    res = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(max_iterations, rel_tol, warm is not None), xs,
+                                residuals=rs)
+    x = np.zeros((P.node_count, 3), np.float32)
+    r = np.zeros((P.node_count, 3), np.float32)
+    for sh, xl, rl in zip(shards, xs, rs):
+        g = sh.node_global[: sh.owned_nodes].astype(np.int64)
+        x[g] = xl.reshape(-1, 3)[: sh.owned_nodes]
+        r[g] = rl.reshape(-1, 3)[: sh.owned_nodes]
+    hists = [pcg.residual_history(s) for s in systems] if res.has_value() else []
+    comm.close()
+    return res, x.reshape(-1), r.reshape(-1), hists
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_local_sharded_parity_solve_bitwise_equals_single_handle(nranks):
+    """SURVEY.md 8e parity gate: owned ranges aligned to 256 nodes, every rank's 256-DOF chunk partials
+    all-gathered and folded in global chunk order -> x, r, the telemetry and the fp64 residual history of
+    the sharded PARITY solve equal the single-handle PARITY solve (and the oracle) bit for bit."""
+    glob = scenarios.block_case(10, 6, 12, h=0.1, tol=1e-6)  # 1,001 nodes
+    sK, sM = glob.scalars()
+    P = glob.packing
+    ranges = shard.slab_ranges(P.node_count, nranks, align=256)
+    res, x, r, hists = _parity_sharded(glob, nranks, ranges=ranges)
+    tel = res.value()
+    single = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_PARITY)
+    rhs = glob.static_rhs()
+    x1, r1 = np.zeros_like(rhs), np.zeros_like(rhs)
+    t1 = pcg.solve_pcg(single, rhs, pcg.PcgSettings(800, 1e-6), pcg.PcgVectors(x1, r1)).value()
+    h1 = pcg.residual_history(single)
+    assert tel.converged and (tel.iterations, tel.residual_norm, tel.rhs_norm, tel.alpha_last, tel.beta_last) == (
+        t1.iterations, t1.residual_norm, t1.rhs_norm, t1.alpha_last, t1.beta_last)
+    assert_bitwise(x, x1, "sharded PARITY x")
+    assert_bitwise(r, r1, "sharded PARITY r")
+    for h in hists:
+        assert np.array_equal(h, h1)
+    ref = oracle_system(P, glob.materials, sK, sM).solve_pcg(rhs, 800, 1e-6, history=True)
+    assert_bitwise(x, ref["x"], "sharded PARITY x vs oracle")
+    assert np.array_equal(hists[0], ref["history"])
+
+
+def test_local_sharded_parity_from_slab_submeshes_warm_start():
+    """The bench's decomposition in PARITY mode: 15 x 15 cross-sections (256 nodes per plane, so every slab
+    boundary is chunk-aligned), each rank builds only its slab sub-mesh; a warm-started solve is bitwise the
+    single-handle one."""
+    nranks, shape = 3, (15, 15, 2)
+    glob = scenarios.block_case(15, 15, 2 * nranks, h=0.1, tol=1e-6)
+    sK, sM = glob.scalars()
+    P = glob.packing
+    warm = (np.arange(P.dof_count) % 5 * 1e-7).astype(np.float32)
+    res, x, r, hists = _parity_sharded(glob, nranks, from_slabs=shape, warm=warm)
+    tel = res.value()
+    ref = oracle_system(P, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 800, 1e-6, warm_start=True, x=warm,
+                                                             history=True)
+    assert tel.iterations == ref["telemetry"].iterations and tel.residual_norm == ref["telemetry"].residual_norm
+    assert_bitwise(x, ref["x"], "slab PARITY x")
+    assert_bitwise(r, ref["r"], "slab PARITY r")
+    assert np.array_equal(hists[1], ref["history"])
+
+
+def test_local_sharded_parity_rejects_unaligned_ranges():
+    glob = scenarios.block_case(10, 6, 12, h=0.1, tol=1e-6)
+    res, *_ = _parity_sharded(glob, 2, ranges=shard.slab_ranges(glob.packing.node_count, 2))  # cut at 500 nodes
+    assert not res.has_value()
+    assert res.error().message.startswith("sharded PARITY needs contiguous owned node ranges")
+    assert res.error().context == ["rank=0", "first_node=0", "owned_nodes=500"]

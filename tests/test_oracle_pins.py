@@ -199,3 +199,26 @@ def test_oracle_reproduces_committed_golden(name):
         a, b = stored[k], fresh[k]
         assert a.dtype == b.dtype and a.shape == b.shape, k
         assert a.tobytes() == b.tobytes(), f"{name}:{k} differs"
+
+
+def test_c4_harmonic_load_curve_and_vectors_match_oracle_loads():
+    """C4's harmonic tip load: F0 sin(2 pi 5 t) as a 64-point curve. The curve evaluation
+    (loads.cpp:63-85) and the packed external_force at t (loads.cpp:87-174, pack.cpp:41-57) equal the oracle's,
+    and base + curve(t) * pattern (the device rewrite, cwf_hip_stepper_set_load_scale) is the same f32 vector."""
+    cfg = scenarios.make_config(harmonic=meshgen.CONFIGS["c4"]["harmonic"])
+    curve = cfg.curves["harmonic"]
+    assert len(curve.points) == scenarios.HARMONIC_POINTS == 64
+    assert cfg.loads.points[0].scale_curve == "harmonic" and cfg.loads.points[0].value == (0.0, 0.0, -500.0)
+    for t in (0.0, 0.013, 0.05, 0.1, 0.137, 0.2):
+        assert physics.evaluate_curve(curve, t) == O.evaluate_curve(curve.points, t)
+        assert abs(O.evaluate_curve(curve.points, t) - np.sin(2 * np.pi * 5.0 * t)) <= 2e-3  # 63 intervals/period
+    case = scenarios.block_case(7, 6, 5, h=0.1, jitter=True, harmonic=5.0)
+    P = case.packing
+    tip = case.mesh.node_groups[case.mesh.group_names["TIP"]]
+    base, pattern = case.load_pattern()
+    for t in (0.0, 0.01, 0.03, 0.27):
+        scale = O.evaluate_curve(curve.points, t % 0.2)
+        ref = O.assemble_loads(P.lumped_mass64, (0.0, 0.0, -9.81), [(tip, (0.0, 0.0, -500.0), scale)])
+        got = case.external_force_at(t)
+        assert got.tobytes() == ref.astype(np.float32).tobytes()
+        assert (base + case.load_scale(t) * pattern).astype(np.float32).tobytes() == got.tobytes()

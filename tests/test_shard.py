@@ -107,3 +107,59 @@ def test_shard_errors():
         shard.build_shard(sysm, np.array([0, 10], np.uint64), 0)
     with pytest.raises(RuntimeError, match="rank out of range"):
         shard.build_shard(sysm, shard.slab_ranges(case.packing.node_count, 2), 2)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_strong_slab_submeshes_match_global(nranks):
+    """bench.py --scaling strong: the config's block itself split into `nranks` slabs; every rank's slab
+    sub-mesh gives the shard cut from the global mesh, and the owned ranges cover it once."""
+    shape = (4, 3, 7)
+    glob = scenarios.block_case(*shape, h=0.1)
+    gsys = _system(glob)
+    owned = []
+    for r in range(nranks):
+        sub, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, stack=False)
+        assert int(begin[-1]) == glob.packing.node_count
+        a = shard.build_shard(gsys, begin, r)
+        b = shard.build_shard(_system(sub), begin, r, node_global)
+        assert np.array_equal(a.node_global, b.node_global) and np.array_equal(a.connectivity, b.connectivity)
+        assert np.array_equal(a.send_nodes, b.send_nodes)
+        owned.append(a.node_global[: a.owned_nodes])
+    assert np.array_equal(np.sort(np.concatenate(owned)), np.arange(glob.packing.node_count))
+
+
+@pytest.mark.parametrize("nranks", [3, 8])
+def test_rcb_partition_of_permuted_mesh(nranks):
+    """C4's decomposition (scenarios.rcb_case): an RCB node partition of the jittered + permuted mesh,
+    renumbered part after part. Parts are balanced, every node is owned once, the halo plans are symmetric,
+    owned K_eff rows are bitwise the global rows, and halos stay small (a contiguous range of the random
+    numbering would make nearly every node a ghost)."""
+    case = scenarios.block_case(12, 10, 9, h=0.1, jitter=True)
+    P = case.packing
+    sK, sM = case.scalars()
+    gid, begin = shard.rcb_node_ranges(case.mesh.coords, nranks)
+    assert np.array_equal(np.sort(gid), np.arange(P.node_count, dtype=np.uint64))
+    sizes = np.diff(begin.astype(np.int64))
+    assert sizes.max() - sizes.min() <= 1
+    sysm = _system(case)
+    shards = [shard.build_shard(sysm, begin, r, gid) for r in range(nranks)]
+    ref = O.System(O.Packed(P.node_count, P.element_count, P.connectivity, P.gradients, P.volume, P.material_index,
+                            P.lumped_mass64, P.lumped_mass, P.offsets, P.element_indices, P.local_indices),
+                   np.concatenate([np.asarray(m.stiffness, np.float64).reshape(-1) for m in case.materials]),
+                   P.bc_mask, sK, sM, 256)
+    x = ((np.arange(P.dof_count, dtype=np.uint64) * 2654435761) % 1000).astype(np.float32) / np.float32(1000.0)
+    y = ref.apply_keff(x).reshape(-1, 3)
+    ghosts = 0
+    for s in shards:
+        src = s.node_source[: s.owned_nodes].astype(np.int64)
+        assert np.array_equal(gid[src], np.arange(int(begin[s.rank]), int(begin[s.rank + 1]), dtype=np.uint64))
+        yl = _local_oracle(s, case, sK, sM).apply_keff(s.local_dofs(x))
+        assert_bitwise(yl[: 3 * s.owned_nodes], y[src].reshape(-1), f"rank {s.rank} owned rows")
+        ghosts += s.local_nodes - s.owned_nodes
+        for k, q in enumerate(s.neighbor_ranks):
+            t = shards[q]
+            j = list(t.neighbor_ranks).index(s.rank)
+            sent = s.node_global[s.send_nodes[int(s.send_offsets[k]):int(s.send_offsets[k + 1])].astype(np.int64)]
+            recv = t.node_global[t.owned_nodes + int(t.recv_offsets[j]): t.owned_nodes + int(t.recv_offsets[j + 1])]
+            assert np.array_equal(sent, recv)
+    assert ghosts < 0.8 * P.node_count

@@ -37,3 +37,25 @@ def test_gloo_sharded_pcg_matches_oracle(tmp_path, world):
     assert abs(its.pop() - int(ref["telemetry"].iterations)) <= 3
     err = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
     assert err < 1e-4, err
+
+
+def test_gloo_sharded_parity_schedule_is_bitwise_the_single_solve(tmp_path):
+    """The PARITY gate of SURVEY.md 8e on two processes: chunk partials of 256-node-aligned owned ranges,
+    all-gathered and folded in global chunk order, give x, r and the fp64 residual history of the one-process
+    oracle solve bit for bit (dist_worker.run_rank_parity restates csrc/comm.cpp sharded_parity_*)."""
+    world, shape = 2, (15, 15, 2)
+    mp.spawn(dist_worker.run_rank_parity, args=(world, _port(), str(tmp_path), shape), nprocs=world, join=True)
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * world, h=0.1)
+    sK, sM = glob.scalars()
+    ref = oracle_system(glob.packing, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 400, 1e-6, history=True)
+    x = np.zeros_like(ref["x"]).reshape(-1, 3)
+    r = np.zeros_like(x)
+    for k in range(world):
+        d = np.load(tmp_path / f"parity_rank{k}.npz")
+        g = d["gid"].astype(np.int64)
+        x[g] = d["x"].reshape(-1, 3)
+        r[g] = d["r"].reshape(-1, 3)
+        assert int(d["iterations"]) == int(ref["telemetry"].iterations)
+        assert np.array_equal(d["hist"], ref["history"])
+    assert x.reshape(-1).tobytes() == ref["x"].tobytes()
+    assert r.reshape(-1).tobytes() == ref["r"].tobytes()
