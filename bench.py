@@ -217,14 +217,17 @@ def main():
         if case.load_curve is not None:
             load_pattern = case.load_pattern()
     else:
-        if mode != _lib.MODE_FAST or args.element != "tet4":
-            raise SystemExit("the multi-GPU bench runs the FAST tet4 path (the bit-exact sharded PARITY solve is "
+        if mode != _lib.MODE_FAST:
+            raise SystemExit("the multi-GPU bench runs the FAST path (the bit-exact sharded PARITY solve is "
                              "the parity gate in tests/test_gpu_shard.py)")
         if unstructured:  # C4: the whole mesh, RCB node partition, renumbered part after part
+            if args.element != "tet4":
+                raise SystemExit("the unstructured configs are tet4 meshes")
             case, node_global, begin = scenarios.rcb_case(args.config, world, max_iterations=args.max_iterations)
         else:
             case, node_global, begin = scenarios.slab_case(args.config, world, rank,
-                                                           max_iterations=args.max_iterations, strong=strong)
+                                                           max_iterations=args.max_iterations, strong=strong,
+                                                           element=args.element)
         P = case.packing
         sK, sM = case.scalars()
         src = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=mode)  # host arrays only

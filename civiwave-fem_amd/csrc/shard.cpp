@@ -1,4 +1,4 @@
-// shard.cpp -- host-side node-range partition of a tet mesh into rank-local shards (SURVEY.md
+// shard.cpp -- host-side node-range partition of a tet4 or hex8 mesh into rank-local shards (SURVEY.md
 // section 8e; no reference counterpart: the reference runs on one device, and its
 // src/gpu/sharding.cpp:38-144 only splits packed buffers under Vulkan's 2 GiB buffer cap).
 //
@@ -45,9 +45,8 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
     if (!d || !rank_node_begin || !out)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
     *out = nullptr;
-    if (d->element_count && d->element_connectivity && d->element_connectivity[4] != 0xFFFFFFFFu)
-        return set_error(nullptr, CWF_ERR_UNSUPPORTED, "sharding supports tet4 systems only",
-                         "hex8 (SURVEY 8f4) runs on one handle");
+    // tet4 (slots 4..7 = UINT32_MAX) or native hex8 (all 8 slots)
+    const int corners = d->element_count && d->element_connectivity && d->element_connectivity[4] != 0xFFFFFFFFu ? 8 : 4;
     if (nranks < 1 || rank < 0 || rank >= nranks)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "rank out of range",
                          "nranks=" + std::to_string(nranks) + "\nrank=" + std::to_string(rank));
@@ -84,8 +83,14 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
         for (uint64_t e = 0; e < E; ++e)
         {
             const uint32_t *c = d->element_connectivity + 8 * e;
+            if ((c[4] != 0xFFFFFFFFu) != (corners == 8))
+            {
+                delete s;
+                return set_error(nullptr, CWF_ERR_UNSUPPORTED, "mixed tet4/hex8 meshes are not supported",
+                                 "element=" + std::to_string(e));
+            }
             bool mine = false;
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < corners; ++a)
             {
                 if (c[a] >= N)
                 {
@@ -98,7 +103,7 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
             if (!mine)
                 continue;
             s->element_source.push_back(e);
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < corners; ++a)
                 used[c[a]] = 1;
         }
         // local numbering: owned (ascending global), ghosts by (owner, global)
@@ -154,11 +159,11 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
             {
                 const uint32_t *c = d->element_connectivity + 8 * e;
                 bool has_q = false;
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < corners; ++a)
                     has_q |= owner[c[a]] == q;
                 if (!has_q)
                     continue;
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < corners; ++a)
                 {
                     const uint32_t l = local[c[a]];
                     if (l < s->owned && stamp[l] != (uint32_t)k)
@@ -185,7 +190,7 @@ int cwf_shard_build(const cwf_system_desc *d, const uint64_t *node_global_ids, c
         for (uint64_t j = 0; j < EL; ++j)
         {
             const uint64_t e = s->element_source[j];
-            for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < corners; ++a)
                 s->conn8[8 * j + a] = local[d->element_connectivity[8 * e + a]];
             std::memcpy(&s->grads[24 * j], d->element_gradients + 24 * e, 24 * sizeof(float));
             s->vol[j] = d->element_volume[e];

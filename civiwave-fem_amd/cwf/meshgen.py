@@ -81,12 +81,12 @@ def hex_block(nx: int, ny: int, nz: int, h: float = 1.0) -> TetMesh:
                                    "CORNER": np.array([(nz * B + ny) * A + nx], np.uint32)}, (nx, ny, nz))
 
 
-def kuhn_slab(nx: int, ny: int, nz: int, kc0: int, kc1: int, h: float = 1.0):
-    """Cells k in [kc0, kc1) of the nx*ny*nz Kuhn block (nodes on planes kc0..kc1), numbered
-    compactly but in the global order -> (TetMesh, global node id per sub-mesh node). Elements keep
-    the global (k-slowest) order, so a rank's sub-mesh feeds cwf_shard_build directly."""
+def kuhn_slab(nx: int, ny: int, nz: int, kc0: int, kc1: int, h: float = 1.0, element: str = "tet4"):
+    """Cells k in [kc0, kc1) of the nx*ny*nz Kuhn block (element="hex8": the native hex block), nodes on
+    planes kc0..kc1, numbered compactly but in the global order -> (TetMesh, global node id per sub-mesh
+    node). Elements keep the global (k-slowest) order, so a rank's sub-mesh feeds cwf_shard_build directly."""
     A, B = nx + 1, ny + 1
-    sub = kuhn_block(nx, ny, kc1 - kc0, h)
+    sub = (hex_block if element == "hex8" else kuhn_block)(nx, ny, kc1 - kc0, h)
     kk = np.arange(kc0, kc1 + 1, dtype=np.float64).repeat(A * B)
     sub.coords[:, 2] = kk if h == 1.0 else h * kk  # the same expression kuhn_block uses
     node_global = np.arange(sub.node_count, dtype=np.uint64) + np.uint64(kc0 * A * B)

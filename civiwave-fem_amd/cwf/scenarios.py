@@ -130,7 +130,7 @@ def config_case(key: str, max_iterations: int = 2000, element: str = "tet4") -> 
 
 
 def slab_case_shape(shape, nranks: int, rank: int, h: float = 0.1, max_iterations: int = 2000, stack: bool = True,
-                    **cfg_kw):
+                    element: str = "tet4", **cfg_kw):
     """Slab decomposition of an nx*ny*nz block. stack=True (weak scaling): the global block stacks `nranks`
     copies along z (nz * nranks cells); stack=False (strong scaling): the global block is the nx*ny*nz block
     itself. Rank r owns a contiguous range of node planes and gets the sub-mesh of every cell touching them
@@ -141,23 +141,26 @@ def slab_case_shape(shape, nranks: int, rank: int, h: float = 0.1, max_iteration
     A, B = nx + 1, ny + 1
     planes = [(nz + 1) * r // nranks for r in range(nranks + 1)]
     kc0, kc1 = max(planes[rank] - 1, 0), min(planes[rank + 1], nz)
-    tm, node_global = meshgen.kuhn_slab(nx, ny, nz, kc0, kc1, h)
+    tm, node_global = meshgen.kuhn_slab(nx, ny, nz, kc0, kc1, h, element)
     mesh = pack.from_tetmesh(tm)
     cfg = make_config(max_iterations=max_iterations, **cfg_kw)
-    case = Case(f"kuhn{nx}x{ny}x{nz}/slab{rank}of{nranks}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
+    tag = "hex" if element == "hex8" else "kuhn"
+    case = Case(f"{tag}{nx}x{ny}x{nz}/slab{rank}of{nranks}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
     begin = np.asarray([p * A * B for p in planes], np.uint64)
     return case, node_global, begin
 
 
-def slab_case(key: str, nranks: int, rank: int, max_iterations: int = 2000, strong: bool = False):
+def slab_case(key: str, nranks: int, rank: int, max_iterations: int = 2000, strong: bool = False,
+              element: str = "tet4"):
     """slab_case_shape for BASELINE config `key`: weak scaling (`key`'s block per rank) or strong scaling
     (`key`'s block split into `nranks` slabs, e.g. C3's fixed 10.1M DOF on 1/2/4/8 GPUs)."""
     c = meshgen.CONFIGS[key]
     case, node_global, begin = slab_case_shape(c["shape"], nranks, rank, h=c["h"], max_iterations=max_iterations,
-                                               stack=not strong, xi=c["xi"], w=c["w"], tol=c["tol"],
-                                               harmonic=c.get("harmonic"))
-    case.name = f"{key}: {c['name']}, " + (f"slab {rank} of {nranks} (strong)" if strong
-                                           else f"x{nranks} stacked, slab {rank} (weak)")
+                                               stack=not strong, element=element, xi=c["xi"], w=c["w"],
+                                               tol=c["tol"], harmonic=c.get("harmonic"))
+    name = c["name"].replace("(Kuhn tets)", "(native hex8)") if element == "hex8" else c["name"]
+    case.name = f"{key}: {name}, " + (f"slab {rank} of {nranks} (strong)" if strong
+                                      else f"x{nranks} stacked, slab {rank} (weak)")
     return case, node_global, begin
 
 

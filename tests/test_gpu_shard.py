@@ -4,6 +4,7 @@ z halo) and the ghost-row handling are the ones RCCL ranks run; only the transpo
 Tolerance: the sharded solve must converge to the single-process oracle solution within 1e-4
 relative (the solve guarantees |r| <= 1e-6 |rhs|) in the same iteration count +-10%."""
 import numpy as np
+import oracle as O
 import pytest
 
 from cwf import _lib, pcg, scenarios, shard
@@ -125,7 +126,10 @@ def _parity_sharded(glob, nranks, ranges=None, from_slabs=None, rel_tol=1e-6, ma
         comm.attach(s, sh)
         systems.append(s)
         shards.append(sh)
-        xs.append(sh.local_dofs(warm) if warm is not None else np.zeros(3 * sh.local_nodes, np.float32))
+        if warm is None:
+            xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+        else:  # by global node id (a slab sub-mesh numbers its nodes locally)
+            xs.append(np.ascontiguousarray(warm.reshape(-1, 3)[sh.node_global.astype(np.int64)].reshape(-1)))
         rs.append(np.zeros(3 * sh.local_nodes, np.float32))
     res = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(max_iterations, rel_tol, warm is not None), xs,
                                 residuals=rs)
@@ -192,3 +196,41 @@ def test_local_sharded_parity_rejects_unaligned_ranges():
     assert not res.has_value()
     assert res.error().message.startswith("sharded PARITY needs contiguous owned node ranges")
     assert res.error().context == ["rank=0", "first_node=0", "owned_nodes=500"]
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_local_sharded_hex8_solve(nranks):
+    """Native hex8 shards (north_star: 'the 8-GPU target on a hex mesh'): every rank builds its hex slab
+    sub-mesh; the sharded FAST solve converges to the fp64 hex8 solution (oracle hex8_solve64) within 1e-4
+    relative, in the single handle's iteration count +-10%."""
+    shape = (8, 5, 3)
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, element="hex8", tol=1e-6)
+    sK, sM = glob.scalars()
+    P = glob.packing
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs = [], [], [], []
+    for k in range(nranks):
+        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, k, tol=1e-6, element="hex8")
+        src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
+        sh = shard.build_shard(src, begin, k, node_global)
+        s = sh.system(glob.materials, sK, sM)
+        comm.attach(s, sh)
+        systems.append(s)
+        shards.append(sh)
+        rhs.append(sh.local_dofs(case.static_rhs()))
+        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    tel = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(3000, 1e-6), xs).value()
+    x = np.zeros((P.node_count, 3), np.float32)
+    for sh, xl in zip(shards, xs):
+        x[sh.node_global[: sh.owned_nodes].astype(np.int64)] = xl.reshape(-1, 3)[: sh.owned_nodes]
+    comm.close()
+    D = np.concatenate([np.asarray(m.stiffness, np.float64).reshape(-1) for m in glob.materials])
+    ref = O.hex8_solve64(glob.mesh.coords, glob.mesh.tets, P.material_index, D, sK, sM, P.lumped_mass, P.bc_mask,
+                         glob.static_rhs())
+    single = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_FAST)
+    rhs1 = glob.static_rhs()
+    x1 = np.zeros_like(rhs1)
+    t1 = pcg.solve_pcg(single, rhs1, pcg.PcgSettings(3000, 1e-6), pcg.PcgVectors(x1, np.zeros_like(rhs1))).value()
+    assert tel.converged and t1.converged
+    assert np.linalg.norm(x.reshape(-1) - ref) <= 1e-4 * np.linalg.norm(ref)
+    assert abs(tel.iterations - t1.iterations) <= max(3, t1.iterations // 10)

@@ -163,3 +163,31 @@ def test_rcb_partition_of_permuted_mesh(nranks):
             recv = t.node_global[t.owned_nodes + int(t.recv_offsets[j]): t.owned_nodes + int(t.recv_offsets[j + 1])]
             assert np.array_equal(sent, recv)
     assert ghosts < 0.8 * P.node_count
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_hex8_shards_rows_and_submeshes(nranks):
+    """Native hex8 shards: 8-corner elements touching the owned nodes, owned rows of the fp64
+    hex8 operator (oracle/hex8_oracle.c, ascending element scatter) bitwise the global rows, and every rank's
+    hex slab sub-mesh gives the shard cut from the global mesh."""
+    shape = (4, 3, 2 * nranks)
+    glob = scenarios.block_case(*shape, h=0.1, element="hex8")
+    P = glob.packing
+    sK, sM = glob.scalars()
+    D = np.concatenate([np.asarray(m.stiffness, np.float64).reshape(-1) for m in glob.materials])
+    x = ((np.arange(P.dof_count, dtype=np.uint64) * 2654435761) % 1000).astype(np.float32) / np.float32(1000.0)
+    y = O.hex8_apply(glob.mesh.coords, glob.mesh.tets, P.material_index, D, sK, sM, P.lumped_mass, P.bc_mask,
+                     x).reshape(-1, 3)
+    gsys = _system(glob)
+    for r in range(nranks):
+        sub, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, stack=False, element="hex8")
+        a = shard.build_shard(gsys, begin, r)
+        b = shard.build_shard(_system(sub), begin, r, node_global)
+        assert np.array_equal(a.node_global, b.node_global) and np.array_equal(a.connectivity, b.connectivity)
+        assert np.array_equal(a.send_nodes, b.send_nodes)
+        lc = a.connectivity.reshape(-1, 8)
+        assert np.all(lc != 0xFFFFFFFF)
+        yl = O.hex8_apply(a.node_coords.reshape(-1, 3), lc, a.material_index, D, sK, sM, a.lumped_mass, a.bc_mask,
+                          a.local_dofs(x))
+        own = a.node_global[: a.owned_nodes].astype(np.int64)
+        assert_bitwise(yl[: 3 * a.owned_nodes], y[own].reshape(-1), f"hex rank {r} owned rows")
