@@ -44,7 +44,7 @@ int hip_fail(cwf_hip_system *h, hipError_t e, const char *what)
 // CWF_HEX_NT=128|256 overrides
 uint32_t hex_tile_lanes(uint64_t hexes)
 {
-    const char *e = getenv("CWF_HEX_NT");
+    const char *e = knob("CWF_HEX_NT");
     if (e)
         return atoi(e) == 256 ? 256u : 128u;
     return hexes >= 1000000ull ? 256u : 128u;
@@ -217,7 +217,7 @@ std::vector<uint32_t> morton_node_order(const double *X, uint64_t N)
 // CWF_GROUPS=0 (diagnostic): the per-tet tiles instead of the fan groups
 bool groups_enabled()
 {
-    const char *gv = getenv("CWF_GROUPS");
+    const char *gv = knob("CWF_GROUPS");
     return !(gv && gv[0] == '0');
 }
 
@@ -229,7 +229,7 @@ bool groups_enabled()
 uint32_t group_lanes(uint64_t E)
 {
     (void)E;
-    const char *gn = getenv("CWF_GROUP_NT");
+    const char *gn = knob("CWF_GROUP_NT");
     return gn && atoi(gn) == 128 ? 128u : 256u;
 }
 
@@ -515,7 +515,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     std::vector<uint32_t> r_perm, r_conn, r_mask;
     std::vector<float> r_mass;
     std::vector<double> r_coords;
-    const char *rn = getenv("CWF_RENUMBER");
+    const char *rn = knob("CWF_RENUMBER");
     const bool renumber = d->mode == CWF_MODE_FAST && E && N && d->node_coords &&
                           !(d->reserved & CWF_DESC_KEEP_NODE_ORDER) && !(rn && rn[0] == '0');
     if (renumber)
@@ -548,7 +548,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             // contiguous id range (whole-line owner p / partial stores, coalesced owned gathers). The groups
             // and tiles are built from coordinates and tet order only, so the rebuild after this renumbering
             // gives the same partition.
-            const char *ot = getenv("CWF_OWNER_ORDER");
+            const char *ot = knob("CWF_OWNER_ORDER");
             if (!(ot && ot[0] == '0') && (hex || (d->material_count <= 16 && groups_enabled())))
             {
                 cwf_system_desc md = *d;
@@ -751,19 +751,19 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         DevTiles &t = s.t;
         // GEO: stream 8-B corner ids + tile-node coordinates and recompute gradients/volume on the fly,
         // when the desc carries coordinates that reproduce its gradients (CWF_GEO=0 forces the records)
-        const char *ge = getenv("CWF_GEO");
+        const char *ge = knob("CWF_GEO");
         t.geo = hex || ((!ge || ge[0] != '0') && d->node_coords && N && geometry_matches(d)) ? 1 : 0;
         if (hex)  // k_keff_hex_tiles: hex_nt lanes, one hex and two tile nodes per lane, push fold
         {
             t.hex = 1;
             t.hex_nt = (int)hex_tile_lanes(E);
-            const char *wt = getenv("CWF_TILES_WT");  // 0|1: write-through hex partials (diagnostic)
+            const char *wt = knob("CWF_TILES_WT");  // 0|1: write-through hex partials (diagnostic)
             t.wt_part = wt && wt[0] == '1';
             t.push = 1;
         }
         else
         {
-            const char *pp = getenv("CWF_TILE_PIPE");  // diagnostic: 0 = the one-tile-per-workgroup kernel
+            const char *pp = knob("CWF_TILE_PIPE");  // diagnostic: 0 = the one-tile-per-workgroup kernel
             t.pipe = t.geo && !(pp && pp[0] == '0') ? 1 : 0;
         }
         // fan groups (groups.cpp, k_keff_groups_pipe): the default FAST tet path when the mesh groups into
@@ -784,7 +784,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 {
                     return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
                 }
-                if (getenv("CWF_VERBOSE"))
+                if (knob("CWF_VERBOSE"))
                     fprintf(stderr, "[cwf] fan groups: status %d, %u groups (%.2f tets each), %u tiles, %zu tile nodes "
                                     "(%.3f per node), max %u nodes / %u slots per tile\n",
                             gst, gt.ngroups, gt.tets_per_group, gt.ntiles, gt.tile_nodes.size(),
@@ -834,7 +834,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     t.pipe = 1;
                     t.pipe_nt = (int)gnt;
                     {
-                        const char *wt = getenv("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
+                        const char *wt = knob("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
                         t.wt_part = wt ? (wt[0] == '1') : (E < 4000000ull);
                     }
                     t.ntiles = gt.ntiles;
@@ -855,7 +855,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             // automatically for meshes whose 512-element tiles would give each resident workgroup < 8 tiles)
             if (t.pipe)
             {
-                const char *pn = getenv("CWF_PIPE_NT");
+                const char *pn = knob("CWF_PIPE_NT");
                 t.pipe_nt = pn ? (atoi(pn) == 128 ? 128 : 256) : (E < 4000000ull ? 128 : 256);
                 t.push = 1;  // the pipelined kernel folds pushed forces (epos), not local-CSR entries
             }
@@ -869,7 +869,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         {
             return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
         }
-        if (getenv("CWF_VERBOSE"))
+        if (knob("CWF_VERBOSE"))
             fprintf(stderr, "[cwf] tiles: %u tiles, %zu tile nodes (%.3f per node), max %u nodes/tile, %s records\n",
                     ht.ntiles, ht.tile_nodes.size(), N ? (double)ht.tile_nodes.size() / (double)N : 0.0,
                     ht.max_tile_nodes, t.geo ? "8-B geometric" : "48-B gradient");
@@ -1142,7 +1142,7 @@ int cwf_hip_keff_timed(cwf_hip_system *h, const float *x, float *y, int reps, do
     hipEvent_t a, b;
     HIPTRY(h, hipEventCreate(&a));
     HIPTRY(h, hipEventCreate(&b));
-    const char *dry = getenv("CWF_TIMED_PCG");  // diagnostic: time the PCG-mode tiles kernel instead
+    const char *dry = knob("CWF_TIMED_PCG");  // diagnostic: time the PCG-mode tiles kernel instead
     if (dry && h->mode == CWF_MODE_FAST && h->ds.iso)
     {
         Ctl c{};
@@ -1254,8 +1254,8 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     if (!h)
         return nullptr;
     const DevTiles &t = h->ds.t;
-    if (h->mode != CWF_MODE_FAST || !t.ntiles)
-        return "k_keff_parity";
+    if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize)
+        return h->ds.iso ? "k_keff_parity<true, false>" : "k_keff_parity<false, false>";
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
     {
         static thread_local char name[96];

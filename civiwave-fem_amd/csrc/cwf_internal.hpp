@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/cwf_hip.h"
+#include "knobs.hpp"
 
 namespace cwf
 {

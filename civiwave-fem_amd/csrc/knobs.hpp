@@ -1,0 +1,45 @@
+// knobs.hpp -- every environment switch libcwf_hip.so reads, in one place. None is needed for a solve: the
+// defaults are the measured-best configuration (DESIGN.md sections 3 and 6); each switch exists for a test or a
+// same-box A/B (tools/ab_env.sh). knob() refuses (returns NULL for) a name that is not listed here.
+#pragma once
+
+#include <cstdlib>
+#include <cstring>
+
+namespace cwf
+{
+struct Knob
+{
+    const char *name;
+    const char *doc;
+};
+
+inline constexpr Knob kKnobs[] = {
+    // node order and tiling of a FAST handle (abi.cpp, groups.cpp, tiles.cpp)
+    {"CWF_RENUMBER", "0: keep the caller's node order (no Morton / owner-tile renumbering)"},
+    {"CWF_OWNER_ORDER", "0: Morton renumbering only, not (owner tile, Morton)"},
+    {"CWF_GEO", "0: the 48-B gradient records instead of recomputing geometry from tile-node coordinates"},
+    {"CWF_GROUPS", "0: per-tet tiles (k_keff_tiles_pipe) instead of the fan groups"},
+    {"CWF_GROUP_NT", "128: 128-lane fan-group tiles (default 256; tests/test_gpu_parity.py)"},
+    {"CWF_GROUP_RCB", "\"tdiv,wdiv\": RCB leaf target and layer-gap window of the fan-group tiling"},
+    {"CWF_GROUP_LANES", "0: keep the RCB order of a tile's groups (no bank-aware lane order)"},
+    {"CWF_TILE_ORDER", "morton|rcb: per-tet / hex8 tile order"},
+    {"CWF_TILE_PIPE", "0: the one-tile-per-workgroup per-tet kernel (k_keff_tiles)"},
+    {"CWF_PIPE_NT", "128|256: lanes of the per-tet pipelined tiles"},
+    {"CWF_HEX_NT", "128|256: lanes of the hex8 tiles (tests/test_hex8.py)"},
+    {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
+    // PCG schedule (spmv_tiles.hip)
+    {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
+    // diagnostics
+    {"CWF_TIMED_PCG", "bits: cwf_hip_keff_timed times the PCG-mode tiles kernel dry (tools/ablate.py)"},
+    {"CWF_VERBOSE", "1: print the tiling statistics at create"},
+};
+
+inline const char *knob(const char *name)
+{
+    for (const Knob &k : kKnobs)
+        if (std::strcmp(k.name, name) == 0)
+            return std::getenv(name);
+    return nullptr;
+}
+}  // namespace cwf

@@ -38,17 +38,6 @@ constexpr int kMaxM = 16;
 #endif
 constexpr int kUpdThreads = CWF_UPD_THREADS;  // update-pass workgroup size (its per-workgroup shares are refolded by every consumer workgroup)
 constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
-// CWF_UPD_U=1|2 (diagnostic): owned nodes per update-pass thread and loop trip (default 1: 2 measured 4-5%
-// slower on C2 and C3, its registers cost more occupancy than the extra loads in flight gain)
-static int upd_unroll()
-{
-    static const int v = [] {
-        const char *e = getenv("CWF_UPD_U");
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
-    return v;
-}
-
 __device__ __forceinline__ double wave_sum(double v)
 {
 #pragma unroll
@@ -359,9 +348,17 @@ struct PcgArgs
     unsigned stride;
     unsigned it;
     double *hist;
-    unsigned abl;  // diagnostic ablation bits (CWF_ABLATE), 0 in normal runs
+    unsigned abl;  // diagnostic ablation bits (ablate(); the dry-run bit 32), 0 in solves
     float *pnew;   // out (PCG): the owner slot of every tile node stores the new p = z + beta p_old here
 };
+
+// Ablation bits (tools/ablate.py): phases of the tiles kernels skipped for diagnostic timing. They are compiled
+// in only by the ablation build (make ABLATION=1, -DCWF_ABLATION=1); release kernels test a constant 0. Bit 32
+// (a side-effect-free residual step, the dry timing of cwf_hip_keff_timed) is not a phase and stays live.
+#ifndef CWF_ABLATION
+#define CWF_ABLATION 0
+#endif
+__device__ __forceinline__ bool ablate(const PcgArgs &pa, unsigned bit) { return CWF_ABLATION && (pa.abl & bit); }
 
 // Pipelined-kernel element body (GEO). With edge columns c_k = x_k - x_0 and r_k their cofactor rows
 // (r_1 = c_2 x c_3, ...), the gradients are g_a = r_a / det and V = |det| / 6, so
@@ -542,7 +539,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     if constexpr (MODE == 1)
     {
         // pcg.cpp:862-895 of the previous update; its fold latency overlaps the loads above
-        if (pa.abl & 1u)
+        if (ablate(pa, 1u))
             beta = (float)pa.ctl->beta;
         else if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta,
                                     pa.abl & 32u))
@@ -572,7 +569,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     }
     __syncthreads();
     // (b) elements
-    if (!(pa.abl & 16u))
+    if (!ablate(pa, 16u))
     {
 #pragma unroll
         for (int k = 0; k < kPer; ++k)
@@ -594,7 +591,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     // (c) fold per tile node (tile-major partials: the tile's block is one contiguous store)
     double pap = 0.0;
     const float sM = (float)s.sM;
-    for (uint32_t i = threadIdx.x; i < ((pa.abl & 8u) ? 0u : nn); i += NT)
+    for (uint32_t i = threadIdx.x; i < (ablate(pa, 8u) ? 0u : nn); i += NT)
     {
         const uint2 tn = i == threadIdx.x ? tn0 : T.tnode[nb + i];
         float a0 = 0.f, a1 = 0.f, a2 = 0.f;
@@ -643,7 +640,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
             q[1] = sp[ms + i];
             q[2] = sp[2 * ms + i];
         }
-        if (MODE == 1 && !(pa.abl & 4u) && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
+        if (MODE == 1 && !ablate(pa, 4u) && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
         {
             const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
             pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
@@ -854,7 +851,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
         for (int k = 0; k < 2; ++k)
         {
             const uint32_t j = threadIdx.x + k * NT;
-            if (j < ne && !(pa.abl & 64u))
+            if (j < ne && !ablate(pa, 64u))
             {
                 float f[12];
                 geo_element_forces<ISO>(s, k ? id1 : id0, sxp, sq, sK6, k ? mat1 : mat0, dtab, f);
@@ -870,10 +867,10 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
         }
         __syncthreads();
         // (d) next tile's gathers (its node records have arrived by now; ablation bit 256: skipped)
-        if (tn_next < t_end && !(pa.abl & 256u))
+        if (tn_next < t_end && !ablate(pa, 256u))
             pipe_issue_gather<SANITIZE, MODE>(s, x, pa.z, hdn.w, cur);
         // (e) fold per tile node -> node-major partials (+ p.Ap) (ablation bit 128: skipped)
-        if (threadIdx.x < ((pa.abl & 128u) ? 0u : nn))  // nn <= 256: one tile node per lane
+        if (threadIdx.x < (ablate(pa, 128u) ? 0u : nn))  // nn <= 256: one tile node per lane
         {
             const uint32_t i = threadIdx.x;
             const uint2 tn = tn_own;
@@ -901,9 +898,9 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                 }
             }
             // ablation (diagnostic timing only): 512 = no partial store, 1024 = tile-major store position
-            if (!(pa.abl & 512u))
+            if (!ablate(pa, 512u))
             {
-                float *o = T.part + 3ull * ((pa.abl & 1024u) ? hd.z + i : slot_own);
+                float *o = T.part + 3ull * (ablate(pa, 1024u) ? hd.z + i : slot_own);
                 o[0] = a0;
                 o[1] = a1;
                 o[2] = a2;
@@ -1246,21 +1243,21 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
             group_issue_records<NT>(s, hdn, cur);
         hd2 = tn_next + nbx < t_end ? hdr[tn_next + nbx] : uint4{0u, 0u, 0u, 0u};
         // (c) this lane's group (ablation bit 64: skipped, diagnostic timing only)
-        if (threadIdx.x < ng && !(pa.abl & 64u))
+        if (threadIdx.x < ng && !ablate(pa, 64u))
         {
             const float *Dm = MONO ? s.d1 : dtab + kTab * (gr.y >> 27);
             group_forces<ISO>(gr, sxp, sq, sst, sK6, Dm, sfxy, sfz);
         }
         __syncthreads();
         // (d) next tile's gathers (ablation bit 256: skipped)
-        if (tn_next < t_end && !(pa.abl & 256u))
+        if (tn_next < t_end && !ablate(pa, 256u))
             group_issue_gather<SANITIZE, MODE>(s, x, pa.z, cur);
         // (e) fold per tile node -> node-major partials (+ p.Ap) (ablation bit 128: skipped)
 #pragma unroll
         for (int k = 0; k < 2; ++k)
         {
             const uint32_t i = threadIdx.x + k * NT;
-            if (i < ((pa.abl & 128u) ? 0u : nn))
+            if (i < (ablate(pa, 128u) ? 0u : nn))
             {
                 const uint2 tn = tn_own[k];
                 float a0, a1, a2;
@@ -1281,7 +1278,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
                             store3(pa.pnew, whole_rsrc(pa.pnew), tn.x & 0x7fffffffu, p0, p1, p2, false);
                     }
                 }
-                if (!(pa.abl & 512u))
+                if (!ablate(pa, 512u))
                     store3(T.part, whole_rsrc(T.part), slot_own[k], a0, a1, a2, T.wt_part != 0);
                 if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
                     pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
@@ -1778,12 +1775,6 @@ unsigned fast_pipe_grid(const DevSys &s)
         const unsigned g = s.iso ? (s.M == 1 ? group_grid<true, true>(nt) : group_grid<true, false>(nt))
                                  : (s.M == 1 ? group_grid<false, true>(nt) : group_grid<false, false>(nt));
         const unsigned need = ((s.t.ntiles + 7u) / 8u) * 8u;
-        static const bool all = [] {  // CWF_GROUP_GRID=all: one tile per workgroup (diagnostic)
-            const char *e = getenv("CWF_GROUP_GRID");
-            return e && std::string(e) == "all";
-        }();
-        if (all)
-            return need ? need : 8u;
         return g < need ? g : (need ? need : 8u);
     }
     if (s.t.hex)
@@ -1809,28 +1800,14 @@ unsigned update_resident()
 // shares ask with the flag of the iteration that produced them
 unsigned fast_update_blocks(const DevSys &s, bool flush)
 {
-    static const unsigned resident[2][2] = {
-        {update_resident<1, false>(), update_resident<1, true>()},
-        {update_resident<2, false>(), update_resident<2, true>()}};
-    const unsigned res = resident[upd_unroll() == 2][flush ? 1 : 0];
-    const unsigned g = grid_for(s.N, kUpdThreads * (unsigned)upd_unroll());
-    static const bool all = [] {  // CWF_UPD_GRID=all: one node per thread, no grid stride (diagnostic)
-        const char *e = getenv("CWF_UPD_GRID");
-        return e && std::string(e) == "all";
-    }();
-    if (all)
-        return g ? g : 1u;
+    static const unsigned resident[2] = {update_resident<1, false>(), update_resident<1, true>()};
+    const unsigned res = resident[flush ? 1 : 0];
+    const unsigned g = grid_for(s.N, kUpdThreads);
     return g < res ? (g ? g : 1u) : res;
 }
 
-static int tile_threads()
-{
-    static int nt = [] {
-        const char *e = getenv("CWF_TILE_THREADS");
-        return e && atoi(e) == 512 ? 512 : 256;
-    }();
-    return nt;
-}
+// workgroup size of the one-tile-per-workgroup per-tet kernel (k_keff_tiles)
+static int tile_threads() { return 256; }
 
 void fast_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, double *part,
                   hipStream_t st)
@@ -1873,7 +1850,7 @@ inline PBufs fast_p_bufs(cwf_hip_system *h) { return PBufs{{h->p, h->p2, h->p3, 
 static unsigned x_lag()
 {
     static const unsigned v = [] {
-        const char *e = getenv("CWF_XLAG");
+        const char *e = knob("CWF_XLAG");
         const int k = e ? atoi(e) : (int)kXLag;
         return (unsigned)(k < 1 ? 1 : k > (int)kXLag ? (int)kXLag : k);
     }();
@@ -1913,15 +1890,8 @@ __global__ __launch_bounds__(256) void k_x_flush(DevSys s, const float *__restri
     }
 }
 
-// CWF_WT=0 (diagnostic): plain x / r / z stores in the update pass instead of write-through
-static bool update_write_through()
-{
-    static const bool v = [] {
-        const char *e = getenv("CWF_WT");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
+// x / r / z of the update pass are stored write-through (store3; C2 +2.7% PCG it/s, C3 neutral)
+static bool update_write_through() { return true; }
 
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
@@ -1929,10 +1899,7 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e
     const DevSys &s = h->ds;
     if (!s.t.ntiles)
         return;
-    static const unsigned abl = [] {
-        const char *e = getenv("CWF_ABLATE");
-        return e ? (unsigned)atoi(e) : 0u;
-    }();
+    const unsigned abl = 0u;
     // beta / convergence: a single handle folds the update kernel's per-workgroup {r.r, r.z} shares
     // directly; a shard reads the all-gathered per-rank pairs
     PcgArgs pa = fast_direct_fold(h)
@@ -1952,8 +1919,7 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
     const DevSys &s = h->ds;
     const bool direct = fast_direct_fold(h);
     const bool xf = x_flush_iter(it);
-    const auto k = upd_unroll() == 2 ? (xf ? k_pcg_update_tiles<2, true> : k_pcg_update_tiles<2, false>)
-                                     : (xf ? k_pcg_update_tiles<1, true> : k_pcg_update_tiles<1, false>);
+    const auto k = xf ? k_pcg_update_tiles<1, true> : k_pcg_update_tiles<1, false>;
     k<<<fast_update_blocks(s, xf), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
         direct ? h->part0 : h->g_pap, direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it,
@@ -2009,16 +1975,9 @@ void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStr
 }
 
 // a single (unsharded) handle skips the per-rank fold kernels: every consumer workgroup refolds the
-// producer's per-workgroup shares itself (<= 2048 doubles, L2-served), two launches fewer per iteration.
-// CWF_FOLD=kernel keeps the fold kernels (A/B diagnostic).
-bool fast_direct_fold(const cwf_hip_system *h)
-{
-    static const bool kernel_fold = [] {
-        const char *e = getenv("CWF_FOLD");
-        return e && std::string(e) == "kernel";
-    }();
-    return !h->sharded() && !kernel_fold;
-}
+// producer's per-workgroup shares itself (<= 2048 doubles, L2-served), two launches fewer per iteration
+// (C2 +11% PCG it/s against fold kernels, same-box A/B, round 2)
+bool fast_direct_fold(const cwf_hip_system *h) { return !h->sharded(); }
 
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st)
 {

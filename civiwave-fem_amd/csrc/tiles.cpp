@@ -151,7 +151,7 @@ int build_tiles(const cwf_system_desc *d, HostTiles &out, uint32_t max_nodes, ui
         }
         std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
         static const int tile_order = [] {  // CWF_TILE_ORDER=morton|rcb (diagnostic; default by element)
-            const char *v = getenv("CWF_TILE_ORDER");
+            const char *v = knob("CWF_TILE_ORDER");
             return !v ? -1 : std::string(v) == "morton" ? 0 : 1;
         }();
         // tets: RCB leaves (C3 tiles kernel 223 -> 200 us, same-box A/B); hex8: Morton segments, whose
