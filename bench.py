@@ -389,11 +389,11 @@ def main():
             "roofline_hbm": hbm,
         }
         if args.mode == "parity" and keff_n.value:
-            # k_keff_parity recomputes each tet's fp64 element math once per incidence (4 per tet): strain 72,
-            # stress 24 (isotropic D), V s_K 1, corner force 24 + scale 3 flops = 124 fp64 flops per incidence
-            # (kernels_parity.hip). Bound: the fp64 vector rate (AMD MI355X spec 78.6 TFLOP/s; not in the
-            # microarch guide) or the L2/MALL traffic of the 4 re-reads per tet, not HBM.
-            flops = 124.0 * 4.0 * local_tets
+            # the element pass computes each tet's fp64 element math once: strain 72, stress 24 (isotropic D),
+            # V s_K 1, 4 corner forces x (18 + 3 scale) = 84, and the node fold adds 3 per incidence (12 per tet):
+            # 193 fp64 flops per tet (kernels_parity.hip). The fp64 vector peak is AMD's MI355X spec (78.6 TFLOP/s,
+            # not in the microarch guide); avg_launch_ms brackets the element pass and the node fold.
+            flops = 193.0 * local_tets
             result["roofline_fp64"] = {"bound": "valu_fp64", "achieved": flops / (avg_keff_ms * 1e-3) / 1e12,
                                        "peak": 78.6, "unit": "TFLOP/s",
                                        "frac": flops / (avg_keff_ms * 1e-3) / 1e12 / 78.6,

@@ -103,6 +103,19 @@ bool iso_pattern(const double *D)
     return true;
 }
 
+// the per-incidence fp64 force planes of the element-centric PARITY K_eff (3 x fslots doubles, ~96 B per tet),
+// allocated once a handle runs PARITY
+int parity_force_buffer(cwf_hip_system *h)
+{
+    if (h->ds.pforce || !h->ds.ipos || !h->ds.E)
+        return 0;
+    double *f = nullptr;
+    if (int st = dalloc(h, &f, 3ull * h->ds.fslots))
+        return st;
+    h->ds.pforce = f;
+    return 0;
+}
+
 int check_ready(cwf_hip_system *h)
 {
     if (!h)
@@ -518,6 +531,12 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     const char *rn = knob("CWF_RENUMBER");
     const bool renumber = d->mode == CWF_MODE_FAST && E && N && d->node_coords &&
                           !(d->reserved & CWF_DESC_KEEP_NODE_ORDER) && !(rn && rn[0] == '0');
+    // FAST recomputes tet geometry from node coordinates when they reproduce the desc's gradients (GEO); only
+    // then can the tets group into fans (the groups kernel has no gradient stream). Node renumbering does not
+    // change it, so it is decided once, on the caller's desc.
+    const char *ge = knob("CWF_GEO");
+    const bool geo_ok = E && N && d->node_coords && !(ge && ge[0] == '0') &&
+                        (d->element_connectivity[4] != 0xFFFFFFFFu || geometry_matches(d));
     if (renumber)
     {
         const auto apply_perm = [&]() {
@@ -549,7 +568,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             // and tiles are built from coordinates and tet order only, so the rebuild after this renumbering
             // gives the same partition.
             const char *ot = knob("CWF_OWNER_ORDER");
-            if (!(ot && ot[0] == '0') && (hex || (d->material_count <= 16 && groups_enabled())))
+            if (!(ot && ot[0] == '0') && (hex || (d->material_count <= 16 && groups_enabled() && geo_ok)))
             {
                 cwf_system_desc md = *d;
                 md.element_connectivity = r_conn.data();
@@ -743,6 +762,46 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(st);
         s.off = doff;
         s.inc = dinc;
+        if (!hex)  // where the element-centric PARITY K_eff stores every incidence's force (kernels_parity.hip)
+        {
+            // node n's k-th incidence (ascending element) goes to slot fblk[n / 64] + 64 k + n % 64 of the
+            // force planes: a wave of 64 consecutive nodes folds slot k of all its nodes with one coalesced load
+            const uint64_t nb = (N + 63) / 64;
+            std::vector<uint32_t> ipos, fblk;
+            try
+            {
+                ipos.resize(4 * E);
+                fblk.resize(nb + 1);
+            }
+            catch (const std::bad_alloc &)
+            {
+                return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
+            }
+            uint64_t slots = 0;
+            for (uint64_t b = 0; b < nb; ++b)
+            {
+                fblk[b] = (uint32_t)slots;
+                uint32_t kmax = 0;
+                for (uint64_t n = 64 * b; n < std::min<uint64_t>(N, 64 * b + 64); ++n)
+                    kmax = std::max(kmax, off[n + 1] - off[n]);
+                slots += 64ull * kmax;
+            }
+            if (slots >= (1ull << 32))
+                return bail(set_error(h, CWF_ERR_UNSUPPORTED, "mesh too large for one PARITY handle (shard it)",
+                                      "force_slots=" + std::to_string(slots)));
+            fblk[nb] = (uint32_t)slots;
+            for (uint64_t n = 0; n < N; ++n)
+                for (uint32_t j = off[n]; j < off[n + 1]; ++j)
+                    ipos[inc[j]] = fblk[n / 64] + 64u * (j - off[n]) + (uint32_t)(n % 64);  // inc = element << 2 | corner
+            uint32_t *dp, *db;
+            if (int st = upload(h, &dp, ipos.data(), 4 * E))
+                return bail(st);
+            if (int st = upload(h, &db, fblk.data(), nb + 1))
+                return bail(st);
+            s.ipos = dp;
+            s.fblk = db;
+            s.fslots = slots;
+        }
     }
     // FAST-mode element tiles (tiles.cpp)
     if (E)
@@ -751,8 +810,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         DevTiles &t = s.t;
         // GEO: stream 8-B corner ids + tile-node coordinates and recompute gradients/volume on the fly,
         // when the desc carries coordinates that reproduce its gradients (CWF_GEO=0 forces the records)
-        const char *ge = knob("CWF_GEO");
-        t.geo = hex || ((!ge || ge[0] != '0') && d->node_coords && N && geometry_matches(d)) ? 1 : 0;
+        t.geo = hex || geo_ok ? 1 : 0;
         if (hex)  // k_keff_hex_tiles: hex_nt lanes, one hex and two tile nodes per lane, push fold
         {
             t.hex = 1;
@@ -1079,6 +1137,9 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (int st = dalloc(h, &h->pbuf, 13 * N))
             return bail(st);
     }
+    if (h->mode == CWF_MODE_PARITY)
+        if (int st = parity_force_buffer(h))
+            return bail(st);
     HIPTRY(h, hipMemset(h->x, 0, D * sizeof(float)));
     HIPTRY(h, hipMemset(h->ctl, 0, sizeof(Ctl)));
     HIPTRY(h, hipMemset(h->g_pap, 0, 6 * sizeof(double)));
@@ -1107,6 +1168,8 @@ int cwf_hip_system_set_mode(cwf_hip_system *h, int mode)
         return set_error(h, CWF_ERR_UNSUPPORTED, "a renumbered FAST handle cannot switch to CWF_MODE_PARITY",
                          "create the PARITY handle separately (or with CWF_DESC_KEEP_NODE_ORDER)");
     h->mode = mode == CWF_MODE_FAST ? CWF_MODE_FAST : CWF_MODE_PARITY;
+    if (h->mode == CWF_MODE_PARITY)
+        return parity_force_buffer(h);
     return 0;
 }
 
@@ -1244,8 +1307,9 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         *layout_bytes = 16ull * s.t.ntiles + E * (rec + (s.t.mat ? 4 : 0)) +
                         T * (8 + (s.t.geo ? 12 : 0) + (s.t.node_major ? 4 : 0) + 12) + N * (24 + 4 + 12);
     }
-    else  // PARITY node gather: 64-B element records + vol + CSR incidences, per node x in / y out + mass + mask
-        *layout_bytes = E * (64 + 4 + 16 + (s.M > 1 ? 4 : 0)) + N * (4 + 12 + 12 + 4 + 4);
+    else  // PARITY element pass + node fold: per tet the 64-B record, vol, 4 incidence positions, the 4 fp64
+          // corner forces written and read back (2 x 96 B); per node CSR offset, x in, y out, mass, mask
+        *layout_bytes = E * (64 + 4 + 16 + 2 * 96 + (s.M > 1 ? 4 : 0)) + N * (4 + 12 + 12 + 4 + 4);
     return 0;
 }
 
@@ -1254,8 +1318,8 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     if (!h)
         return nullptr;
     const DevTiles &t = h->ds.t;
-    if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize)
-        return h->ds.iso ? "k_keff_parity<true, false>" : "k_keff_parity<false, false>";
+    if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
+        return h->ds.iso ? "k_keff_parity_elem<true, false>" : "k_keff_parity_elem<false, false>";
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
     {
         static thread_local char name[96];

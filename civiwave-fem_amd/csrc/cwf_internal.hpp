@@ -158,6 +158,13 @@ struct DevSys
     const uint32_t *mask = nullptr;
     const uint32_t *off = nullptr;
     const uint32_t *inc = nullptr;
+    // element-centric PARITY K_eff (kernels_parity.hip): the force of node n's k-th incidence (ascending element)
+    // lives in slot fblk[n / 64] + 64 k + n % 64 of three fp64 planes pforce[c * fslots + slot] (allocated with
+    // PARITY mode); ipos[4e + a] = the slot of incidence (e, a)
+    const uint32_t *ipos = nullptr;
+    const uint32_t *fblk = nullptr;  // [ceil(N / 64) + 1]
+    uint64_t fslots = 0;
+    double *pforce = nullptr;
     double sK = 1.0;  // stiffness_scale
     double sM = 0.0;  // mass_factor
     int iso = 0;      // every material has the isotropic Voigt zero pattern

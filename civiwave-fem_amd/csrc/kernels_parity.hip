@@ -87,15 +87,97 @@ __device__ __forceinline__ void stress_fp64(const double *Dm, const double e[6],
     }
 }
 
-// K_eff x, one thread per node, fp64 element math recomputed per incidence (pcg.cpp:505-694).
+// f[col] = (sum_r B[r][col] sigma_r) * vol for one corner (pcg.cpp:643-651), the term the scatter adds
+__device__ __forceinline__ void corner_force(double ax, double ay, double az, const double sig[6], double vol,
+                                             double f[3])
+{
+    double fx = 0.0, fy = 0.0, fz = 0.0;
+    fx += ax * sig[0];
+    fx += ay * sig[3];
+    fx += az * sig[5];
+    fy += ay * sig[1];
+    fy += ax * sig[3];
+    fy += az * sig[4];
+    fz += az * sig[2];
+    fz += ay * sig[4];
+    fz += ax * sig[5];
+    f[0] = fx * vol;
+    f[1] = fy * vol;
+    f[2] = fz * vol;
+}
+
+// strain / stress of tet e from its record and the (optionally sanitised) corner values (pcg.cpp:574-640):
+// gradients g{x,y,z}[4] in fp64, stress sig[6]
 template <bool ISO, bool SANITIZE>
-__global__ __launch_bounds__(kBlock) void k_keff_parity(DevSys s, const float *__restrict__ x,
-                                                        float *__restrict__ y, const Ctl *__restrict__ ctl)
+__device__ __forceinline__ void tet_stress(const DevSys &s, const Grad &G, const float *__restrict__ x,
+                                           const double *dtab, uint32_t mi, double gx[4], double gy[4], double gz[4],
+                                           double sig[6])
 {
     constexpr int kTab = ISO ? 12 : 36;
-    __shared__ double dtab[kMaxLdsMaterials * 36];
-    if (ctl && !ctl->active)
-        return;
+    double u[12];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t m = G.c[q];
+        const float *xp = x + 3u * m;
+        double u0 = (double)xp[0], u1 = (double)xp[1], u2 = (double)xp[2];
+        if constexpr (SANITIZE)
+        {
+            const uint32_t mk = s.mask[m];
+            if (mk & 1u)
+                u0 = 0.0;
+            if (mk & 2u)
+                u1 = 0.0;
+            if (mk & 4u)
+                u2 = 0.0;
+        }
+        u[3 * q + 0] = u0;
+        u[3 * q + 1] = u1;
+        u[3 * q + 2] = u2;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        gx[q] = (double)G.g[3 * q + 0];
+        gy[q] = (double)G.g[3 * q + 1];
+        gz[q] = (double)G.g[3 * q + 2];
+    }
+    double eps[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        eps[0] += gx[q] * u[3 * q + 0];
+        eps[1] += gy[q] * u[3 * q + 1];
+        eps[2] += gz[q] * u[3 * q + 2];
+        eps[3] += gy[q] * u[3 * q + 0];
+        eps[3] += gx[q] * u[3 * q + 1];
+        eps[4] += gz[q] * u[3 * q + 1];
+        eps[4] += gy[q] * u[3 * q + 2];
+        eps[5] += gz[q] * u[3 * q + 0];
+        eps[5] += gx[q] * u[3 * q + 2];
+    }
+    if (mi < (uint32_t)kMaxLdsMaterials)
+        stress_fp64<ISO>(dtab + kTab * mi, eps, sig);
+    else
+    {
+        double tab[36];
+        for (int t = 0; t < kTab; ++t)
+        {
+            uint32_t src;
+            if constexpr (ISO)
+                src = t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7;
+            else
+                src = t;
+            tab[t] = s.dmat[36u * mi + src];
+        }
+        stress_fp64<ISO>(tab, eps, sig);
+    }
+}
+
+template <bool ISO>
+__device__ __forceinline__ void stage_dtab(const DevSys &s, double *dtab)
+{
+    constexpr int kTab = ISO ? 12 : 36;
     const uint32_t nm = s.M < kMaxLdsMaterials ? s.M : kMaxLdsMaterials;
     for (uint32_t i = threadIdx.x; i < nm * kTab; i += kBlock)
     {
@@ -107,101 +189,64 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity(DevSys s, const float *_
             src = t;
         dtab[i] = s.dmat[36u * m + src];
     }
+}
+
+// K_eff x (pcg.cpp:505-694), element-centric: one thread per tet computes its strain and stress once and its 4
+// corner forces, each the exact fp64 term the reference's scatter adds (pcg.cpp:643-661), and stores it at the
+// incidence's position in the node-major CSR (ipos). The node pass then folds each node's contiguous run in
+// ascending element order from +0.0: the reference's additions in the reference's order, so y is bit-identical.
+// Round 2's node-centric gather (one thread per node recomputing every incident tet, 4x the fp64 element work
+// and 4 reads of every tet record) took 293 us on C2 against 76 + 85 us for this pair (r03c / r03f profiles).
+template <bool ISO, bool SANITIZE>
+__global__ __launch_bounds__(kBlock) void k_keff_parity_elem(DevSys s, const float *__restrict__ x,
+                                                             const Ctl *__restrict__ ctl)
+{
+    __shared__ double dtab[kMaxLdsMaterials * 36];
+    if (ctl && !ctl->active)
+        return;
+    stage_dtab<ISO>(s, dtab);
     __syncthreads();
+    const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= s.E)
+        return;
+    Grad G;
+    load_erec(s.erec, e, G);
+    double gx[4], gy[4], gz[4], sig[6];
+    tet_stress<ISO, SANITIZE>(s, G, x, dtab, s.mat[e], gx, gy, gz, sig);
+    const double vol = (double)s.vol[e] * s.sK;  // pcg.cpp:642
+    const uint4 pos = reinterpret_cast<const uint4 *>(s.ipos)[e];
+    const uint32_t j[4] = {pos.x, pos.y, pos.z, pos.w};
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+    {
+        double f[3];
+        corner_force(gx[a], gy[a], gz[a], sig, vol, f);
+        s.pforce[j[a]] = f[0];
+        s.pforce[s.fslots + j[a]] = f[1];
+        s.pforce[2 * s.fslots + j[a]] = f[2];
+    }
+}
+
+// node pass of the element-centric K_eff: the ascending-element fold of the node's incidence forces, then the
+// mass term, Dirichlet identity rows and the cast (pcg.cpp:653-691)
+template <bool SANITIZE>
+__global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const float *__restrict__ x,
+                                                             float *__restrict__ y, const Ctl *__restrict__ ctl)
+{
+    if (ctl && !ctl->active)
+        return;
     const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
     if (n >= s.N)
         return;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-    const uint32_t jb = s.off[n], je = s.off[n + 1];
-    for (uint32_t j = jb; j < je; ++j)
+    const double *f = s.pforce + s.fblk[n / 64u] + (n % 64u);
+    const uint32_t cnt = s.off[n + 1] - s.off[n];
+    for (uint32_t k = 0; k < cnt; ++k)  // slot k of the node's wave block: one coalesced load per plane
     {
-        const uint32_t inc = s.inc[j];
-        const uint32_t e = inc >> 2, a = inc & 3u;
-        Grad G;
-        load_erec(s.erec, e, G);
-        double u[12];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            const uint32_t m = G.c[q];
-            const float *xp = x + 3u * m;
-            double u0 = (double)xp[0], u1 = (double)xp[1], u2 = (double)xp[2];
-            if constexpr (SANITIZE)
-            {
-                const uint32_t mk = s.mask[m];
-                if (mk & 1u)
-                    u0 = 0.0;
-                if (mk & 2u)
-                    u1 = 0.0;
-                if (mk & 4u)
-                    u2 = 0.0;
-            }
-            u[3 * q + 0] = u0;
-            u[3 * q + 1] = u1;
-            u[3 * q + 2] = u2;
-        }
-        double gx[4], gy[4], gz[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            gx[q] = (double)G.g[3 * q + 0];
-            gy[q] = (double)G.g[3 * q + 1];
-            gz[q] = (double)G.g[3 * q + 2];
-        }
-        // strain = B u, columns ascending (pcg.cpp:622-630)
-        double eps[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            eps[0] += gx[q] * u[3 * q + 0];
-            eps[1] += gy[q] * u[3 * q + 1];
-            eps[2] += gz[q] * u[3 * q + 2];
-            eps[3] += gy[q] * u[3 * q + 0];
-            eps[3] += gx[q] * u[3 * q + 1];
-            eps[4] += gz[q] * u[3 * q + 1];
-            eps[4] += gy[q] * u[3 * q + 2];
-            eps[5] += gz[q] * u[3 * q + 0];
-            eps[5] += gx[q] * u[3 * q + 2];
-        }
-        const uint32_t mi = s.mat[e];
-        const double *Dm = mi < (uint32_t)kMaxLdsMaterials ? dtab + kTab * mi : nullptr;
-        double sig[6];
-        if (Dm)
-            stress_fp64<ISO>(Dm, eps, sig);
-        else
-        {
-            double tab[36];
-            for (int t = 0; t < kTab; ++t)
-            {
-                uint32_t src;
-                if constexpr (ISO)
-                    src = t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7;
-                else
-                    src = t;
-                tab[t] = s.dmat[36u * mi + src];
-            }
-            stress_fp64<ISO>(tab, eps, sig);
-        }
-        const double vol = (double)s.vol[e] * s.sK;  // pcg.cpp:642
-        const double ax = a == 0 ? gx[0] : a == 1 ? gx[1] : a == 2 ? gx[2] : gx[3];
-        const double ay = a == 0 ? gy[0] : a == 1 ? gy[1] : a == 2 ? gy[2] : gy[3];
-        const double az = a == 0 ? gz[0] : a == 1 ? gz[1] : a == 2 ? gz[2] : gz[3];
-        // f[col] = (sum_r B[r][col] sigma_r) * vol (pcg.cpp:643-651)
-        double fx = 0.0, fy = 0.0, fz = 0.0;
-        fx += ax * sig[0];
-        fx += ay * sig[3];
-        fx += az * sig[5];
-        fy += ay * sig[1];
-        fy += ax * sig[3];
-        fy += az * sig[4];
-        fz += az * sig[2];
-        fz += ay * sig[4];
-        fz += ax * sig[5];
-        acc0 += fx * vol;
-        acc1 += fy * vol;
-        acc2 += fz * vol;
+        acc0 += f[64ull * k];
+        acc1 += f[s.fslots + 64ull * k];
+        acc2 += f[2 * s.fslots + 64ull * k];
     }
-    // mass term (pcg.cpp:664-672), Dirichlet identity rows (674-686), cast (688-691)
     const uint32_t mk = s.mask[n];
     const double m = (double)s.mass[n] * s.sM;
     const float x0 = x[3u * n + 0], x1 = x[3u * n + 1], x2 = x[3u * n + 2];
@@ -449,104 +494,193 @@ __global__ __launch_bounds__(kBlock) void k_dot_chunks_generic(const float *__re
         pac[k] = s1;
 }
 
-// chunk = 256 DOFs: one wave per 64 chunks, 32-DOF slabs staged through LDS so that the
-// global loads are coalesced 128-B runs while each lane keeps its chunk's sequential fold.
+// chunk = 256 DOFs: a 256-thread workgroup per 32 chunks. The workgroup stages the 32 x 256 values of every
+// operand through LDS with coalesced loads (rows padded to 257 floats, so the 32 folding lanes hit 32 different
+// banks), then lane c of wave 0 folds chunk c sequentially, in DOF order (pcg.cpp:189-199); the fp32 x fp32
+// products are exact in fp64. Values past D are staged as 0: +0.0 * +0.0 added to a fold that started at +0.0 is
+// exact (such a fold is never -0.0), so the tail chunk equals the reference's shorter loop.
+constexpr int kDotChunksPerBlock = 32;
+constexpr int kDotRow = 257;
 template <int NV>
-__global__ __launch_bounds__(64) void k_dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
-                                                      const float *__restrict__ c, uint32_t D, uint32_t chunks,
-                                                      double *__restrict__ pab, double *__restrict__ pac,
-                                                      const Ctl *__restrict__ ctl)
+__global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
+                                                       const float *__restrict__ c, uint32_t D, uint32_t chunks,
+                                                       double *__restrict__ pab, double *__restrict__ pac,
+                                                       const Ctl *__restrict__ ctl)
 {
-    __shared__ float sa[64][33];
-    __shared__ float sb[64][33];
-    __shared__ float sc[NV == 2 ? 64 : 1][33];
+    __shared__ float sa[kDotChunksPerBlock * kDotRow];
+    __shared__ float sb[kDotChunksPerBlock * kDotRow];
+    __shared__ float sc[NV == 2 ? kDotChunksPerBlock * kDotRow : 1];
     if (ctl && !ctl->active)
         return;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t c0 = blockIdx.x * 64u;
+    const uint64_t base = (uint64_t)blockIdx.x * kDotChunksPerBlock * 256u;
+    // 16-B loads (4 DOFs per lane and step) when the operands are 16-B aligned (a caller's device pointer need
+    // not be); a block's range starts 32 KB into the vector, the tail past D goes scalar
+    const bool al = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                      reinterpret_cast<uintptr_t>(NV == 2 ? c : a)) & 15u) == 0;
+    for (uint32_t i = 4u * threadIdx.x; i < kDotChunksPerBlock * 256u; i += 1024u)
+    {
+        const uint64_t gi = base + i;
+        const uint32_t l = (i >> 8) * kDotRow + (i & 255u);  // 4 consecutive DOFs stay in one row
+        if (al && gi + 4u <= D)
+        {
+            const float4 va = *reinterpret_cast<const float4 *>(a + gi);
+            const float4 vb = *reinterpret_cast<const float4 *>(b + gi);
+            sa[l] = va.x, sa[l + 1] = va.y, sa[l + 2] = va.z, sa[l + 3] = va.w;
+            sb[l] = vb.x, sb[l + 1] = vb.y, sb[l + 2] = vb.z, sb[l + 3] = vb.w;
+            if constexpr (NV == 2)
+            {
+                const float4 vc = *reinterpret_cast<const float4 *>(c + gi);
+                sc[l] = vc.x, sc[l + 1] = vc.y, sc[l + 2] = vc.z, sc[l + 3] = vc.w;
+            }
+        }
+        else
+            for (uint32_t u = 0; u < 4u; ++u)
+            {
+                const bool ok = gi + u < D;
+                sa[l + u] = ok ? a[gi + u] : 0.0f;
+                sb[l + u] = ok ? b[gi + u] : 0.0f;
+                if constexpr (NV == 2)
+                    sc[l + u] = ok ? c[gi + u] : 0.0f;
+            }
+    }
+    __syncthreads();
+    if (threadIdx.x >= kDotChunksPerBlock)
+        return;
+    const uint32_t k = blockIdx.x * kDotChunksPerBlock + threadIdx.x;
+    if (k >= chunks)
+        return;
+    const float *ra = sa + threadIdx.x * kDotRow, *rb = sb + threadIdx.x * kDotRow;
+    const float *rc = sc + (NV == 2 ? threadIdx.x * kDotRow : 0u);
     double s0 = 0.0, s1 = 0.0;
-    for (uint32_t step = 0; step < 8; ++step)
+#pragma unroll 16
+    for (uint32_t i = 0; i < 256u; ++i)
     {
-#pragma unroll 8
-        for (uint32_t q = 0; q < 32; ++q)
-        {
-            const uint32_t chunk = q * 2u + (lane >> 5), o = lane & 31u;
-            const uint64_t gi = (uint64_t)(c0 + chunk) * 256u + step * 32u + o;
-            const bool ok = gi < D;
-            sa[chunk][o] = ok ? a[gi] : 0.0f;
-            sb[chunk][o] = ok ? b[gi] : 0.0f;
-            if constexpr (NV == 2)
-                sc[chunk][o] = ok ? c[gi] : 0.0f;
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (uint32_t i = 0; i < 32; ++i)
-        {
-            const double av = (double)sa[lane][i];
-            s0 += av * (double)sb[lane][i];
-            if constexpr (NV == 2)
-                s1 += av * (double)sc[lane][i];
-        }
-        __syncthreads();
-    }
-    const uint32_t k = c0 + lane;
-    if (k < chunks)
-    {
-        pab[k] = s0;
+        const double av = (double)ra[i];
+        s0 += av * (double)rb[i];
         if constexpr (NV == 2)
-            pac[k] = s1;
+            s1 += av * (double)rc[i];
     }
+    pab[k] = s0;
+    if constexpr (NV == 2)
+        pac[k] = s1;
 }
 
-// ordered sequential fold over chunk partials: total += partial[c] (pcg.cpp:200)
+// Ordered sequential fold over chunk partials: total += partial[c] in chunk order (pcg.cpp:200). The chain of
+// fp64 adds is inherently serial (each rounding depends on the running sum), so thread 0 of a 256-thread
+// workgroup runs it, from LDS: the other 255 threads stage the next block of partials (coalesced) while thread 0
+// folds the current one, so the fold runs at the add latency instead of one global load round trip per 8
+// partials (C2: 117-127 us per scalar kernel with a single thread, r03c profile). t0 / t1 are valid in thread 0.
+constexpr int kFoldThreads = 256;
+constexpr uint32_t kFoldBlock = 2048;  // partials per staged block and operand
 template <int NC>
 __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict__ p1, uint32_t count, double &t0,
                          double &t1)
 {
+    __shared__ double buf[2][NC][kFoldBlock];
+    const uint32_t nb = (count + kFoldBlock - 1u) / kFoldBlock;
+    const auto stage = [&](uint32_t blk, uint32_t first, uint32_t step) {
+        const uint32_t b0 = blk * kFoldBlock, n = min(kFoldBlock, count - b0);
+        for (uint32_t i = first; i < n; i += step)
+        {
+            buf[blk & 1u][0][i] = p0[b0 + i];
+            if constexpr (NC == 2)
+                buf[blk & 1u][NC - 1][i] = p1[b0 + i];
+        }
+    };
     double a0 = 0.0, a1 = 0.0;
-    uint32_t c = 0;
-    for (; c + 8 <= count; c += 8)
+    if (nb)
+        stage(0, threadIdx.x, kFoldThreads);
+    __syncthreads();
+    for (uint32_t blk = 0; blk < nb; ++blk)
     {
-        double v0[8], v1[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
+        if (threadIdx.x)
         {
-            v0[q] = p0[c + q];
-            if constexpr (NC == 2)
-                v1[q] = p1[c + q];
+            if (blk + 1u < nb)
+                stage(blk + 1u, threadIdx.x - 1u, kFoldThreads - 1u);
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
+        else
         {
-            a0 += v0[q];
-            if constexpr (NC == 2)
-                a1 += v1[q];
+            // 16 partials per batch, the next batch's LDS reads issued before this batch's dependent adds
+            const double *v0 = buf[blk & 1u][0], *v1 = buf[blk & 1u][NC - 1];
+            const uint32_t n = min(kFoldBlock, count - blk * kFoldBlock);
+            constexpr uint32_t W = 16;
+            uint32_t i = 0;
+            if (n >= W)
+            {
+                double q0[W], q1[W];
+#pragma unroll
+                for (uint32_t u = 0; u < W; ++u)
+                {
+                    q0[u] = v0[u];
+                    if constexpr (NC == 2)
+                        q1[u] = v1[u];
+                }
+                for (; i + 2u * W <= n; i += W)
+                {
+                    double r0[W], r1[W];
+#pragma unroll
+                    for (uint32_t u = 0; u < W; ++u)
+                    {
+                        r0[u] = v0[i + W + u];
+                        if constexpr (NC == 2)
+                            r1[u] = v1[i + W + u];
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < W; ++u)
+                    {
+                        a0 += q0[u];
+                        if constexpr (NC == 2)
+                            a1 += q1[u];
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < W; ++u)
+                    {
+                        q0[u] = r0[u];
+                        if constexpr (NC == 2)
+                            q1[u] = r1[u];
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < W; ++u)
+                {
+                    a0 += q0[u];
+                    if constexpr (NC == 2)
+                        a1 += q1[u];
+                }
+                i += W;
+            }
+            for (; i < n; ++i)
+            {
+                a0 += v0[i];
+                if constexpr (NC == 2)
+                    a1 += v1[i];
+            }
         }
-    }
-    for (; c < count; ++c)
-    {
-        a0 += p0[c];
-        if constexpr (NC == 2)
-            a1 += p1[c];
+        __syncthreads();
     }
     t0 = a0;
     t1 = a1;
 }
 
-__global__ void k_fold1(const double *__restrict__ p, uint32_t count, double *__restrict__ out)
+__global__ __launch_bounds__(kFoldThreads) void k_fold1(const double *__restrict__ p, uint32_t count,
+                                                        double *__restrict__ out)
 {
     double t0, t1;
     fold_seq<1>(p, nullptr, count, t0, t1);
-    out[0] = t0;
+    if (threadIdx.x == 0)
+        out[0] = t0;
 }
 
-// ---- PCG scalar phases (single thread), pcg.cpp:768-895 ----
+// ---- PCG scalar phases (one workgroup; thread 0 decides), pcg.cpp:768-895 ----
 
-__global__ void k_pcg_init_scalars(Ctl *ctl, const double *__restrict__ p_rhs, const double *__restrict__ p_rr,
-                                   uint32_t count, double rel_tol, double *__restrict__ hist)
+__global__ __launch_bounds__(kFoldThreads) void k_pcg_init_scalars(Ctl *ctl, const double *__restrict__ p_rhs,
+                                                                   const double *__restrict__ p_rr, uint32_t count,
+                                                                   double rel_tol, double *__restrict__ hist)
 {
     double rhs_sq, rr;
     fold_seq<2>(p_rhs, p_rr, count, rhs_sq, rr);
+    if (threadIdx.x)
+        return;
     double rhs_norm = sqrt(rhs_sq);
     if (rhs_norm < 1.0e-12)
         rhs_norm = 1.0;
@@ -565,12 +699,15 @@ __global__ void k_pcg_init_scalars(Ctl *ctl, const double *__restrict__ p_rhs, c
     *ctl = c;
 }
 
-__global__ void k_pcg_init_rho(Ctl *ctl, const double *__restrict__ p_rz, uint32_t count)
+__global__ __launch_bounds__(kFoldThreads) void k_pcg_init_rho(Ctl *ctl, const double *__restrict__ p_rz,
+                                                               uint32_t count)
 {
     if (!ctl->active)
         return;
     double rho, unused;
     fold_seq<1>(p_rz, nullptr, count, rho, unused);
+    if (threadIdx.x)
+        return;
     ctl->rho = rho;
     if (fabs(rho) < 1.0e-18)
     {
@@ -580,12 +717,14 @@ __global__ void k_pcg_init_rho(Ctl *ctl, const double *__restrict__ p_rz, uint32
     }
 }
 
-__global__ void k_pcg_alpha(Ctl *ctl, const double *__restrict__ p_pAp, uint32_t count)
+__global__ __launch_bounds__(kFoldThreads) void k_pcg_alpha(Ctl *ctl, const double *__restrict__ p_pAp, uint32_t count)
 {
     if (!ctl->active)
         return;
     double denom, unused;
     fold_seq<1>(p_pAp, nullptr, count, denom, unused);
+    if (threadIdx.x)
+        return;
     ctl->denom = denom;
     if (fabs(denom) < 1.0e-18)
     {
@@ -599,13 +738,16 @@ __global__ void k_pcg_alpha(Ctl *ctl, const double *__restrict__ p_pAp, uint32_t
     ctl->alpha_last = alpha;
 }
 
-__global__ void k_pcg_beta(Ctl *ctl, const double *__restrict__ p_rr, const double *__restrict__ p_rz,
-                           uint32_t count, double *__restrict__ hist)
+__global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const double *__restrict__ p_rr,
+                                                           const double *__restrict__ p_rz, uint32_t count,
+                                                           double *__restrict__ hist)
 {
     if (!ctl->active)
         return;
     double rr, rz;
     fold_seq<2>(p_rr, p_rz, count, rr, rz);
+    if (threadIdx.x)
+        return;
     const double res = sqrt(rr);
     const unsigned long long it = ctl->iterations;
     ctl->res = res;
@@ -770,25 +912,24 @@ uint32_t parity_chunk_count(const cwf_hip_system *h)
     return (uint32_t)((h->ds.D + B - 1) / B);
 }
 
+// element-centric K_eff: the 4 corner forces of every tet once, then the ordered node fold (the handle holds the
+// incidence positions and the force buffer whenever it runs PARITY: abi.cpp parity_force_buffer)
 void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
 {
     if (s.N == 0)
         return;
-    const dim3 g(grid_for(s.N, kBlock)), b(kBlock);
-    if (s.iso)
+    const dim3 ge(grid_for(s.E, kBlock)), gn(grid_for(s.N, kBlock)), b(kBlock);
+    if (s.E)
     {
-        if (sanitize)
-            k_keff_parity<true, true><<<g, b, 0, st>>>(s, x, y, ctl);
+        if (s.iso)
+            sanitize ? k_keff_parity_elem<true, true><<<ge, b, 0, st>>>(s, x, ctl)
+                     : k_keff_parity_elem<true, false><<<ge, b, 0, st>>>(s, x, ctl);
         else
-            k_keff_parity<true, false><<<g, b, 0, st>>>(s, x, y, ctl);
+            sanitize ? k_keff_parity_elem<false, true><<<ge, b, 0, st>>>(s, x, ctl)
+                     : k_keff_parity_elem<false, false><<<ge, b, 0, st>>>(s, x, ctl);
     }
-    else
-    {
-        if (sanitize)
-            k_keff_parity<false, true><<<g, b, 0, st>>>(s, x, y, ctl);
-        else
-            k_keff_parity<false, false><<<g, b, 0, st>>>(s, x, y, ctl);
-    }
+    sanitize ? k_keff_parity_fold<true><<<gn, b, 0, st>>>(s, x, y, ctl)
+             : k_keff_parity_fold<false><<<gn, b, 0, st>>>(s, x, y, ctl);
 }
 
 void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
@@ -820,9 +961,9 @@ void parity_dot_partials_n(uint32_t D, uint32_t B, const float *a, const float *
     if (B == 256)
     {
         if (c)
-            k_dot_chunks256<2><<<grid_for(chunks, 64), 64, 0, st>>>(a, b, c, D, chunks, pab, pac, ctl);
+            k_dot_chunks256<2><<<grid_for(chunks, kDotChunksPerBlock), 256, 0, st>>>(a, b, c, D, chunks, pab, pac, ctl);
         else
-            k_dot_chunks256<1><<<grid_for(chunks, 64), 64, 0, st>>>(a, b, c, D, chunks, pab, pac, ctl);
+            k_dot_chunks256<1><<<grid_for(chunks, kDotChunksPerBlock), 256, 0, st>>>(a, b, c, D, chunks, pab, pac, ctl);
     }
     else
     {
@@ -843,7 +984,7 @@ void parity_dot_partials(const cwf_hip_system *h, const float *a, const float *b
 
 void parity_fold(const double *part, uint32_t count, double *out, hipStream_t st)
 {
-    k_fold1<<<1, 1, 0, st>>>(part, count, out);
+    k_fold1<<<1, kFoldThreads, 0, st>>>(part, count, out);
 }
 
 void launch_init_residual(const cwf_hip_system *h, const float *rhs, hipStream_t st)
@@ -872,10 +1013,10 @@ void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
     k_init_residual<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->Ap, h->x, h->r);
     parity_dot_partials(h, rhs, rhs, nullptr, h->part0, nullptr, nullptr, st);
     parity_dot_partials(h, h->r, h->r, nullptr, h->part1, nullptr, nullptr, st);
-    k_pcg_init_scalars<<<1, 1, 0, st>>>(h->ctl, h->part0, h->part1, chunks, rel_tol, h->hist);
+    k_pcg_init_scalars<<<1, kFoldThreads, 0, st>>>(h->ctl, h->part0, h->part1, chunks, rel_tol, h->hist);
     k_precond<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->inv, h->r, h->z, h->ctl);
     parity_dot_partials(h, h->r, h->z, nullptr, h->part0, nullptr, h->ctl, st);
-    k_pcg_init_rho<<<1, 1, 0, st>>>(h->ctl, h->part0, chunks);
+    k_pcg_init_rho<<<1, kFoldThreads, 0, st>>>(h->ctl, h->part0, chunks);
     k_p_init<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
 }
 
@@ -884,17 +1025,17 @@ void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
 void parity_init_scalars(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count, double rel_tol,
                          hipStream_t st)
 {
-    k_pcg_init_scalars<<<1, 1, 0, st>>>(h->ctl, p_rhs, p_rr, count, rel_tol, h->hist);
+    k_pcg_init_scalars<<<1, kFoldThreads, 0, st>>>(h->ctl, p_rhs, p_rr, count, rel_tol, h->hist);
 }
 
 void parity_init_rho(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st)
 {
-    k_pcg_init_rho<<<1, 1, 0, st>>>(h->ctl, p_rz, count);
+    k_pcg_init_rho<<<1, kFoldThreads, 0, st>>>(h->ctl, p_rz, count);
 }
 
 void parity_alpha(cwf_hip_system *h, const double *p_pap, uint32_t count, hipStream_t st)
 {
-    k_pcg_alpha<<<1, 1, 0, st>>>(h->ctl, p_pap, count);
+    k_pcg_alpha<<<1, kFoldThreads, 0, st>>>(h->ctl, p_pap, count);
 }
 
 void parity_update(cwf_hip_system *h, const float *rhs, hipStream_t st)
@@ -904,7 +1045,7 @@ void parity_update(cwf_hip_system *h, const float *rhs, hipStream_t st)
 
 void parity_beta(cwf_hip_system *h, const double *p_rr, const double *p_rz, uint32_t count, hipStream_t st)
 {
-    k_pcg_beta<<<1, 1, 0, st>>>(h->ctl, p_rr, p_rz, count, h->hist);
+    k_pcg_beta<<<1, kFoldThreads, 0, st>>>(h->ctl, p_rr, p_rz, count, h->hist);
 }
 
 void parity_p_update(cwf_hip_system *h, hipStream_t st)
@@ -923,10 +1064,10 @@ void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, h
     if (e1)
         (void)hipEventRecord(e1, st);
     parity_dot_partials(h, h->p, h->Ap, nullptr, h->part0, nullptr, h->ctl, st);
-    k_pcg_alpha<<<1, 1, 0, st>>>(h->ctl, h->part0, chunks);
+    k_pcg_alpha<<<1, kFoldThreads, 0, st>>>(h->ctl, h->part0, chunks);
     k_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl);
     parity_dot_partials(h, h->r, h->r, h->z, h->part0, h->part1, h->ctl, st);
-    k_pcg_beta<<<1, 1, 0, st>>>(h->ctl, h->part0, h->part1, chunks, h->hist);
+    k_pcg_beta<<<1, kFoldThreads, 0, st>>>(h->ctl, h->part0, h->part1, chunks, h->hist);
     k_p_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
 }
 

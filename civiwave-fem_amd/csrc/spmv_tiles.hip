@@ -107,6 +107,55 @@ __device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigne
     return block_sum<NT>(v, red);
 }
 
+// the two folds of fold_all in one pass: every load of both arrays in flight together, one block reduction of
+// the pair (red: 2 NT / 64 doubles); fixed order, so every workgroup gets the same pair
+template <int NT>
+__device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const double *__restrict__ pb, unsigned count,
+                                          double *red, unsigned stride, double &ta, double &tb)
+{
+    double va = 0.0, vb = 0.0;
+    unsigned i = threadIdx.x;
+    for (; i + 3u * NT < count; i += 4u * NT)
+    {
+        double qa[4], qb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            qa[u] = pa[(size_t)(i + u * NT) * stride];
+            qb[u] = pb[(size_t)(i + u * NT) * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            va += qa[u];
+            vb += qb[u];
+        }
+    }
+    for (; i < count; i += NT)
+    {
+        va += pa[(size_t)i * stride];
+        vb += pb[(size_t)i * stride];
+    }
+    va = wave_sum(va);
+    vb = wave_sum(vb);
+    if ((threadIdx.x & 63) == 0)
+    {
+        red[2 * (threadIdx.x >> 6)] = va;
+        red[2 * (threadIdx.x >> 6) + 1] = vb;
+    }
+    __syncthreads();
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w)
+    {
+        a += red[2 * w];
+        b += red[2 * w + 1];
+    }
+    __syncthreads();
+    ta = a;
+    tb = b;
+}
+
 // pcg.cpp:862-895 for iteration `it` >= 1 from the update kernel's r.r / r.z shares (stride 1), or
 // from the all-gathered per-rank {r.r, r.z} pairs of a sharded system (stride 2, rank order).
 // Returns false when the solve is over (converged or rho breakdown); *beta_out = beta for this iteration.
@@ -121,8 +170,8 @@ __device__ __forceinline__ bool residual_step(Ctl *ctl, const double *__restrict
         *beta_out = 0.f;
         return true;
     }
-    const double rr = fold_all<NT>(prr, nparts, red, stride);
-    const double rz = fold_all<NT>(prz, nparts, red, stride);
+    double rr, rz;
+    fold_all2<NT>(prr, prz, nparts, red, stride, rr, rz);
     const double res = sqrt(rr);
     const double rho_old = ctl->rho2[(it - 1) & 1u];
     const bool conv = res <= ctl->tol;
@@ -463,7 +512,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     float *sp = lds + 14 * kTileElems;                                   // [3][ms] node values
     float *sx = sp + 3 * ms;                                             // [3][ms] node coordinates (GEO)
     __shared__ float dtab[kMaxM * kTab];
-    __shared__ double red[NT / 64];
+    __shared__ double red[2 * (NT / 64)];
     if constexpr (MODE == 1)
     {
         if (!pa.ctl->active)
@@ -785,7 +834,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
     float4 *sxp = reinterpret_cast<float4 *>(lds + 3 * SP);  // [ms] {x, y, z, v_x}
     float2 *sq = reinterpret_cast<float2 *>(sxp + ms);                   // [ms] {v_y, v_z}
     __shared__ float dtab[kMaxM * kTab];
-    __shared__ double red[NT / 64];
+    __shared__ double red[2 * (NT / 64)];
     if constexpr (MODE == 1)
     {
         if (!pa.ctl->active)
@@ -1178,7 +1227,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
     float2 *sq = reinterpret_cast<float2 *>(sxp + MS);       // [MS] {v_y, v_z}
     uint16_t *sst = reinterpret_cast<uint16_t *>(sq + MS);   // [MS] run start in the local CSR
     __shared__ float dtab[MONO ? 1 : kMaxM * kTab];
-    __shared__ double red[NT / 64];
+    __shared__ double red[2 * (NT / 64)];
     if constexpr (MODE == 1)
     {
         if (!pa.ctl->active)
@@ -1301,7 +1350,7 @@ __global__ __launch_bounds__(256) void k_pcg_check(Ctl *ctl, const double *__res
                                                    const double *__restrict__ prz, unsigned nparts, unsigned stride,
                                                    unsigned it, double *__restrict__ hist)
 {
-    __shared__ double red[4];
+    __shared__ double red[8];
     if (!ctl->active)
         return;
     float beta;
