@@ -371,11 +371,9 @@ int sharded_parity_iteration(const std::vector<cwf_hip_system *> &g, const std::
         cwf_hip_system *h = g[i];
         if (i == 0 && e0)
             (void)hipEventRecord(e0, h->stream);
-        parity_keff(h, h->p, h->Ap, false, h->ctl, h->stream);
+        parity_keff_dot(h, h->p, h->Ap, h->ctl, h->gp0 + (size_t)h->rank * S, h->stream);
         if (i == 0 && e1)
             (void)hipEventRecord(e1, h->stream);
-        parity_dot_partials_n(owned_dofs(h), block_of(h), h->p, h->Ap, nullptr, h->gp0 + (size_t)h->rank * S, nullptr,
-                              h->ctl, h->stream);
     }
     if (int st = comm_allgather(g, &cwf_hip_system::gp0, S))
         return st;
@@ -384,9 +382,7 @@ int sharded_parity_iteration(const std::vector<cwf_hip_system *> &g, const std::
         cwf_hip_system *h = g[i];
         const size_t slot = (size_t)h->rank * S;
         parity_alpha(h, h->gp0, total, h->stream);
-        parity_update(h, rhs[i], h->stream);
-        parity_dot_partials_n(owned_dofs(h), block_of(h), h->r, h->r, h->z, h->gp0 + slot, h->gp1 + slot, h->ctl,
-                              h->stream);
+        parity_update(h, rhs[i], h->gp0 + slot, h->gp1 + slot, h->stream);
     }
     if (int st = comm_exchange(g, {Gather{&cwf_hip_system::gp0, S}, Gather{&cwf_hip_system::gp1, S}}, nullptr))
         return st;

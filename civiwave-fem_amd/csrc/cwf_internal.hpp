@@ -295,7 +295,10 @@ void parity_init_scalars(cwf_hip_system *h, const double *p_rhs, const double *p
                          hipStream_t st);
 void parity_init_rho(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st);
 void parity_alpha(cwf_hip_system *h, const double *p_pap, uint32_t count, hipStream_t st);
-void parity_update(cwf_hip_system *h, const float *rhs, hipStream_t st);
+void parity_update(cwf_hip_system *h, const float *rhs, double *prr, double *prz, hipStream_t st);
+// the PCG loop's K_eff p and the chunk partials of p . Ap over the owned nodes (fused for 256-DOF chunks); and
+// parity_update's r . r / r . z partials likewise
+void parity_keff_dot(const cwf_hip_system *h, const float *p, float *Ap, const Ctl *ctl, double *pdot, hipStream_t st);
 void parity_beta(cwf_hip_system *h, const double *p_rr, const double *p_rz, uint32_t count, hipStream_t st);
 void parity_p_update(cwf_hip_system *h, hipStream_t st);
 void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);

@@ -227,44 +227,105 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_elem(DevSys s, const flo
     }
 }
 
-// node pass of the element-centric K_eff: the ascending-element fold of the node's incidence forces, then the
-// mass term, Dirichlet identity rows and the cast (pcg.cpp:653-691)
-template <bool SANITIZE>
-__global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const float *__restrict__ x,
-                                                             float *__restrict__ y, const Ctl *__restrict__ ctl)
+// A 256-thread workgroup of consecutive nodes covers 768 DOFs = three whole 256-DOF reduction chunks (workgroup b:
+// chunks 3b .. 3b + 2), so the node kernels that produce a dot's operands also produce its chunk partials: the
+// operands of the workgroup's DOFs are staged in LDS (chunk k at row 257 k, against bank conflicts) and lanes
+// 0..2 fold one chunk each, sequentially in DOF order (pcg.cpp:189-199). DOFs of nodes at or past `nlim` (the
+// owned nodes of a shard, or N) are staged as 0, an exact no-op in a fold from +0.0.
+constexpr int kChunkRow = 257;
+template <int NV>
+__device__ __forceinline__ void wg_chunk_partials(const float *sa, const float *sb, const float *sc, uint32_t chunks,
+                                                  double *pab, double *pac)
 {
+    if (threadIdx.x >= 3u)
+        return;
+    const uint32_t k = 3u * blockIdx.x + threadIdx.x;
+    if (k >= chunks)
+        return;
+    const float *ra = sa + threadIdx.x * kChunkRow, *rb = sb + threadIdx.x * kChunkRow;
+    const float *rc = sc + (NV == 2 ? threadIdx.x * kChunkRow : 0u);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll 16
+    for (uint32_t i = 0; i < 256u; ++i)
+    {
+        const double av = (double)ra[i];
+        s0 += av * (double)rb[i];
+        if constexpr (NV == 2)
+            s1 += av * (double)rc[i];
+    }
+    pab[k] = s0;
+    if constexpr (NV == 2)
+        pac[k] = s1;
+}
+
+__device__ __forceinline__ uint32_t chunk_slot(uint32_t d)  // LDS index of the workgroup's d-th DOF
+{
+    return (d >> 8) * kChunkRow + (d & 255u);
+}
+
+// node pass of the element-centric K_eff: the ascending-element fold of the node's incidence forces, then the
+// mass term, Dirichlet identity rows and the cast (pcg.cpp:653-691). DOT (the PCG loop): also the chunk partials of
+// x . y, the p . Ap of pcg.cpp:840 (wg_chunk_partials), so no separate dot pass reads p and Ap again.
+template <bool SANITIZE, bool DOT>
+__global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const float *__restrict__ x,
+                                                             float *__restrict__ y, const Ctl *__restrict__ ctl,
+                                                             double *__restrict__ pdot, uint32_t nlim,
+                                                             uint32_t chunks)
+{
+    __shared__ float sx[DOT ? 3 * kChunkRow : 1], sy[DOT ? 3 * kChunkRow : 1];
     if (ctl && !ctl->active)
         return;
     const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
-    if (n >= s.N)
-        return;
-    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-    const double *f = s.pforce + s.fblk[n / 64u] + (n % 64u);
-    const uint32_t cnt = s.off[n + 1] - s.off[n];
-    for (uint32_t k = 0; k < cnt; ++k)  // slot k of the node's wave block: one coalesced load per plane
+    float yv[3] = {0.f, 0.f, 0.f}, xv[3] = {0.f, 0.f, 0.f};
+    if (n < s.N)
     {
-        acc0 += f[64ull * k];
-        acc1 += f[s.fslots + 64ull * k];
-        acc2 += f[2 * s.fslots + 64ull * k];
+        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+        const double *f = s.pforce + s.fblk[n / 64u] + (n % 64u);
+        const uint32_t cnt = s.off[n + 1] - s.off[n];
+        for (uint32_t k = 0; k < cnt; ++k)  // slot k of the node's wave block: one coalesced load per plane
+        {
+            acc0 += f[64ull * k];
+            acc1 += f[s.fslots + 64ull * k];
+            acc2 += f[2 * s.fslots + 64ull * k];
+        }
+        const uint32_t mk = s.mask[n];
+        const double m = (double)s.mass[n] * s.sM;
+        const float x0 = x[3u * n + 0], x1 = x[3u * n + 1], x2 = x[3u * n + 2];
+        const double s0 = (SANITIZE && (mk & 1u)) ? 0.0 : (double)x0;
+        const double s1 = (SANITIZE && (mk & 2u)) ? 0.0 : (double)x1;
+        const double s2 = (SANITIZE && (mk & 4u)) ? 0.0 : (double)x2;
+        acc0 += m * s0;
+        acc1 += m * s1;
+        acc2 += m * s2;
+        if (mk & 1u)
+            acc0 = (double)x0;
+        if (mk & 2u)
+            acc1 = (double)x1;
+        if (mk & 4u)
+            acc2 = (double)x2;
+        yv[0] = (float)acc0;
+        yv[1] = (float)acc1;
+        yv[2] = (float)acc2;
+        y[3u * n + 0] = yv[0];
+        y[3u * n + 1] = yv[1];
+        y[3u * n + 2] = yv[2];
+        xv[0] = x0;
+        xv[1] = x1;
+        xv[2] = x2;
     }
-    const uint32_t mk = s.mask[n];
-    const double m = (double)s.mass[n] * s.sM;
-    const float x0 = x[3u * n + 0], x1 = x[3u * n + 1], x2 = x[3u * n + 2];
-    const double s0 = (SANITIZE && (mk & 1u)) ? 0.0 : (double)x0;
-    const double s1 = (SANITIZE && (mk & 2u)) ? 0.0 : (double)x1;
-    const double s2 = (SANITIZE && (mk & 4u)) ? 0.0 : (double)x2;
-    acc0 += m * s0;
-    acc1 += m * s1;
-    acc2 += m * s2;
-    if (mk & 1u)
-        acc0 = (double)x0;
-    if (mk & 2u)
-        acc1 = (double)x1;
-    if (mk & 4u)
-        acc2 = (double)x2;
-    y[3u * n + 0] = (float)acc0;
-    y[3u * n + 1] = (float)acc1;
-    y[3u * n + 2] = (float)acc2;
+    if constexpr (DOT)
+    {
+        const bool own = n < nlim;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+        {
+            const uint32_t l = chunk_slot(3u * threadIdx.x + k);
+            sx[l] = own ? xv[k] : 0.f;
+            sy[l] = own ? yv[k] : 0.f;
+        }
+        __syncthreads();
+        wg_chunk_partials<1>(sx, sy, nullptr, chunks, pdot, nullptr);
+    }
 }
 
 __device__ void invert_spd_3x3(double m[9], double inv[9])
@@ -567,9 +628,9 @@ __global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__
 
 // Ordered sequential fold over chunk partials: total += partial[c] in chunk order (pcg.cpp:200). The chain of
 // fp64 adds is inherently serial (each rounding depends on the running sum), so thread 0 of a 256-thread
-// workgroup runs it, from LDS: the other 255 threads stage the next block of partials (coalesced) while thread 0
-// folds the current one, so the fold runs at the add latency instead of one global load round trip per 8
-// partials (C2: 117-127 us per scalar kernel with a single thread, r03c profile). t0 / t1 are valid in thread 0.
+// workgroup runs it, from LDS: waves 1-3 stage the next block of partials (coalesced) while thread 0 folds the
+// current one, so the fold runs at the add latency instead of one global load round trip per 8 partials (C2:
+// 117-127 us per scalar kernel with a single thread, r03c profile). t0 / t1 are valid in thread 0.
 constexpr int kFoldThreads = 256;
 constexpr uint32_t kFoldBlock = 2048;  // partials per staged block and operand
 template <int NC>
@@ -593,61 +654,58 @@ __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict
     __syncthreads();
     for (uint32_t blk = 0; blk < nb; ++blk)
     {
-        if (threadIdx.x)
+        if (threadIdx.x >= 64u)  // waves 1.. stage; wave 0 is thread 0's alone (no divergent staging before it)
         {
             if (blk + 1u < nb)
-                stage(blk + 1u, threadIdx.x - 1u, kFoldThreads - 1u);
+                stage(blk + 1u, threadIdx.x - 64u, kFoldThreads - 64u);
         }
-        else
+        else if (threadIdx.x == 0)
         {
-            // 16 partials per batch, the next batch's LDS reads issued before this batch's dependent adds
+            // batches of 16 partials in two register sets: the next batch's LDS reads are issued before this
+            // batch's dependent adds, and the sets alternate (no register copies)
             const double *v0 = buf[blk & 1u][0], *v1 = buf[blk & 1u][NC - 1];
             const uint32_t n = min(kFoldBlock, count - blk * kFoldBlock);
             constexpr uint32_t W = 16;
+            double qa0[W], qa1[W], qb0[W], qb1[W];
+            const auto rd = [&](double *d0, double *d1, uint32_t at) {
+#pragma unroll
+                for (uint32_t u = 0; u < W; ++u)
+                {
+                    d0[u] = v0[at + u];
+                    if constexpr (NC == 2)
+                        d1[u] = v1[at + u];
+                }
+            };
+            const auto add = [&](const double *d0, const double *d1) {
+#pragma unroll
+                for (uint32_t u = 0; u < W; ++u)
+                {
+                    a0 += d0[u];
+                    if constexpr (NC == 2)
+                        a1 += d1[u];
+                }
+            };
             uint32_t i = 0;
             if (n >= W)
             {
-                double q0[W], q1[W];
-#pragma unroll
-                for (uint32_t u = 0; u < W; ++u)
+                rd(qa0, qa1, 0);
+                for (;;)
                 {
-                    q0[u] = v0[u];
-                    if constexpr (NC == 2)
-                        q1[u] = v1[u];
+                    const bool more_b = i + 2u * W <= n;
+                    if (more_b)
+                        rd(qb0, qb1, i + W);
+                    add(qa0, qa1);
+                    i += W;
+                    if (!more_b)
+                        break;
+                    const bool more_a = i + 2u * W <= n;
+                    if (more_a)
+                        rd(qa0, qa1, i + W);
+                    add(qb0, qb1);
+                    i += W;
+                    if (!more_a)
+                        break;
                 }
-                for (; i + 2u * W <= n; i += W)
-                {
-                    double r0[W], r1[W];
-#pragma unroll
-                    for (uint32_t u = 0; u < W; ++u)
-                    {
-                        r0[u] = v0[i + W + u];
-                        if constexpr (NC == 2)
-                            r1[u] = v1[i + W + u];
-                    }
-#pragma unroll
-                    for (uint32_t u = 0; u < W; ++u)
-                    {
-                        a0 += q0[u];
-                        if constexpr (NC == 2)
-                            a1 += q1[u];
-                    }
-#pragma unroll
-                    for (uint32_t u = 0; u < W; ++u)
-                    {
-                        q0[u] = r0[u];
-                        if constexpr (NC == 2)
-                            q1[u] = r1[u];
-                    }
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < W; ++u)
-                {
-                    a0 += q0[u];
-                    if constexpr (NC == 2)
-                        a1 += q1[u];
-                }
-                i += W;
             }
             for (; i < n; ++i)
             {
@@ -845,41 +903,56 @@ __global__ __launch_bounds__(kBlock) void k_p_init(DevSys s, const float *__rest
         p[3u * n + k] = (mk & (1u << k)) ? 0.0f : z[3u * n + k];
 }
 
-// x += f32(alpha p); r -= f32(alpha Ap); enforce; z = M^-1 r  (pcg.cpp:854-860, 877)
+// x += f32(alpha p); r -= f32(alpha Ap); enforce; z = M^-1 r  (pcg.cpp:854-860, 877), and the chunk partials of
+// r . r and r . z (pcg.cpp:862, 883) from the workgroup's own DOFs (wg_chunk_partials)
 __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__restrict__ rhs,
                                                    const float *__restrict__ inv, const float *__restrict__ p,
                                                    const float *__restrict__ Ap, float *__restrict__ x,
                                                    float *__restrict__ r, float *__restrict__ z,
-                                                   const Ctl *__restrict__ ctl)
+                                                   const Ctl *__restrict__ ctl, double *__restrict__ prr,
+                                                   double *__restrict__ prz, uint32_t nlim, uint32_t chunks)
 {
+    __shared__ float sr[3 * kChunkRow], sz[3 * kChunkRow];
     if (!ctl->active)
         return;
     const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
-    if (n >= s.N)
+    float rv[3] = {0.f, 0.f, 0.f}, zv[3] = {0.f, 0.f, 0.f};
+    if (n < s.N)
+    {
+        const double alpha = ctl->alpha;
+        const uint32_t mk = s.mask[n];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+        {
+            const uint32_t d = 3u * n + k;
+            float xv = x[d] + (float)(alpha * (double)p[d]);
+            float rr = r[d] - (float)(alpha * (double)Ap[d]);
+            if (mk & (1u << k))
+            {
+                xv = rhs[d];
+                rr = 0.0f;
+            }
+            x[d] = xv;
+            r[d] = rr;
+            rv[k] = rr;
+        }
+        precond_node(inv, n, mk, rv, zv);
+        z[3u * n] = zv[0];
+        z[3u * n + 1] = zv[1];
+        z[3u * n + 2] = zv[2];
+    }
+    if (!prr)  // a reduction chunk other than 256 DOFs: the partials are a separate pass
         return;
-    const double alpha = ctl->alpha;
-    const uint32_t mk = s.mask[n];
-    float rv[3];
+    const bool own = n < nlim;
 #pragma unroll
     for (int k = 0; k < 3; ++k)
     {
-        const uint32_t d = 3u * n + k;
-        float xv = x[d] + (float)(alpha * (double)p[d]);
-        float rr = r[d] - (float)(alpha * (double)Ap[d]);
-        if (mk & (1u << k))
-        {
-            xv = rhs[d];
-            rr = 0.0f;
-        }
-        x[d] = xv;
-        r[d] = rr;
-        rv[k] = rr;
+        const uint32_t l = chunk_slot(3u * threadIdx.x + k);
+        sr[l] = own ? rv[k] : 0.f;
+        sz[l] = own ? zv[k] : 0.f;
     }
-    float zv[3];
-    precond_node(inv, n, mk, rv, zv);
-    z[3u * n] = zv[0];
-    z[3u * n + 1] = zv[1];
-    z[3u * n + 2] = zv[2];
+    __syncthreads();
+    wg_chunk_partials<2>(sr, sr, sz, chunks, prr, prz);
 }
 
 // p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
@@ -928,8 +1001,32 @@ void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, co
             sanitize ? k_keff_parity_elem<false, true><<<ge, b, 0, st>>>(s, x, ctl)
                      : k_keff_parity_elem<false, false><<<ge, b, 0, st>>>(s, x, ctl);
     }
-    sanitize ? k_keff_parity_fold<true><<<gn, b, 0, st>>>(s, x, y, ctl)
-             : k_keff_parity_fold<false><<<gn, b, 0, st>>>(s, x, y, ctl);
+    sanitize ? k_keff_parity_fold<true, false><<<gn, b, 0, st>>>(s, x, y, ctl, nullptr, 0u, 0u)
+             : k_keff_parity_fold<false, false><<<gn, b, 0, st>>>(s, x, y, ctl, nullptr, 0u, 0u);
+}
+
+// the PCG loop's K_eff p with the chunk partials of p . Ap over nodes [0, Nown) into pdot: fused into the node fold
+// when the reduction chunk is 256 DOFs (every workgroup then owns three whole chunks), a separate pass otherwise
+void parity_keff_dot(const cwf_hip_system *h, const float *p, float *Ap, const Ctl *ctl, double *pdot, hipStream_t st)
+{
+    const DevSys &s = h->ds;
+    if (h->reduction_block != 256)
+    {
+        parity_keff_ds(s, p, Ap, false, ctl, st);
+        parity_dot_partials_n(3u * s.Nown, (uint32_t)h->reduction_block, p, Ap, nullptr, pdot, nullptr, ctl, st);
+        return;
+    }
+    if (s.N == 0)
+        return;
+    const dim3 ge(grid_for(s.E, kBlock)), gn(grid_for(s.N, kBlock)), b(kBlock);
+    if (s.E)
+    {
+        if (s.iso)
+            k_keff_parity_elem<true, false><<<ge, b, 0, st>>>(s, p, ctl);
+        else
+            k_keff_parity_elem<false, false><<<ge, b, 0, st>>>(s, p, ctl);
+    }
+    k_keff_parity_fold<false, true><<<gn, b, 0, st>>>(s, p, Ap, ctl, pdot, s.Nown, grid_for(3u * s.Nown, 256u));
 }
 
 void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
@@ -1038,9 +1135,14 @@ void parity_alpha(cwf_hip_system *h, const double *p_pap, uint32_t count, hipStr
     k_pcg_alpha<<<1, kFoldThreads, 0, st>>>(h->ctl, p_pap, count);
 }
 
-void parity_update(cwf_hip_system *h, const float *rhs, hipStream_t st)
+void parity_update(cwf_hip_system *h, const float *rhs, double *prr, double *prz, hipStream_t st)
 {
-    k_update<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl);
+    const uint32_t nlim = h->ds.Nown;
+    const bool fused = h->reduction_block == 256;
+    k_update<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl,
+                                                           fused ? prr : nullptr, prz, nlim, grid_for(3u * nlim, 256u));
+    if (!fused)
+        parity_dot_partials_n(3u * nlim, (uint32_t)h->reduction_block, h->r, h->r, h->z, prr, prz, h->ctl, st);
 }
 
 void parity_beta(cwf_hip_system *h, const double *p_rr, const double *p_rz, uint32_t count, hipStream_t st)
@@ -1060,13 +1162,11 @@ void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, h
     const uint32_t chunks = parity_chunk_count(h);
     if (e0)
         (void)hipEventRecord(e0, st);
-    parity_keff(h, h->p, h->Ap, false, h->ctl, st);
+    parity_keff_dot(h, h->p, h->Ap, h->ctl, h->part0, st);  // + the p . Ap chunk partials
     if (e1)
         (void)hipEventRecord(e1, st);
-    parity_dot_partials(h, h->p, h->Ap, nullptr, h->part0, nullptr, h->ctl, st);
     k_pcg_alpha<<<1, kFoldThreads, 0, st>>>(h->ctl, h->part0, chunks);
-    k_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl);
-    parity_dot_partials(h, h->r, h->r, h->z, h->part0, h->part1, h->ctl, st);
+    parity_update(h, rhs, h->part0, h->part1, st);  // + the r . r and r . z chunk partials
     k_pcg_beta<<<1, kFoldThreads, 0, st>>>(h->ctl, h->part0, h->part1, chunks, h->hist);
     k_p_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
 }

@@ -99,6 +99,26 @@ def test_solve_pcg_bitwise_with_history(case):
     assert np.array_equal(h, ref["history"])  # fp64 residual norms bit-comparable
 
 
+def test_solve_pcg_bitwise_with_reduction_block_100():
+    """A reduction chunk other than 256 DOFs (pack_cpu_elements' reduction_block_size): the fused K_eff / update
+    chunk partials give way to the separate dot pass, and the solve stays bit-exact."""
+    import dataclasses
+    case = CASES["jitter"]()
+    D = case.packing.dof_count
+    P = dataclasses.replace(case.packing, reduction_block=100, reduction_partials=(D + 99) // 100)
+    s0, m0 = case.scalars()
+    s = pcg.MatrixFreeSystem.from_packing(P, case.materials, s0, m0, mode=_lib.MODE_PARITY)
+    o = oracle_system(P, case.materials, s0, m0, reduction_block=100)
+    rhs = case.static_rhs()
+    x, r = np.zeros_like(rhs), np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(600, 1e-6), pcg.PcgVectors(x, r)).value()
+    ref = o.solve_pcg(rhs, 600, 1e-6, history=True)
+    assert (t.iterations, t.residual_norm, t.alpha_last) == (ref["telemetry"].iterations,
+                                                             ref["telemetry"].residual_norm, ref["telemetry"].alpha_last)
+    assert_bitwise(x, ref["x"], "x rb100")
+    assert np.array_equal(pcg.residual_history(s), ref["history"])
+
+
 def test_solve_pcg_warm_start_bitwise(case):
     s = gpu_system(case)
     o = oracle_system(case.packing, case.materials, *case.scalars())
