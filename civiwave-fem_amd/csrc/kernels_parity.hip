@@ -632,7 +632,7 @@ __global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__
 // current one, so the fold runs at the add latency instead of one global load round trip per 8 partials (C2:
 // 117-127 us per scalar kernel with a single thread, r03c profile). t0 / t1 are valid in thread 0.
 constexpr int kFoldThreads = 256;
-constexpr uint32_t kFoldBlock = 2048;  // partials per staged block and operand
+constexpr uint32_t kFoldBlock = 4096;  // partials per staged block and operand (one block: C2's 4,030 chunks)
 template <int NC>
 __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict__ p1, uint32_t count, double &t0,
                          double &t1)
@@ -661,50 +661,29 @@ __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict
         }
         else if (threadIdx.x == 0)
         {
-            // batches of 16 partials in two register sets: the next batch's LDS reads are issued before this
-            // batch's dependent adds, and the sets alternate (no register copies)
+            // batches of 16 partials: the batch's LDS reads issue back to back, then its dependent adds
+            // (tools/fold_chain_bench.hip: 4.5 ns per add against 2.8 from registers; a software-pipelined
+            // ping-pong of two batches measured slower, and readlane / global-load chains 2-4x slower)
             const double *v0 = buf[blk & 1u][0], *v1 = buf[blk & 1u][NC - 1];
             const uint32_t n = min(kFoldBlock, count - blk * kFoldBlock);
             constexpr uint32_t W = 16;
-            double qa0[W], qa1[W], qb0[W], qb1[W];
-            const auto rd = [&](double *d0, double *d1, uint32_t at) {
-#pragma unroll
-                for (uint32_t u = 0; u < W; ++u)
-                {
-                    d0[u] = v0[at + u];
-                    if constexpr (NC == 2)
-                        d1[u] = v1[at + u];
-                }
-            };
-            const auto add = [&](const double *d0, const double *d1) {
-#pragma unroll
-                for (uint32_t u = 0; u < W; ++u)
-                {
-                    a0 += d0[u];
-                    if constexpr (NC == 2)
-                        a1 += d1[u];
-                }
-            };
             uint32_t i = 0;
-            if (n >= W)
+            for (; i + W <= n; i += W)
             {
-                rd(qa0, qa1, 0);
-                for (;;)
+                double q0[W], q1[W];
+#pragma unroll
+                for (uint32_t u = 0; u < W; ++u)
                 {
-                    const bool more_b = i + 2u * W <= n;
-                    if (more_b)
-                        rd(qb0, qb1, i + W);
-                    add(qa0, qa1);
-                    i += W;
-                    if (!more_b)
-                        break;
-                    const bool more_a = i + 2u * W <= n;
-                    if (more_a)
-                        rd(qa0, qa1, i + W);
-                    add(qb0, qb1);
-                    i += W;
-                    if (!more_a)
-                        break;
+                    q0[u] = v0[i + u];
+                    if constexpr (NC == 2)
+                        q1[u] = v1[i + u];
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < W; ++u)
+                {
+                    a0 += q0[u];
+                    if constexpr (NC == 2)
+                        a1 += q1[u];
                 }
             }
             for (; i < n; ++i)

@@ -1,0 +1,196 @@
+// Microbenchmark: the latency floor of an ordered fp64 fold (total += partial[c] in chunk order) run by one
+// thread, with its operands in registers, LDS (ds_read_b64 / b128) or global memory (L2-resident).
+// hipcc --offload-arch=gfx950 -O3 -o fold_chain_bench fold_chain_bench.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+constexpr int N = 4096;
+
+__global__ __launch_bounds__(256) void k_regs(const double *p, double *out, int reps)
+{
+    double v[16];
+    for (int u = 0; u < 16; ++u)
+        v[u] = p[u];
+    double a = 0.0;
+    if (threadIdx.x == 0)
+        for (int r = 0; r < N / 16 * reps; ++r)
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                a += v[u];
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_lds(const double *p, double *out, int reps)
+{
+    __shared__ double buf[N];
+    for (int i = threadIdx.x; i < N; i += 256)
+        buf[i] = p[i];
+    __syncthreads();
+    double a = 0.0;
+    if (threadIdx.x == 0)
+        for (int r = 0; r < reps; ++r)
+            for (int i = 0; i < N; i += W)
+            {
+                double q[W];
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    q[u] = buf[i + u];
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    a += q[u];
+            }
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
+// software pipelined: the next W values are loaded while the current W are added
+template <int W>
+__global__ __launch_bounds__(256) void k_lds_pipe(const double *p, double *out, int reps)
+{
+    __shared__ double buf[N + W];
+    for (int i = threadIdx.x; i < N + W; i += 256)
+        buf[i] = i < N ? p[i] : 0.0;
+    __syncthreads();
+    double a = 0.0;
+    if (threadIdx.x == 0)
+        for (int r = 0; r < reps; ++r)
+        {
+            double q[W], n[W];
+#pragma unroll
+            for (int u = 0; u < W; ++u)
+                q[u] = buf[u];
+            for (int i = W; i <= N; i += W)
+            {
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    n[u] = buf[i + u];
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    a += q[u];
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    q[u] = n[u];
+            }
+        }
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void k_glob(const double *p, double *out, int reps)
+{
+    double a = 0.0;
+    if (threadIdx.x == 0)
+        for (int r = 0; r < reps; ++r)
+            for (int i = 0; i < N; i += W)
+            {
+                double q[W];
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    q[u] = p[i + u];
+#pragma unroll
+                for (int u = 0; u < W; ++u)
+                    a += q[u];
+            }
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
+
+// wave-uniform chain: wave 0 loads 64 partials per batch (one coalesced load per lane, PF batches ahead) and
+// every lane adds them in order through readlane (SGPR operands), so no LDS and no divergence
+__device__ __forceinline__ double lane_val(double v, int l)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int PF>
+__global__ __launch_bounds__(256) void k_lane(const double *p, double *out, int reps)
+{
+    double a = 0.0;
+    if (threadIdx.x < 64)
+        for (int r = 0; r < reps; ++r)
+        {
+            double q[PF];
+#pragma unroll
+            for (int b = 0; b < PF; ++b)
+                q[b] = p[64 * b + threadIdx.x];
+            for (int base = 0; base < N; base += 64 * PF)
+            {
+#pragma unroll
+                for (int b = 0; b < PF; ++b)
+                {
+                    const double v = q[b];
+                    const int nb = base + 64 * (b + PF);
+                    q[b] = nb < N ? p[nb + threadIdx.x] : 0.0;
+#pragma unroll
+                    for (int l = 0; l < 64; ++l)
+                        a += lane_val(v, l);
+                }
+            }
+        }
+    if (threadIdx.x == 0)
+        out[blockIdx.x] = a;
+}
+
+template <typename K>
+static void timeit(const char *name, K kern, int threads, const double *p, double *out, int grid = 1)
+{
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int reps : {1, 9})
+    {
+        kern<<<grid, threads>>>(p, out, reps);
+        (void)hipDeviceSynchronize();
+        (void)hipEventRecord(a);
+        for (int k = 0; k < 20; ++k)
+            kern<<<grid, threads>>>(p, out, reps);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, a, b);
+        printf("%-14s g%-5d reps %d: %8.2f us per launch, %6.2f ns per add\n", name, grid, reps, ms * 1e3 / 20,
+               ms * 1e6 / 20 / (double)(N * reps));
+    }
+}
+
+int main()
+{
+    std::vector<double> h(N + 64);
+    for (int i = 0; i < N + 64; ++i)
+        h[i] = 1.0 / (i + 1);
+    double *p, *out;
+    (void)hipMalloc(&p, (N + 64) * sizeof(double));
+    (void)hipMalloc(&out, 8 * 4096);
+    (void)hipMemcpy(p, h.data(), (N + 64) * sizeof(double), hipMemcpyHostToDevice);
+    timeit("regs", k_regs, 256, p, out);
+    timeit("lds W8", k_lds<8>, 256, p, out);
+    timeit("lds W16", k_lds<16>, 256, p, out);
+    timeit("lds W32", k_lds<32>, 256, p, out);
+    timeit("lds_pipe W8", k_lds_pipe<8>, 256, p, out);
+    timeit("lds_pipe W16", k_lds_pipe<16>, 256, p, out);
+    timeit("glob W16", k_glob<16>, 64, p, out);
+    timeit("glob W64", k_glob<64>, 64, p, out);
+    timeit("lane PF4", k_lane<4>, 256, p, out);
+    timeit("lane PF8", k_lane<8>, 256, p, out);
+    timeit("lane PF8", k_lane<8>, 256, p, out, 1024);
+    timeit("lds W16", k_lds<16>, 256, p, out, 1024);
+    h.resize(N);
+    for (int i = 0; i < N; ++i)
+        h[i] = 1.0 / (i + 1);
+    double ref = 0.0;
+    for (int i = 0; i < N; ++i)
+        ref += h[i];
+    double got = 0.0;
+    k_lane<8><<<1, 256>>>(p, out, 1);
+    (void)hipMemcpy(&got, out, 8, hipMemcpyDeviceToHost);
+    printf("lane fold == host sequential fold: %d\n", (int)(got == ref));
+    return 0;
+}
