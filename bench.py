@@ -274,10 +274,12 @@ def main():
     torch.cuda.synchronize()
     barrier()
     total_iters = 0
+    steps_converged = 0
     t0 = time.perf_counter()
     for k in range(args.steps):
         tel = step(t_sim)
         total_iters += tel.pcg.iterations
+        steps_converged += bool(tel.pcg.converged)
         t_sim += case.cfg.time.initial_dt
     torch.cuda.synchronize()
     barrier()
@@ -375,6 +377,9 @@ def main():
                        if world > 1 else "single"},
             "ranks": per_rank if world > 1 else None,
             "pcg_iterations": int(iters_sum),
+            # steps whose PCG met the tolerance (C5's slender slab runs block-Jacobi PCG into max_iterations:
+            # its DOF-updates/s then times capped, unconverged steps; PCG-it/s is the meaningful figure there)
+            "steps_converged": steps_converged,
             "pcg_iterations_per_sec": iters_sum / world / elapsed,
             "dof_updates_per_sec": dofs_sum * args.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -390,6 +395,10 @@ def main():
             "cpu_baseline": cpu,
             "roofline_hbm": hbm,
         }
+        if args.mode == "parity":
+            # the events bracket both PARITY K_eff passes: the element pass and the node fold that also forms
+            # the p . Ap chunk partials (rocprof lists them as two kernels; their averages add up to this)
+            result["roofline"]["kernels_bracketed"] = [kname, "k_keff_parity_fold<false, true>"]
         if args.mode == "parity" and keff_n.value:
             # the element pass computes each tet's fp64 element math once: strain 72, stress 24 (isotropic D),
             # V s_K 1, 4 corner forces x (18 + 3 scale) = 84, and the node fold adds 3 per incidence (12 per tet):
