@@ -112,47 +112,44 @@ def cpu_baseline(case, sK, sM, iters):
                                "converged": bool(o1["telemetry"].converged)})
 
 
-def hbm_roofline(L, device, key="c3", iters=200, sample=5):
+def hbm_roofline(L, device, key="c3", steps=2, sample=5):
     """The same PCG-mode K_eff kernel, live, on the configs[2] block (C2's working set sits in
-    the 256 MB MALL, so its roofline is not an HBM figure; C3 moves 0.38 GB per launch). A FAST solve of
-    `iters` iterations from x = 0 on the static load, every `sample`-th launch hipEvent-timed (as in the
-    Newmark steps; coprime with the lazy-x period) on the handle's stream;
-    two untimed warm-up solves come first. Outside the timed Newmark steps, so it changes no other field."""
+    the 256 MB MALL, so its roofline is not an HBM figure; C3 moves 0.38 GB per launch): `steps` FAST Newmark
+    steps of C3 after one untimed step, every `sample`-th K_eff launch hipEvent-timed on the handle's stream
+    exactly as in the main timed steps (coprime with the lazy-x period). Round 2 timed a 200-iteration solve
+    from x = 0 instead, which read ~10% above rocprofv3's average of the same kernel (109 vs 98 us); a C3
+    Newmark step's launches read within 1% of it. Outside the timed Newmark steps, so it changes no other field."""
     import ctypes as C
 
-    import numpy as np
-
-    from cwf import _lib, pcg, scenarios
+    from cwf import _lib, scenarios
+    from cwf.stepper import Stepper
 
     case = scenarios.config_case(key)
     P = case.packing
-    sK, sM = case.scalars()
-    sysm = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=_lib.MODE_FAST, device=device)
-    rhs = case.static_rhs()
-    h = sysm.handle()
-    out = None
-    # two untimed solves first: the second makes the handle's last two iteration counts agree, so the timed
-    # solve is enqueued as one long first batch (no control-block read-backs between the timed launches)
-    for timed in (False, False, True):
-        x = np.zeros(P.dof_count, np.float32)
-        r = np.zeros(P.dof_count, np.float32)
-        L.cwf_hip_system_set_timing(h, sample if timed else 0)
-        res = pcg.solve_pcg(sysm, rhs, pcg.PcgSettings(iters, 1e-12, False), pcg.PcgVectors(x, r))
-        if not res.has_value():
-            raise SystemExit(f"hbm roofline solve failed: {res.error()}")
-        if timed:
-            ms, n = C.c_double(), C.c_uint64()
-            L.cwf_hip_system_timing(h, C.byref(ms), C.byref(n))
-            lay_b, ref_b = C.c_uint64(), C.c_uint64()
-            L.cwf_hip_system_keff_traffic(h, C.byref(lay_b), C.byref(ref_b))
-            avg = ms.value / max(1, n.value)
-            ach = lay_b.value / (avg * 1e-3) / 1e9
-            out = {"bound": "hbm", "workload": case.name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": ach / HBM_PEAK_GBS, "kernel": (L.cwf_hip_system_keff_kernel(h) or b"").decode(),
-                   "avg_launch_ms": avg, "launches": int(n.value), "algorithmic_bytes_per_launch": float(lay_b.value),
-                   "reference_layout_equiv_gbs": ref_b.value / (avg * 1e-3) / 1e9}
+    st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST,
+                 device=device)
+    h = st.system.handle()
+    t = 0.0
+    st.step(t).value()
+    t += case.cfg.time.initial_dt
+    L.cwf_hip_system_set_timing(h, sample)
+    for _ in range(steps):
+        st.step(t).value()
+        t += case.cfg.time.initial_dt
+    ms, n = C.c_double(), C.c_uint64()
+    L.cwf_hip_system_timing(h, C.byref(ms), C.byref(n))
     L.cwf_hip_system_set_timing(h, 0)
-    sysm.close()
+    lay_b, ref_b = C.c_uint64(), C.c_uint64()
+    L.cwf_hip_system_keff_traffic(h, C.byref(lay_b), C.byref(ref_b))
+    avg = ms.value / max(1, n.value)
+    ach = lay_b.value / (avg * 1e-3) / 1e9
+    out = {"bound": "hbm", "workload": case.name + f" ({steps} FAST Newmark steps after 1 untimed)",
+           "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+           "kernel": (L.cwf_hip_system_keff_kernel(h) or b"").decode(), "avg_launch_ms": avg,
+           "launches": int(n.value), "algorithmic_bytes_per_launch": float(lay_b.value),
+           "reference_layout_equiv_gbs": ref_b.value / (avg * 1e-3) / 1e9}
+    st.close()
+    st.system.close()
     return out
 
 

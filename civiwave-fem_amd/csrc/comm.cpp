@@ -49,14 +49,24 @@ const Rccl *rccl(std::string *why)
     if (!tried)
     {
         tried = true;
-        void *lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // the process's RCCL (torch's), if any
-        if (!lib)
-            lib = dlopen("librccl.so.1", RTLD_NOW);
-        if (!lib)
-            lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
-        if (!lib)
-            err = std::string("dlopen librccl.so.1 failed: ") + dlerror();
+        void *lib = nullptr;
+        if (const char *alt = knob("CWF_RCCL_LIB"))  // a test transport with the same entry points
+        {
+            lib = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+            if (!lib)
+                err = std::string("dlopen ") + alt + " failed: " + dlerror();
+        }
         else
+        {
+            lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // the process's RCCL (torch's), if any
+            if (!lib)
+                lib = dlopen("librccl.so.1", RTLD_NOW);
+            if (!lib)
+                lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+            if (!lib)
+                err = std::string("dlopen librccl.so.1 failed: ") + dlerror();
+        }
+        if (lib)
         {
             bool ok = true;
             auto sym = [&](auto &fn, const char *name) {

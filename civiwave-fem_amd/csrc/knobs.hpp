@@ -30,6 +30,9 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
+    // multi-GPU (comm.cpp)
+    {"CWF_RCCL_LIB", "path: load this NCCL-API library instead of librccl (tests/transport: the host-staged "
+                     "test transport that runs several ranks on one GPU, where RCCL refuses duplicate devices)"},
     // diagnostics
     {"CWF_TIMED_PCG", "bits: cwf_hip_keff_timed times the PCG-mode tiles kernel dry (tools/ablate.py)"},
     {"CWF_VERBOSE", "1: print the tiling statistics at create"},
