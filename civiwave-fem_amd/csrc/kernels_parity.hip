@@ -637,66 +637,83 @@ template <int NC>
 __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict__ p1, uint32_t count, double &t0,
                          double &t1)
 {
-    __shared__ double buf[2][NC][kFoldBlock];
+    // W partials per register set, two sets alternating (ping-pong); a staged block is padded with +0.0 to a
+    // multiple of 2W (a sequential sum from +0.0 is never -0.0, so adding +0.0 is exact) plus W readable slots
+    // for the last set's (unused) prefetch, so the chain runs branch-free. Two operands (NC = 2) are two
+    // independent chains, run by thread 0 (operand 0) and thread 64 (operand 1) in different waves: interleaved
+    // in one thread they measured no faster than back to back (C2 beta 39 us; a ping-pong of both 42-45).
+    constexpr uint32_t W = 16, kRow = kFoldBlock + W;
+    constexpr uint32_t kStage = NC == 2 ? 128u : 64u;  // the first thread of the staging waves
+    __shared__ double2 buf[2][NC][kRow / 2];
+    __shared__ double other;
     const uint32_t nb = (count + kFoldBlock - 1u) / kFoldBlock;
     const auto stage = [&](uint32_t blk, uint32_t first, uint32_t step) {
         const uint32_t b0 = blk * kFoldBlock, n = min(kFoldBlock, count - b0);
-        for (uint32_t i = first; i < n; i += step)
+        const uint32_t npad = (n + 2u * W - 1u) / (2u * W) * (2u * W);
+        double *d0 = reinterpret_cast<double *>(buf[blk & 1u][0]);
+        double *d1 = reinterpret_cast<double *>(buf[blk & 1u][NC - 1]);
+        for (uint32_t i = first; i < npad; i += step)
         {
-            buf[blk & 1u][0][i] = p0[b0 + i];
+            d0[i] = i < n ? p0[b0 + i] : 0.0;
             if constexpr (NC == 2)
-                buf[blk & 1u][NC - 1][i] = p1[b0 + i];
+                d1[i] = i < n ? p1[b0 + i] : 0.0;
         }
     };
-    double a0 = 0.0, a1 = 0.0;
+    // one chain over a padded block: the next set's 16-B LDS reads issue before the current set's dependent adds
+    // (tools/fold_chain_bench.hip: 4.2 ns per add; one set of reads then its adds 4.5, the operands in registers
+    // 2.8 (the v_add_f64 latency), readlane / global-load chains 2-4x slower)
+    const auto chain = [](const double2 *v, uint32_t npad, double &acc) {
+        constexpr uint32_t H = W / 2;
+        double2 A[H], B[H];
+#pragma unroll
+        for (uint32_t u = 0; u < H; ++u)
+            A[u] = v[u];
+        for (uint32_t i = 0; i < npad; i += 2u * W)
+        {
+#pragma unroll
+            for (uint32_t u = 0; u < H; ++u)
+                B[u] = v[(i + W) / 2u + u];
+#pragma unroll
+            for (uint32_t u = 0; u < H; ++u)
+            {
+                acc += A[u].x;
+                acc += A[u].y;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < H; ++u)
+                A[u] = v[(i + 2u * W) / 2u + u];  // the block's tail reads the W spare slots past npad (unused)
+#pragma unroll
+            for (uint32_t u = 0; u < H; ++u)
+            {
+                acc += B[u].x;
+                acc += B[u].y;
+            }
+        }
+    };
+    double acc = 0.0;
     if (nb)
         stage(0, threadIdx.x, kFoldThreads);
     __syncthreads();
     for (uint32_t blk = 0; blk < nb; ++blk)
     {
-        if (threadIdx.x >= 64u)  // waves 1.. stage; wave 0 is thread 0's alone (no divergent staging before it)
+        const uint32_t n = min(kFoldBlock, count - blk * kFoldBlock);
+        const uint32_t npad = (n + 2u * W - 1u) / (2u * W) * (2u * W);
+        if (threadIdx.x >= kStage)  // the staging waves; the folding threads' waves do nothing else
         {
             if (blk + 1u < nb)
-                stage(blk + 1u, threadIdx.x - 64u, kFoldThreads - 64u);
+                stage(blk + 1u, threadIdx.x - kStage, kFoldThreads - kStage);
         }
         else if (threadIdx.x == 0)
-        {
-            // batches of 16 partials: the batch's LDS reads issue back to back, then its dependent adds
-            // (tools/fold_chain_bench.hip: 4.5 ns per add against 2.8 from registers; a software-pipelined
-            // ping-pong of two batches measured slower, and readlane / global-load chains 2-4x slower)
-            const double *v0 = buf[blk & 1u][0], *v1 = buf[blk & 1u][NC - 1];
-            const uint32_t n = min(kFoldBlock, count - blk * kFoldBlock);
-            constexpr uint32_t W = 16;
-            uint32_t i = 0;
-            for (; i + W <= n; i += W)
-            {
-                double q0[W], q1[W];
-#pragma unroll
-                for (uint32_t u = 0; u < W; ++u)
-                {
-                    q0[u] = v0[i + u];
-                    if constexpr (NC == 2)
-                        q1[u] = v1[i + u];
-                }
-#pragma unroll
-                for (uint32_t u = 0; u < W; ++u)
-                {
-                    a0 += q0[u];
-                    if constexpr (NC == 2)
-                        a1 += q1[u];
-                }
-            }
-            for (; i < n; ++i)
-            {
-                a0 += v0[i];
-                if constexpr (NC == 2)
-                    a1 += v1[i];
-            }
-        }
+            chain(buf[blk & 1u][0], npad, acc);
+        else if (NC == 2 && threadIdx.x == 64)
+            chain(buf[blk & 1u][NC - 1], npad, acc);
         __syncthreads();
     }
-    t0 = a0;
-    t1 = a1;
+    if (NC == 2 && threadIdx.x == 64)
+        other = acc;
+    __syncthreads();
+    t0 = acc;
+    t1 = NC == 2 ? other : 0.0;
 }
 
 __global__ __launch_bounds__(kFoldThreads) void k_fold1(const double *__restrict__ p, uint32_t count,

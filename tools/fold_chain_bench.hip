@@ -139,6 +139,79 @@ __global__ __launch_bounds__(256) void k_lane(const double *p, double *out, int 
         out[blockIdx.x] = a;
 }
 
+// ping-pong: two register sets of W doubles (read as W/2 16-B LDS reads); the next set's reads are issued before
+// the current set's dependent adds, so the adds wait only for reads issued a batch earlier
+template <int W>
+__global__ __launch_bounds__(256) void k_lds_pp(const double *p, double *out, int reps)
+{
+    __shared__ double2 buf[(N + 2 * W) / 2];
+    double *b = reinterpret_cast<double *>(buf);
+    for (int i = threadIdx.x; i < N + 2 * W; i += 256)
+        b[i] = i < N ? p[i] : 0.0;
+    __syncthreads();
+    double a = 0.0;
+    if (threadIdx.x == 0)
+        for (int r = 0; r < reps; ++r)
+        {
+            double2 A[W / 2], B[W / 2];
+#pragma unroll
+            for (int u = 0; u < W / 2; ++u)
+                A[u] = buf[u];
+            for (int i = 0; i < N; i += 2 * W)
+            {
+#pragma unroll
+                for (int u = 0; u < W / 2; ++u)
+                    B[u] = buf[(i + W) / 2 + u];
+#pragma unroll
+                for (int u = 0; u < W / 2; ++u)
+                {
+                    a += A[u].x;
+                    a += A[u].y;
+                }
+#pragma unroll
+                for (int u = 0; u < W / 2; ++u)
+                    A[u] = buf[(i + 2 * W) / 2 + u];
+#pragma unroll
+                for (int u = 0; u < W / 2; ++u)
+                {
+                    a += B[u].x;
+                    a += B[u].y;
+                }
+            }
+        }
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
+// plain batches read as 16-B LDS reads
+template <int W>
+__global__ __launch_bounds__(256) void k_lds128(const double *p, double *out, int reps)
+{
+    __shared__ double2 buf[N / 2];
+    double *b = reinterpret_cast<double *>(buf);
+    for (int i = threadIdx.x; i < N; i += 256)
+        b[i] = p[i];
+    __syncthreads();
+    double a = 0.0;
+    if (threadIdx.x == 0)
+        for (int r = 0; r < reps; ++r)
+            for (int i = 0; i < N / 2; i += W / 2)
+            {
+                double2 q[W / 2];
+#pragma unroll
+                for (int u = 0; u < W / 2; ++u)
+                    q[u] = buf[i + u];
+#pragma unroll
+                for (int u = 0; u < W / 2; ++u)
+                {
+                    a += q[u].x;
+                    a += q[u].y;
+                }
+            }
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
 template <typename K>
 static void timeit(const char *name, K kern, int threads, const double *p, double *out, int grid = 1)
 {
@@ -178,6 +251,11 @@ int main()
     timeit("lds_pipe W16", k_lds_pipe<16>, 256, p, out);
     timeit("glob W16", k_glob<16>, 64, p, out);
     timeit("glob W64", k_glob<64>, 64, p, out);
+    timeit("lds_pp W8", k_lds_pp<8>, 256, p, out);
+    timeit("lds_pp W16", k_lds_pp<16>, 256, p, out);
+    timeit("lds_pp W24", k_lds_pp<24>, 256, p, out);
+    timeit("lds128 W16", k_lds128<16>, 256, p, out);
+    timeit("lds128 W32", k_lds128<32>, 256, p, out);
     timeit("lane PF4", k_lane<4>, 256, p, out);
     timeit("lane PF8", k_lane<8>, 256, p, out);
     timeit("lane PF8", k_lane<8>, 256, p, out, 1024);
@@ -192,5 +270,8 @@ int main()
     k_lane<8><<<1, 256>>>(p, out, 1);
     (void)hipMemcpy(&got, out, 8, hipMemcpyDeviceToHost);
     printf("lane fold == host sequential fold: %d\n", (int)(got == ref));
+    k_lds_pp<16><<<1, 256>>>(p, out, 1);
+    (void)hipMemcpy(&got, out, 8, hipMemcpyDeviceToHost);
+    printf("lds_pp fold == host sequential fold: %d\n", (int)(got == ref));
     return 0;
 }
