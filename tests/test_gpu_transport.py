@@ -10,6 +10,8 @@ cwf_hip_solve_pcg with its grouped all-gathers and halo send/recv.
   bit for bit (the SURVEY 8e gate across processes).
 - FAST: bitwise equal to the same decomposition solved in one process over the LOCAL communicator (same
   kernels, same rank-order folds; only the transport differs), and within 1e-4 of the oracle solution.
+- PARITY Newmark steps (the bench's Stepper over a shard, Rayleigh beta_R != 0): u, v, a and every step's
+  telemetry equal the one-handle Stepper bit for bit.
 """
 import multiprocessing as mp
 import os
@@ -42,7 +44,7 @@ def _uid() -> bytes:
     return d + b"\0" * (_lib.COMM_ID_BYTES - len(d))
 
 
-def _run(spec, nranks, transport):
+def _run(spec, nranks, transport, target="run_rank"):
     import transport_worker
 
     ctx = mp.get_context("spawn")
@@ -51,7 +53,8 @@ def _run(spec, nranks, transport):
     old = os.environ.get("CWF_RCCL_LIB")
     os.environ["CWF_RCCL_LIB"] = transport  # inherited by the spawned ranks only when set before start()
     try:
-        procs = [ctx.Process(target=transport_worker.run_rank, args=(k, nranks, uid, spec, q)) for k in range(nranks)]
+        fn = getattr(transport_worker, target)
+        procs = [ctx.Process(target=fn, args=(k, nranks, uid, spec, q)) for k in range(nranks)]
         for p in procs:
             p.start()
         out = {}
@@ -136,3 +139,34 @@ def test_multiprocess_fast_solve_equals_local_communicator(transport, nranks):
     ref = oracle_system(P, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 800, 1e-6)
     assert tl.converged
     assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+
+
+def test_multiprocess_parity_newmark_steps_bitwise_equal_single_handle(transport):
+    """Three PARITY Newmark steps (Rayleigh beta_R != 0, so the damping K_eff product runs on the shards too) on
+    2 processes: u, v, a and every step's PCG telemetry equal the one-handle Stepper's bit for bit."""
+    from cwf.stepper import Stepper
+
+    spec = dict(block=(10, 6, 12), tol=1e-6, max_iterations=800, rayleigh=True, steps=3)
+    import transport_worker
+
+    glob = transport_worker.case_for(spec)
+    P = glob.packing
+    spec["ranges"] = [int(v) for v in shard.slab_ranges(P.node_count, 2, align=256)]
+    out = _run(spec, 2, transport, target="run_rank_stepper")
+    st = Stepper(P, glob.materials, glob.rayleigh, glob.cfg.solver, glob.cfg.time)
+    ref_tel = []
+    t = 0.0
+    for _ in range(spec["steps"]):
+        tel = st.step(t).value()
+        ref_tel.append((tel.pcg.iterations, tel.pcg.converged, tel.pcg.residual_norm))
+        t += glob.cfg.time.initial_dt
+    assert abs(glob.rayleigh.beta) > 0
+    for d in out.values():
+        assert d["telemetry"] == ref_tel
+    for key, which in (("u", Stepper.DISPLACEMENT), ("v", Stepper.VELOCITY), ("a", Stepper.ACCELERATION)):
+        ref = st.get_state(which)
+        got = np.zeros((P.node_count, 3), np.float32)
+        for d in out.values():
+            got[d["nodes"]] = d[key].reshape(-1, 3)
+        assert_bitwise(got.reshape(-1), ref, f"multi-process PARITY Stepper {key}")
+    st.close()
