@@ -692,7 +692,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
         if (MODE == 1 && !ablate(pa, 4u) && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
         {
             const float p0 = sp[i], p1 = sp[ms + i], p2 = sp[2 * ms + i];
-            pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+            pap += (double)fmaf(p2, a2, fmaf(p1, a1, p0 * a0));  // fp32 per node, fp64 across nodes
             if (tn.x & 0x80000000u)  // the node's owner slot adds its mass term m s_M |p|^2 once
             {
                 const float m = s.mass[tn.x & 0x7fffffffu] * sM;
@@ -955,7 +955,7 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
                 o[2] = a2;
             }
             if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
-                pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+                pap += (double)fmaf(p2, a2, fmaf(p1, a1, p0 * a0));  // fp32 per node, fp64 across nodes
         }
         __syncthreads();  // LDS is refilled by the next tile
         hd = hdn;
@@ -1330,7 +1330,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
                 if (!ablate(pa, 512u))
                     store3(T.part, whole_rsrc(T.part), slot_own[k], a0, a1, a2, T.wt_part != 0);
                 if (MODE == 1 && (tn.x & 0x7fffffffu) < s.Nown)  // ghosts: another rank's row
-                    pap += (double)p0 * (double)a0 + (double)p1 * (double)a1 + (double)p2 * (double)a2;
+                    pap += (double)fmaf(p2, a2, fmaf(p1, a1, p0 * a0));  // fp32 per node, fp64 across nodes
             }
         }
         __syncthreads();  // LDS is refilled by the next tile
