@@ -212,6 +212,38 @@ __global__ __launch_bounds__(256) void k_lds128(const double *p, double *out, in
         out[0] = a;
 }
 
+// the chain with wave 0's lanes all active on uniform addresses: the compiler turns the loads into scalar
+// loads (SGPR operands of v_add_f64), one set of W requested ahead of the current set's adds
+template <int W>
+__global__ __launch_bounds__(64) void k_sgpr2(const double *__restrict__ p, double *out, int reps)
+{
+    double a = 0.0;
+    for (int r = 0; r < reps; ++r)
+    {
+        double A[W], B[W];
+#pragma unroll
+        for (int u = 0; u < W; ++u)
+            A[u] = p[u];
+        for (int i = 0; i < N; i += 2 * W)
+        {
+#pragma unroll
+            for (int u = 0; u < W; ++u)
+                B[u] = p[i + W + u];
+#pragma unroll
+            for (int u = 0; u < W; ++u)
+                a += A[u];
+#pragma unroll
+            for (int u = 0; u < W; ++u)
+                A[u] = p[i + 2 * W + u];
+#pragma unroll
+            for (int u = 0; u < W; ++u)
+                a += B[u];
+        }
+    }
+    if (threadIdx.x == 0)
+        out[0] = a;
+}
+
 template <typename K>
 static void timeit(const char *name, K kern, int threads, const double *p, double *out, int grid = 1)
 {
@@ -236,13 +268,13 @@ static void timeit(const char *name, K kern, int threads, const double *p, doubl
 
 int main()
 {
-    std::vector<double> h(N + 64);
-    for (int i = 0; i < N + 64; ++i)
+    std::vector<double> h(N + 128);
+    for (int i = 0; i < N + 128; ++i)
         h[i] = 1.0 / (i + 1);
     double *p, *out;
-    (void)hipMalloc(&p, (N + 64) * sizeof(double));
+    (void)hipMalloc(&p, (N + 128) * sizeof(double));
     (void)hipMalloc(&out, 8 * 4096);
-    (void)hipMemcpy(p, h.data(), (N + 64) * sizeof(double), hipMemcpyHostToDevice);
+    (void)hipMemcpy(p, h.data(), (N + 128) * sizeof(double), hipMemcpyHostToDevice);
     timeit("regs", k_regs, 256, p, out);
     timeit("lds W8", k_lds<8>, 256, p, out);
     timeit("lds W16", k_lds<16>, 256, p, out);
@@ -256,6 +288,9 @@ int main()
     timeit("lds_pp W24", k_lds_pp<24>, 256, p, out);
     timeit("lds128 W16", k_lds128<16>, 256, p, out);
     timeit("lds128 W32", k_lds128<32>, 256, p, out);
+    timeit("sgpr2 W8", k_sgpr2<8>, 64, p, out);
+    timeit("sgpr2 W16", k_sgpr2<16>, 64, p, out);
+    timeit("sgpr2 W24", k_sgpr2<24>, 64, p, out);
     timeit("lane PF4", k_lane<4>, 256, p, out);
     timeit("lane PF8", k_lane<8>, 256, p, out);
     timeit("lane PF8", k_lane<8>, 256, p, out, 1024);
@@ -273,5 +308,8 @@ int main()
     k_lds_pp<16><<<1, 256>>>(p, out, 1);
     (void)hipMemcpy(&got, out, 8, hipMemcpyDeviceToHost);
     printf("lds_pp fold == host sequential fold: %d\n", (int)(got == ref));
+    k_sgpr2<16><<<1, 64>>>(p, out, 1);
+    (void)hipMemcpy(&got, out, 8, hipMemcpyDeviceToHost);
+    printf("sgpr2 fold == host sequential fold: %d\n", (int)(got == ref));
     return 0;
 }
