@@ -4,7 +4,7 @@ C2 = configs[1] (69^3 hex block -> 1,971,054 Kuhn tets, 1.03M DOF): PARITY is bi
 pinned oracle at full size: apply_keff, the block-Jacobi inverse, and 25 PCG iterations (x, r, the fp64
 residual history, the max-iterations stop).
 C3 = configs[2] (149^3 -> 19.8M tets, 10.1M DOF, Rayleigh): PARITY apply_keff bit-exact against the
-oracle over the whole vector, plus size-independent properties of the FAST path: symmetry of the
+oracle over the whole vector, 8 PARITY PCG iterations bit-exact (multi-block scalar folds), plus size-independent properties of the FAST path: symmetry of the
 constrained operator, rigid translation in the interior, FAST within 2e-5 of PARITY (relative to the
 operator scale), and a FAST Newmark step that converges with the PARITY step's iteration count +-15%.
 """
@@ -57,6 +57,26 @@ def test_c2_parity_pcg_25_iterations_bitwise(c2):
     assert (t.residual_norm, t.alpha_last, t.beta_last) == (rt.residual_norm, rt.alpha_last, rt.beta_last)
     assert_bitwise(x, ref["x"], "C2 x")
     assert_bitwise(r, ref["r"], "C2 r")
+    assert np.array_equal(pcg.residual_history(s), ref["history"])
+    s.close()
+
+
+@pytest.mark.timeout(900)
+def test_c3_parity_pcg_8_iterations_bitwise(c3):
+    """C3's 39,551 reduction chunks span ten 4,096-partial blocks of the ordered scalar folds (C2's 4,020 fit in
+    one), so this pins the multi-block fold (waves 1-3 staging the next block while thread 0 folds) and the
+    fused chunk partials at 10M DOF: x, r and the fp64 history bit-exact after 8 iterations."""
+    s = _system(c3, _lib.MODE_PARITY)
+    o = oracle_system(c3.packing, c3.materials, *c3.scalars())
+    rhs = c3.static_rhs()
+    x, r = np.zeros_like(rhs), np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(8, 1e-12), pcg.PcgVectors(x, r)).value()
+    ref = o.solve_pcg(rhs, 8, 1e-12, history=True)
+    rt = ref["telemetry"]
+    assert (t.iterations, t.converged) == (rt.iterations, bool(rt.converged)) == (8, False)
+    assert (t.residual_norm, t.alpha_last, t.beta_last) == (rt.residual_norm, rt.alpha_last, rt.beta_last)
+    assert_bitwise(x, ref["x"], "C3 x")
+    assert_bitwise(r, ref["r"], "C3 r")
     assert np.array_equal(pcg.residual_history(s), ref["history"])
     s.close()
 
