@@ -381,6 +381,15 @@ public:
     {
         return cwf_hip_stepper_set_external_force(st_, f.data(), f.size(), CWF_PTR_HOST) == 0;
     }
+    // one curve-scaled point-load pattern on the device: after set_load_pattern(base, pattern), each
+    // set_load_scale(evaluate_curve(curve, t)) writes external_force = safe_cast(base + c * pattern), bitwise
+    // what assemble_load_vector packs at t (loads.cpp:63-172), without the host round trip of set_external_force
+    bool set_load_pattern(std::span<const double> base, std::span<const double> pattern)
+    {
+        return base.size() == pattern.size() &&
+               cwf_hip_stepper_set_load_pattern(st_, base.data(), pattern.data(), base.size()) == 0;
+    }
+    bool set_load_scale(double scale) { return cwf_hip_stepper_set_load_scale(st_, scale) == 0; }
     [[nodiscard]] auto dof_count() const noexcept -> std::size_t { return dofs_; }
 
 private:

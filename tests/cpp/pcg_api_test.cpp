@@ -84,6 +84,14 @@ int main()
     EXPECT(g9(u[11]) == "-7.85199674e-08");  // from rest: u = u_pred + x = x
     auto s2 = stepper.step(stepper.current_time(), true);
     EXPECT(s2.has_value() && s2->paused_mode && s2->applied_tolerance == 1.0e-5);
+    // the device-side load rewrite: external_force = f32(base + c * pattern)
+    std::vector<double> base(12, 0.0), pattern(12, 0.0);
+    base[2] = -9.81;
+    pattern[11] = -500.0;
+    EXPECT(stepper.set_load_pattern(base, pattern) && stepper.set_load_scale(0.5));
+    std::vector<float> fe(12);
+    EXPECT(stepper.state(4, fe));
+    EXPECT(fe[2] == (float)-9.81 && fe[11] == -250.0f && fe[0] == 0.0f);
 
     // two-entry breadcrumbs come back as two entries (pcg.cpp:566-570, 609-613), so a caller rebuilds a
     // PcgError equal to the reference's
