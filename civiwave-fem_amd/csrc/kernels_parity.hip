@@ -11,6 +11,7 @@
 #include "cwf_internal.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace cwf
 {
@@ -228,39 +229,47 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_elem(DevSys s, const flo
 }
 
 // A 256-thread workgroup of consecutive nodes covers 768 DOFs = three whole 256-DOF reduction chunks (workgroup b:
-// chunks 3b .. 3b + 2), so the node kernels that produce a dot's operands also produce its chunk partials: the
-// operands of the workgroup's DOFs are staged in LDS (chunk k at row 257 k, against bank conflicts) and lanes
-// 0..2 fold one chunk each, sequentially in DOF order (pcg.cpp:189-199). DOFs of nodes at or past `nlim` (the
-// owned nodes of a shard, or N) are staged as 0, an exact no-op in a fold from +0.0.
+// chunks 3b .. 3b + 2), so the node kernels that produce a dot's operands also produce its chunk partials. Every
+// thread stages the fp64 products of its own DOFs in LDS (chunk k at row 257 k, against bank conflicts); a
+// product of two fp32 values is exact in fp64, so staging (double)a * (double)b is bitwise the term
+// pcg.cpp:189-199 adds. Lanes 0..2 then fold one chunk each, sequentially in DOF order, adds only (the chains
+// are the critical path: staging the fp32 operands and forming the products in the chains measured 22 us for
+// the C2 update pass against 14 us without the partials). DOFs of nodes at or past `nlim` (the owned nodes of
+// a shard, or N) are staged as +0.0, an exact no-op in a fold from +0.0. NV = 2: two dots per DOF, {ab, ac}.
 constexpr int kChunkRow = 257;
 template <int NV>
-__device__ __forceinline__ void wg_chunk_partials(const float *sa, const float *sb, const float *sc, uint32_t chunks,
-                                                  double *pab, double *pac)
+using ChunkTerm = std::conditional_t<NV == 2, double2, double>;
+
+__device__ __forceinline__ uint32_t chunk_slot(uint32_t d)  // LDS index of the workgroup's d-th DOF
+{
+    return (d >> 8) * kChunkRow + (d & 255u);
+}
+
+template <int NV>
+__device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint32_t chunks, double *pab, double *pac)
 {
     if (threadIdx.x >= 3u)
         return;
     const uint32_t k = 3u * blockIdx.x + threadIdx.x;
     if (k >= chunks)
         return;
-    const float *ra = sa + threadIdx.x * kChunkRow, *rb = sb + threadIdx.x * kChunkRow;
-    const float *rc = sc + (NV == 2 ? threadIdx.x * kChunkRow : 0u);
+    const ChunkTerm<NV> *row = st + threadIdx.x * kChunkRow;
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll 16
     for (uint32_t i = 0; i < 256u; ++i)
     {
-        const double av = (double)ra[i];
-        s0 += av * (double)rb[i];
         if constexpr (NV == 2)
-            s1 += av * (double)rc[i];
+        {
+            const double2 t = row[i];
+            s0 += t.x;
+            s1 += t.y;
+        }
+        else
+            s0 += row[i];
     }
     pab[k] = s0;
     if constexpr (NV == 2)
         pac[k] = s1;
-}
-
-__device__ __forceinline__ uint32_t chunk_slot(uint32_t d)  // LDS index of the workgroup's d-th DOF
-{
-    return (d >> 8) * kChunkRow + (d & 255u);
 }
 
 // node pass of the element-centric K_eff: the ascending-element fold of the node's incidence forces, then the
@@ -272,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const flo
                                                              double *__restrict__ pdot, uint32_t nlim,
                                                              uint32_t chunks)
 {
-    __shared__ float sx[DOT ? 3 * kChunkRow : 1], sy[DOT ? 3 * kChunkRow : 1];
+    __shared__ double sxy[DOT ? 3 * kChunkRow : 1];
     if (ctl && !ctl->active)
         return;
     const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
@@ -318,13 +327,9 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const flo
         const bool own = n < nlim;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
-        {
-            const uint32_t l = chunk_slot(3u * threadIdx.x + k);
-            sx[l] = own ? xv[k] : 0.f;
-            sy[l] = own ? yv[k] : 0.f;
-        }
+            sxy[chunk_slot(3u * threadIdx.x + k)] = own ? (double)xv[k] * (double)yv[k] : 0.0;
         __syncthreads();
-        wg_chunk_partials<1>(sx, sy, nullptr, chunks, pdot, nullptr);
+        wg_chunk_partials<1>(sxy, chunks, pdot, nullptr);
     }
 }
 
@@ -908,7 +913,7 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
                                                    const Ctl *__restrict__ ctl, double *__restrict__ prr,
                                                    double *__restrict__ prz, uint32_t nlim, uint32_t chunks)
 {
-    __shared__ float sr[3 * kChunkRow], sz[3 * kChunkRow];
+    __shared__ double2 srz[3 * kChunkRow];
     if (!ctl->active)
         return;
     const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
@@ -943,12 +948,11 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
 #pragma unroll
     for (int k = 0; k < 3; ++k)
     {
-        const uint32_t l = chunk_slot(3u * threadIdx.x + k);
-        sr[l] = own ? rv[k] : 0.f;
-        sz[l] = own ? zv[k] : 0.f;
+        const double r = (double)rv[k];
+        srz[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
     }
     __syncthreads();
-    wg_chunk_partials<2>(sr, sr, sz, chunks, prr, prz);
+    wg_chunk_partials<2>(srz, chunks, prr, prz);
 }
 
 // p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
