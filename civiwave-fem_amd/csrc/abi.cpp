@@ -529,8 +529,32 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     std::vector<float> r_mass;
     std::vector<double> r_coords;
     const char *rn = knob("CWF_RENUMBER");
-    const bool renumber = d->mode == CWF_MODE_FAST && E && N && d->node_coords &&
-                          !(d->reserved & CWF_DESC_KEEP_NODE_ORDER) && !(rn && rn[0] == '0');
+    const bool may_renumber = d->mode == CWF_MODE_FAST && E && N && d->node_coords &&
+                              !(d->reserved & CWF_DESC_KEEP_NODE_ORDER) && !(rn && rn[0] == '0');
+    // structured Kuhn block (lattice.cpp): the FAST operator is the node-pair stencil of the one shared cell
+    // stiffness (k_keff_lattice). Its nodes stay in the caller's order when that is lexicographic within planes
+    // (a shard's local order too); otherwise a handle that may renumber takes the lexicographic order.
+    Lattice lat;
+    bool is_lat = false;
+    {
+        const char *lv = knob("CWF_LATTICE");
+        if (d->mode == CWF_MODE_FAST && !hex && E && N && N < 0x15555555ull && d->node_coords && !(lv && lv[0] == '0'))
+        {
+            std::string why;
+            try
+            {
+                is_lat = detect_lattice(d, may_renumber, lat, &why);
+            }
+            catch (const std::bad_alloc &)
+            {
+                return set_error(nullptr, CWF_ERR_ALLOC, "host allocation failed");
+            }
+            if (knob("CWF_VERBOSE"))
+                fprintf(stderr, "[cwf] lattice: %s (%u x %u x %u nodes%s)\n", is_lat ? "yes" : why.c_str(), lat.nx,
+                        lat.ny, lat.nz, is_lat && !lat.perm.empty() ? ", renumbered" : "");
+        }
+    }
+    const bool renumber = may_renumber && (!is_lat || !lat.perm.empty());
     // FAST recomputes tet geometry from node coordinates when they reproduce the desc's gradients (GEO); only
     // then can the tets group into fans (the groups kernel has no gradient stream). Node renumbering does not
     // change it, so it is decided once, on the caller's desc.
@@ -561,6 +585,13 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         };
         try
         {
+            if (is_lat)  // lexicographic lattice order (lattice.cpp)
+            {
+                r_perm.swap(lat.perm);
+                apply_perm();
+            }
+            else
+            {
             r_perm = morton_node_order(d->node_coords, N);
             apply_perm();
             // fan-group and hex8 meshes: renumber again by (owner tile, Morton) so every tile's owned nodes are one
@@ -613,6 +644,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     apply_perm();
                 }
             }
+            }  // !is_lat
         }
         catch (const std::bad_alloc &)
         {
@@ -803,8 +835,45 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             s.fslots = slots;
         }
     }
+    // structured Kuhn block: the stencil blocks, the plane table and one row value per node (lattice.inc)
+    if (E && is_lat)
+    {
+        DevTiles &t = s.t;
+        std::vector<uint32_t> npo(N + 1);
+        for (uint64_t n = 0; n <= N; ++n)
+            npo[n] = (uint32_t)n | (n < N ? (d->bc_mask[n] & 7u) << 29 : 0u);
+        uint32_t *dpl, *dnpo;
+        float *dcf, *part;
+        if (int st = upload(h, &dpl, lat.plane.data(), lat.plane.size()))
+            return bail(st);
+        if (int st = upload(h, &dcf, lat.coef, (uint64_t)kLatCoef))
+            return bail(st);
+        if (int st = upload(h, &dnpo, npo.data(), npo.size()))
+            return bail(st);
+        if (int st = dalloc(h, &part, 3 * (N + 2)))  // + 2 padding slots (update pass)
+            return bail(st);
+        t.lat = 1;
+        t.lnx = lat.nx;
+        t.lny = lat.ny;
+        t.lnz = lat.nz;
+        t.lk0 = 0;
+        t.lk1 = lat.nz;
+        t.lplane = dpl;
+        t.lcoef = dcf;
+        t.node_part_off = dnpo;
+        t.off_mask = 1;
+        t.node_major = 1;
+        t.part = part;
+        t.E = (uint32_t)E;
+        t.geo = 1;
+        t.total_tile_nodes = (uint32_t)N;
+        const char *wt = knob("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
+        t.wt_part = wt ? (wt[0] == '1') : 0;
+        h->lat_plane.swap(lat.plane);
+        lattice_plan(t);
+    }
     // FAST-mode element tiles (tiles.cpp)
-    if (E)
+    else if (E)
     {
         HostTiles ht;
         DevTiles &t = s.t;
@@ -1298,6 +1367,11 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
+        if (s.t.lat)  // per owned node: z and p_old read, mass read, the new p and the row value written
+        {
+            *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 4 + 12 + 12);
+            return 0;
+        }
         if (s.t.grp)
         {
             *layout_bytes = 16ull * s.t.ntiles + (uint64_t)s.t.ngroups * 16 +
@@ -1320,6 +1394,8 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
         return h->ds.iso ? "k_keff_parity_elem<true, false>" : "k_keff_parity_elem<false, false>";
+    if (t.lat)
+        return "k_keff_lattice<1, false>";
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
     {
         static thread_local char name[96];

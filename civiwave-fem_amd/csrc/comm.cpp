@@ -577,6 +577,20 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         h->recv_off.assign(1, 0);
     }
     h->ds.Nown = (uint32_t)plan->owned_nodes;
+    if (h->ds.t.lat)  // structured block: compute the rows of the planes holding owned nodes only
+    {
+        DevTiles &t = h->ds.t;
+        uint32_t k0 = t.lnz, k1 = 0;
+        for (uint32_t k = 0; k < t.lnz; ++k)
+            if (h->lat_plane[k] < h->ds.Nown)
+            {
+                k0 = std::min(k0, k);
+                k1 = std::max(k1, k + 1);
+            }
+        t.lk0 = k0 < k1 ? k0 : 0;
+        t.lk1 = k0 < k1 ? k1 : 1;
+        lattice_plan(t);
+    }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
     h->owned_contiguous = true;  // PARITY shards fold chunk partials in global order (comm.cpp parity_setup)
     if (plan->node_global)

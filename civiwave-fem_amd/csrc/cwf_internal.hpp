@@ -81,7 +81,17 @@ struct DevTiles
     // MALL (abi.cpp: < 4M tets)
     int wt_part = 0;
     float *part = nullptr;                    // [3*total] tile-node partial sums, node-major (scratch)
+    // structured Kuhn block (lattice.cpp, lattice.inc): k_keff_lattice; part is one row value per node
+    // (node_part_off[n] = n), ntiles = lnwork
+    int lat = 0;
+    uint32_t lnx = 0, lny = 0, lnz = 0;  // lattice nodes per axis (a shard: its local planes)
+    uint32_t lk0 = 0, lk1 = 0;           // planes holding the rows this handle computes (a shard: its owned planes)
+    uint32_t lnbx = 0, lnby = 0, lL = 0, lnwork = 0;  // 32 x 8 column bricks, planes per work item, work items
+    const uint32_t *lplane = nullptr;    // [lnz] storage index of node (0, 0, k)
+    const float *lcoef = nullptr;        // [kLatCoef] stencil blocks, then cell-pair blocks (unscaled by s_K)
 };
+// lattice work items for planes [lk0, lk1) (lattice.cpp): sets lnbx, lnby, lL, lnwork, ntiles
+void lattice_plan(DevTiles &t);
 
 struct HostTiles
 {
@@ -134,6 +144,43 @@ struct GroupTiles
 // order_lanes: bank-aware lane order within each tile (groups.cpp); off where only the tiles' node sets matter
 int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, uint32_t max_nodes,
                       uint32_t slot_budget, bool order_lanes = true);
+
+// Structured Kuhn blocks (lattice.cpp, lattice.inc): the 15 node-pair offsets of a Kuhn node's row (the node,
+// +-x, +-y, +-z, +-(1,1,0), +-(1,0,1), +-(0,1,1), +-(1,1,1)) and the 46 corner pairs (c, c') of one cell that share
+// a tet, with the offset index of c' - c
+constexpr int kLatOffsets = 15, kLatPairs = 46;
+constexpr int kLatOff[kLatOffsets][3] = {{0, 0, 0},  {1, 0, 0},  {-1, 0, 0},  {0, 1, 0},   {0, -1, 0},
+                                         {0, 0, 1},  {0, 0, -1}, {1, 1, 0},   {-1, -1, 0}, {1, 0, 1},
+                                         {-1, 0, -1}, {0, 1, 1}, {0, -1, -1}, {1, 1, 1},   {-1, -1, -1}};
+constexpr int kLatPair[kLatPairs][2] = {
+    {0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 5}, {0, 6}, {0, 7},  // corner 0: every corner
+    {1, 0}, {1, 1}, {1, 3}, {1, 5}, {1, 7},                          //
+    {2, 0}, {2, 2}, {2, 3}, {2, 6}, {2, 7},                          //
+    {3, 0}, {3, 1}, {3, 2}, {3, 3}, {3, 7},                          //
+    {4, 0}, {4, 4}, {4, 5}, {4, 6}, {4, 7},                          //
+    {5, 0}, {5, 1}, {5, 4}, {5, 5}, {5, 7},                          //
+    {6, 0}, {6, 2}, {6, 4}, {6, 6}, {6, 7},                          //
+    {7, 0}, {7, 1}, {7, 2}, {7, 3}, {7, 4}, {7, 5}, {7, 6}, {7, 7}};  // corner 7: every corner
+constexpr int kLatPairOff[kLatPairs] = {0,  1,  3,  7,  5,  9,  11, 13,  // 0 -> 0..7
+                                        2,  0,  3,  5,  11,              // 1 -> 0 1 3 5 7
+                                        4,  0,  1,  5,  9,               // 2 -> 0 2 3 6 7
+                                        8,  4,  2,  0,  5,               // 3 -> 0 1 2 3 7
+                                        6,  0,  1,  3,  7,               // 4 -> 0 4 5 6 7
+                                        10, 6,  2,  0,  3,               // 5 -> 0 1 4 5 7
+                                        12, 6,  4,  0,  1,               // 6 -> 0 2 4 6 7
+                                        14, 12, 10, 6,  8,  4,  2,  0};  // 7 -> 0..7
+constexpr int kLatCoef = 9 * (kLatOffsets + kLatPairs);  // f32: [15][3][3] stencil, then [46][3][3] cell blocks
+
+struct Lattice
+{
+    uint32_t nx = 0, ny = 0, nz = 0;  // nodes per axis
+    std::vector<uint32_t> plane;      // [nz] storage index of node (0, 0, k)
+    std::vector<uint32_t> perm;       // when renumbered: internal (lexicographic) index -> caller's node
+    float coef[kLatCoef] = {};
+};
+// true when the desc is a Kuhn-split box lattice with one gradient / volume set per Kuhn type (lattice.cpp);
+// allow_perm: the handle may renumber (otherwise the nodes must already be lexicographic within planes)
+bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::string *why = nullptr);
 
 constexpr uint32_t kPartOffBits = 0x1fffffffu;  // node_part_off value bits (the rest: bc_mask, off_mask)
 // cap of the first batch of PCG iterations enqueued before the first control-block read-back (abi.cpp: sized from
@@ -233,6 +280,7 @@ struct cwf_hip_system
     double *hist = nullptr;        // device residual history
     uint64_t hist_cap = 0;
     uint64_t hist_count = 0;
+    std::vector<uint32_t> lat_plane;  // structured block: host copy of ds.t.lplane (attach derives the owned planes)
     uint64_t last_iters = 0, prev_iters = 0;  // iterations of the last two solves on this handle (first batch size)
     std::string err, ctx;
     // live K_eff timing (cwf_hip_system_set_timing)

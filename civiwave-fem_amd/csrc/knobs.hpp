@@ -28,6 +28,8 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_PIPE_NT", "128|256: lanes of the per-tet pipelined tiles"},
     {"CWF_HEX_NT", "128|256: lanes of the hex8 tiles (tests/test_hex8.py)"},
     {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
+    {"CWF_LATTICE", "0: no structured-block stencil (lattice.cpp); structured Kuhn blocks then run the fan groups"},
+    {"CWF_LAT_L", "n: planes per lattice work item (default: about 1536 work items)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
     // multi-GPU (comm.cpp)

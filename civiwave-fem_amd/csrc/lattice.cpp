@@ -1,0 +1,337 @@
+// lattice.cpp -- structured-block specialisation of the FAST operator ("structured-block
+// specialisation with a single shared K_e").
+//
+// The reference's operator is the element loop of pcg.cpp:561-662: per tet, f = vol s_K B^T D B u, scattered to
+// its 4 corners. On a Kuhn block (every hex cell split into the 6 tets {0,1,3,7} {0,1,5,7} {0,2,3,7} {0,2,6,7}
+// {0,4,5,7} {0,4,6,7} of its corner bits (i, j, k)) whose tets of one Kuhn type all carry the same gradients and
+// volume, every cell contributes the same 24 x 24 cell stiffness Kc = sum of its 6 K_e (fp64, from the desc's own
+// f32 gradients and volumes, the reference's B / D / vol products), and K u = sum over cells of Kc u_cell. Regrouped
+// by node pair, an interior node's row is 15 3x3 blocks (the Kuhn edges: +-x, +-y, +-z, +-(1,1,0), +-(1,0,1),
+// +-(0,1,1), +-(1,1,1), and the node itself):
+//   (K u)_n = sum_d S_d u_(n+d),  S_d = sum over the cell corners c with c + d a corner of Kc[c][c + d].
+// The kernel (lattice.inc) forms it in difference form, sum_(d != 0) S_d (u_(n+d) - u_n) (rigid translations
+// are in the null space of every row), so each fp32 term is strain-sized as in the element loop. A node on the
+// block's surface misses some of its 8 cells; the kernel subtracts a missing cell's row-c blocks Kc[c][.] (in the
+// same difference form) from the interior row, with positions outside the block clamped to the nearest node (their
+// differences cancel). The regrouping changes the fp32 summation order only (FAST's tolerance contract,
+// tests/test_lattice.py on the CPU, tests/test_gpu_lattice.py).
+//
+// detect_lattice() decides it for a desc: integer lattice coordinates of every node (from the first tet's cell
+// size), a bijection onto an nx * ny * nz lattice, every tet one Kuhn tet of one cell (each of a cell's 6 types
+// exactly once), one material, and every tet's gradients / volume within 1e-6 (relative) of the first tet of its
+// Kuhn type. Storage order: lexicographic (i fastest) inside each k plane, planes anywhere (a shard's local order:
+// owned planes, then its ghost planes; shard.cpp), or, when the handle may renumber, any order (perm).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "cwf_internal.hpp"
+
+namespace cwf
+{
+namespace
+{
+constexpr int kKuhn[6][4] = {{0, 1, 3, 7}, {0, 1, 5, 7}, {0, 2, 3, 7}, {0, 2, 6, 7}, {0, 4, 5, 7}, {0, 4, 6, 7}};
+
+// 6x3 strain-displacement block of one corner (the reference's B rows: xx, yy, zz, xy, yz, zx;
+// pcg.cpp:622-630)
+void b_block(const double g[3], double B[6][3])
+{
+    std::memset(B, 0, sizeof(double) * 18);
+    B[0][0] = g[0];
+    B[1][1] = g[1];
+    B[2][2] = g[2];
+    B[3][0] = g[1];
+    B[3][1] = g[0];
+    B[4][1] = g[2];
+    B[4][2] = g[1];
+    B[5][0] = g[2];
+    B[5][2] = g[0];
+}
+}  // namespace
+
+// kLatPair (cwf_internal.hpp) lists exactly the corner pairs that share a Kuhn tet, in (c, c') order, and
+// kLatPairOff names each pair's offset c' - c
+bool lattice_tables_ok()
+{
+    int q = 0;
+    for (int c = 0; c < 8; ++c)
+        for (int c2 = 0; c2 < 8; ++c2)
+        {
+            bool edge = c == c2;
+            for (int t = 0; t < 6 && !edge; ++t)
+            {
+                bool a = false, b = false;
+                for (int s = 0; s < 4; ++s)
+                {
+                    a |= kKuhn[t][s] == c;
+                    b |= kKuhn[t][s] == c2;
+                }
+                edge = a && b;
+            }
+            if (!edge)
+                continue;
+            if (q >= kLatPairs || kLatPair[q][0] != c || kLatPair[q][1] != c2)
+                return false;
+            const int o = kLatPairOff[q];
+            if (kLatOff[o][0] != (c2 & 1) - (c & 1) || kLatOff[o][1] != ((c2 >> 1) & 1) - ((c >> 1) & 1) ||
+                kLatOff[o][2] != ((c2 >> 2) & 1) - ((c >> 2) & 1))
+                return false;
+            ++q;
+        }
+    return q == kLatPairs;
+}
+
+bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::string *why)
+{
+    const auto fail = [&](const char *m) {
+        if (why)
+            *why = m;
+        return false;
+    };
+    const uint64_t N = d->node_count, E = d->element_count;
+    static const bool tables_ok = lattice_tables_ok();
+    if (!tables_ok)
+        return fail("lattice tables inconsistent");
+    if (!E || N < 8 || !d->node_coords)
+        return fail("no elements or no node coordinates");
+    if (d->element_connectivity[4] != 0xFFFFFFFFu)
+        return fail("hex8 elements");
+    const uint32_t *conn = d->element_connectivity;
+    const double *X = d->node_coords;
+    const uint32_t m0 = d->element_material_index[0];
+    for (uint64_t e = 0; e < E; ++e)
+        if (d->element_material_index[e] != m0)
+            return fail("more than one material");
+    // cell size from the first tet (a Kuhn tet spans its whole cell: it holds corners 0 and 7)
+    double h[3], lo[3];
+    for (int k = 0; k < 3; ++k)
+    {
+        double a = X[3ull * conn[0] + k], b = a;
+        for (int s = 1; s < 4; ++s)
+        {
+            a = std::min(a, X[3ull * conn[s] + k]);
+            b = std::max(b, X[3ull * conn[s] + k]);
+        }
+        h[k] = b - a;
+        if (!(h[k] > 0.0))
+            return fail("degenerate first element");
+        lo[k] = X[k];
+    }
+    for (uint64_t n = 1; n < N; ++n)
+        for (int k = 0; k < 3; ++k)
+            lo[k] = std::min(lo[k], X[3 * n + k]);
+    std::vector<uint32_t> q(3 * N);
+    uint32_t nn[3] = {0, 0, 0};
+    for (uint64_t n = 0; n < N; ++n)
+        for (int k = 0; k < 3; ++k)
+        {
+            const double f = (X[3 * n + k] - lo[k]) / h[k];
+            const double r = std::nearbyint(f);
+            if (!(std::fabs(f - r) <= 1e-3) || r >= 1048576.0)
+                return fail("nodes off the lattice");
+            q[3 * n + k] = (uint32_t)r;
+            nn[k] = std::max(nn[k], (uint32_t)r + 1u);
+        }
+    if (nn[0] < 2 || nn[1] < 2 || nn[2] < 2 || (uint64_t)nn[0] * nn[1] * nn[2] != N)
+        return fail("nodes do not fill a box lattice");
+    const uint64_t nx = nn[0], ny = nn[1], nz = nn[2];
+    std::vector<uint32_t> at(N, 0xFFFFFFFFu);  // lexicographic lattice index -> node
+    for (uint64_t n = 0; n < N; ++n)
+    {
+        const uint64_t li = ((uint64_t)q[3 * n + 2] * ny + q[3 * n + 1]) * nx + q[3 * n];
+        if (at[li] != 0xFFFFFFFFu)
+            return fail("two nodes on one lattice point");
+        at[li] = (uint32_t)n;
+    }
+    const uint64_t C = (nx - 1) * (ny - 1) * (nz - 1);
+    if (E != 6 * C)
+        return fail("element count is not 6 per cell");
+    // every tet a Kuhn tet of one cell, each of a cell's 6 types once; gradients / volume per type
+    int type_of[256];
+    std::fill(type_of, type_of + 256, -1);
+    for (int t = 0; t < 6; ++t)
+    {
+        int m = 0;
+        for (int s = 0; s < 4; ++s)
+            m |= 1 << kKuhn[t][s];
+        type_of[m] = t;
+    }
+    std::vector<uint8_t> seen(C, 0);
+    double G[6][8][3];
+    double V[6], gmax[6];
+    bool have[6] = {false, false, false, false, false, false};
+    const float *grad = d->element_gradients;
+    for (uint64_t e = 0; e < E; ++e)
+    {
+        uint32_t c[3] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        for (int s = 0; s < 4; ++s)
+            for (int k = 0; k < 3; ++k)
+                c[k] = std::min(c[k], q[3ull * conn[8 * e + s] + k]);
+        int bits[4], m = 0;
+        for (int s = 0; s < 4; ++s)
+        {
+            const uint32_t *qs = &q[3ull * conn[8 * e + s]];
+            const uint32_t ox = qs[0] - c[0], oy = qs[1] - c[1], oz = qs[2] - c[2];
+            if (ox > 1 || oy > 1 || oz > 1)
+                return fail("an element spans more than one cell");
+            bits[s] = (int)(ox | oy << 1 | oz << 2);
+            m |= 1 << bits[s];
+        }
+        const int t = type_of[m];
+        if (t < 0 || c[0] >= nx - 1 || c[1] >= ny - 1 || c[2] >= nz - 1)
+            return fail("an element is not a Kuhn tet of a cell");
+        const uint64_t cell = ((uint64_t)c[2] * (ny - 1) + c[1]) * (nx - 1) + c[0];
+        if (seen[cell] & (1u << t))
+            return fail("a cell holds one Kuhn type twice");
+        seen[cell] |= (uint8_t)(1u << t);
+        const float *g = grad + 24 * e;
+        const double vol = d->element_volume[e];
+        if (!have[t])
+        {
+            have[t] = true;
+            V[t] = vol;
+            gmax[t] = 0.0;
+            for (int s = 0; s < 4; ++s)
+                for (int k = 0; k < 3; ++k)
+                {
+                    G[t][bits[s]][k] = g[3 * s + k];
+                    gmax[t] = std::max(gmax[t], std::fabs((double)g[3 * s + k]));
+                }
+            if (!(V[t] > 0.0) || !(gmax[t] > 0.0))
+                return fail("degenerate element");
+            continue;
+        }
+        if (!(std::fabs(vol - V[t]) <= 1e-6 * V[t]))
+            return fail("element volumes differ within a Kuhn type");
+        for (int s = 0; s < 4; ++s)
+            for (int k = 0; k < 3; ++k)
+                if (!(std::fabs((double)g[3 * s + k] - G[t][bits[s]][k]) <= 1e-6 * gmax[t]))
+                    return fail("element gradients differ within a Kuhn type");
+    }
+    // storage order: lexicographic inside every k plane (caller order), or renumbered
+    L.nx = (uint32_t)nx;
+    L.ny = (uint32_t)ny;
+    L.nz = (uint32_t)nz;
+    L.plane.assign(nz, 0);
+    L.perm.clear();
+    bool caller_order = true;
+    for (uint64_t k = 0; k < nz && caller_order; ++k)
+    {
+        const uint32_t base = at[k * nx * ny];
+        L.plane[k] = base;
+        if ((uint64_t)base + nx * ny > N)
+            caller_order = false;
+        for (uint64_t j = 0; j < ny && caller_order; ++j)
+            for (uint64_t i = 0; i < nx; ++i)
+                if (at[(k * ny + j) * nx + i] != base + j * nx + i)
+                {
+                    caller_order = false;
+                    break;
+                }
+    }
+    if (!caller_order)
+    {
+        if (!allow_perm)
+            return fail("node order is not lexicographic within planes");
+        L.perm = at;
+        for (uint64_t k = 0; k < nz; ++k)
+            L.plane[k] = (uint32_t)(k * nx * ny);
+    }
+    // cell stiffness Kc[c][c'] = sum over the cell's tets of vol B_c^T D B_c' (fp64, pcg.cpp:622-651 products)
+    const double *D = d->material_stiffness + 36ull * m0;
+    double Kc[8][8][3][3];
+    std::memset(Kc, 0, sizeof Kc);
+    for (int t = 0; t < 6; ++t)
+        for (int sa = 0; sa < 4; ++sa)
+            for (int sb = 0; sb < 4; ++sb)
+            {
+                const int a = kKuhn[t][sa], b = kKuhn[t][sb];
+                double Ba[6][3], Bb[6][3];
+                b_block(G[t][a], Ba);
+                b_block(G[t][b], Bb);
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k)
+                    {
+                        double sum = 0.0;
+                        for (int i = 0; i < 6; ++i)
+                            for (int j = 0; j < 6; ++j)
+                                sum += Ba[i][r] * D[6 * i + j] * Bb[j][k];
+                        Kc[a][b][r][k] += V[t] * sum;
+                    }
+            }
+    // interior stencil, offsets in lattice.inc's order; then the cell-pair blocks
+    for (int o = 0; o < kLatOffsets; ++o)
+    {
+        const int dx = kLatOff[o][0], dy = kLatOff[o][1], dz = kLatOff[o][2];
+        double S[3][3] = {};
+        for (int c = 0; c < 8; ++c)
+        {
+            const int cx = (c & 1) + dx, cy = ((c >> 1) & 1) + dy, cz = ((c >> 2) & 1) + dz;
+            if (cx < 0 || cx > 1 || cy < 0 || cy > 1 || cz < 0 || cz > 1)
+                continue;
+            const int c2 = cx | cy << 1 | cz << 2;
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k)
+                    S[r][k] += Kc[c][c2][r][k];
+        }
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k)
+                L.coef[9 * o + 3 * r + k] = (float)S[r][k];
+    }
+    for (int p = 0; p < kLatPairs; ++p)
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k)
+                L.coef[9 * (kLatOffsets + p) + 3 * r + k] = (float)Kc[kLatPair[p][0]][kLatPair[p][1]][r][k];
+    // every block outside the Kuhn pattern is structurally zero (never accumulated): nothing to check
+    return true;
+}
+
+// Work items: 32 x 8 column bricks times L planes, L sized for about kLatTargetItems workgroups (about six
+// resident 256-thread workgroups per CU on 256 CUs) and at least 2 (each item reads L + 2 planes)
+void lattice_plan(DevTiles &t)
+{
+    constexpr uint64_t kLatTargetItems = 1536;
+    t.lnbx = (t.lnx + 31u) / 32u;
+    t.lnby = (t.lny + 7u) / 8u;
+    const uint64_t planes = t.lk1 > t.lk0 ? t.lk1 - t.lk0 : 0u, cols = (uint64_t)t.lnbx * t.lnby;
+    uint64_t L = (planes * cols + kLatTargetItems - 1) / kLatTargetItems;
+    const char *lk = knob("CWF_LAT_L");
+    if (lk && atoi(lk) > 0)
+        L = (uint64_t)atoi(lk);
+    L = std::max<uint64_t>(2, std::min<uint64_t>(L, 64));
+    t.lL = (uint32_t)L;
+    t.lnwork = planes ? (uint32_t)(cols * ((planes + L - 1) / L)) : 0u;
+    t.ntiles = t.lnwork;
+}
+
+}  // namespace cwf
+
+extern "C" int cwf_lattice_describe(const cwf_system_desc *desc, int renumber, uint32_t dims[3], float *coef,
+                                    uint32_t *plane)
+{
+    static_assert(cwf::kLatCoef == CWF_LATTICE_COEFS, "cwf_hip.h CWF_LATTICE_COEFS");
+    if (!desc || !dims || !coef || !desc->element_connectivity || !desc->element_gradients || !desc->element_volume ||
+        !desc->element_material_index || !desc->material_stiffness)
+        return CWF_ERR_ARGUMENT;
+    if (desc->mode != CWF_MODE_FAST || desc->node_count >= 0x15555555ull)  // 12-B rows addressable by 32-bit offsets
+        return 0;
+    for (uint64_t e = 0; e < desc->element_count; ++e)
+    {
+        if (desc->element_material_index[e] >= desc->material_count)
+            return CWF_ERR_MATERIAL_RANGE;
+        for (int a = 0; a < 4; ++a)
+            if (desc->element_connectivity[8 * e + a] >= desc->node_count)
+                return CWF_ERR_NODE_RANGE;
+    }
+    cwf::Lattice L;
+    if (!cwf::detect_lattice(desc, renumber != 0, L))
+        return 0;
+    dims[0] = L.nx;
+    dims[1] = L.ny;
+    dims[2] = L.nz;
+    std::memcpy(coef, L.coef, sizeof L.coef);
+    if (plane)
+        std::memcpy(plane, L.plane.data(), L.plane.size() * sizeof(uint32_t));
+    return 1;
+}

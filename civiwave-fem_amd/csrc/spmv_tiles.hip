@@ -1700,6 +1700,7 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 }
 
 #include "hex8_tiles.inc"
+#include "lattice.inc"
 
 // pipelined kernel: element forces + local CSR + per tile node {x y z v_x}{v_y v_z}
 inline size_t pipe_lds(const DevSys &s)
@@ -1785,6 +1786,11 @@ template <bool ISO, bool SAN, int MODE>
 void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hipStream_t st,
                   hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
+    if (s.t.lat)
+    {
+        launch_lattice<MODE, SAN>(s, x, pa, st, e0, e1);
+        return;
+    }
     if (s.t.grp)
     {
         launch_groups<ISO, SAN, MODE>(s, x, pa, st, e0, e1);
@@ -1814,7 +1820,10 @@ void launch_tiles(const DevSys &s, const float *x, const PcgArgs &pa, int nt, hi
 }
 }  // namespace
 
-unsigned fast_tile_blocks(const DevSys &s) { return (s.t.pipe || s.t.hex) ? s.t.pipe_grid : s.t.ntiles; }
+unsigned fast_tile_blocks(const DevSys &s)
+{
+    return s.t.lat ? s.t.lnwork : (s.t.pipe || s.t.hex) ? s.t.pipe_grid : s.t.ntiles;
+}
 
 unsigned fast_pipe_grid(const DevSys &s)
 {

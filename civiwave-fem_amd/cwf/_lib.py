@@ -133,6 +133,7 @@ def load() -> C.CDLL:
         "cwf_hip_bandwidth_probe": ([i32, u64, i32, P], i32),
         "cwf_hip_system_keff_traffic": ([P, P, P], i32),
         "cwf_hip_system_keff_kernel": ([P], C.c_char_p),
+        "cwf_lattice_describe": ([P, i32, P, P, P], i32),
         "cwf_hip_system_set_timing": ([P, i32], i32),
         "cwf_hip_system_timing": ([P, P, P], i32),
         "cwf_hip_keff_timed": ([P, P, P, i32, P], i32),

@@ -144,9 +144,17 @@ int cwf_hip_bandwidth_probe(int device, uint64_t bytes, int reps, double *gbs);
  * once (the headline roofline uses the build's own layout when it reads less);
  * `reference_layout_bytes` = 32 N + 72 E, the same SpMV over the reference's packed layout. */
 int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes, uint64_t *reference_layout_bytes);
-/* Name of the kernel the handle's K_eff launches in its current mode ("k_keff_groups_pipe",
+/* Name of the kernel the handle's K_eff launches in its current mode ("k_keff_lattice", "k_keff_groups_pipe",
  * "k_keff_tiles_pipe", "k_keff_tiles", "k_keff_hex_tiles" or "k_keff_parity"); NULL for a NULL handle. */
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
+/* Structured-block introspection (host only, no device; not a reference interface): whether a FAST handle
+ * created from `desc` runs the structured Kuhn-block stencil (lattice.cpp). Returns 1 and fills dims (nodes per
+ * axis), coef (CWF_LATTICE_COEFS floats: the 15 interior stencil blocks, then the 46 cell-pair blocks, row-major
+ * 3x3, unscaled by stiffness_scale) and plane ([dims[2]] storage index of node (0, 0, k); NULL: not wanted)
+ * when it does, 0 when it does not, a cwf_status (< 0) on bad arguments. `renumber` != 0 allows the
+ * lexicographic renumbering a handle without CWF_DESC_KEEP_NODE_ORDER may apply. */
+#define CWF_LATTICE_COEFS 549
+int cwf_lattice_describe(const cwf_system_desc *desc, int renumber, uint32_t dims[3], float *coef, uint32_t *plane);
 
 /* Live kernel timing (measurement support, not a reference interface): when enabled, every
  * K_eff launch inside solve_pcg / stepper_step is bracketed by hipEvents on the handle's stream;

@@ -1,0 +1,178 @@
+"""The structured-block FAST operator (lattice.cpp / lattice.inc, k_keff_lattice) against the pinned oracle.
+
+A FAST handle whose mesh is a Kuhn-split box lattice (one gradient / volume set per Kuhn type) applies K_eff as
+the node-pair stencil of the shared cell stiffness. Its arithmetic is the element loop's regrouped in fp32, so it
+carries FAST's tolerance contract: K x within 2e-5 of the bit-exact operator relative to its scale (max |row|),
+solves at tol 1e-6 within 1e-4 (relative) of the oracle's solution and its iteration count +-10%. Covered: the
+detection (and its refusal of a jittered mesh), bricks cut by the block's faces in every direction, partial
+Dirichlet masks, Rayleigh scalars, a randomly permuted node order (renumbered to the lattice order and back at
+the boundary), Newmark steps, the fan-group path on the same mesh (CWF_LATTICE=0), and slab shards (a shard's
+local order: owned planes, then ghost planes) through the LOCAL communicator."""
+import numpy as np
+import pytest
+
+from cwf import _lib, meshgen, pack, pcg, scenarios, shard
+from cwf.stepper import Stepper
+from helpers import oracle_system
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "8x3x4": lambda: scenarios.block_case(8, 3, 4, h=0.1, tol=1e-6, max_iterations=600),
+    "33x9x5": lambda: scenarios.block_case(33, 9, 5, h=0.1, tol=1e-6, max_iterations=800),
+    "rayleigh": lambda: scenarios.block_case(6, 4, 3, h=0.1, xi=0.05, w=(10.0, 100.0), tol=1e-6,
+                                             max_iterations=600),
+    "rollers": lambda: scenarios.roller_case(12, 10, 7, tol=1e-6, max_iterations=1500),
+    "c1": lambda: scenarios.config_case("c1"),
+}
+
+
+@pytest.fixture(scope="module", params=sorted(CASES))
+def case(request):
+    return CASES[request.param]()
+
+
+def _system(case, mode=_lib.MODE_FAST, sK=None, sM=None):
+    s0, m0 = case.scalars()
+    return pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, s0 if sK is None else sK,
+                                             m0 if sM is None else sM, mode=mode)
+
+
+def _kernel(s):
+    return (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
+
+
+def _apply_err(case, s, seed=3):
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rng = np.random.Generator(np.random.PCG64(seed))
+    x = rng.uniform(-1, 1, case.packing.dof_count).astype(np.float32)
+    y = np.zeros_like(x)
+    pcg.apply_keff(s, x, y).value()
+    ref = o.apply_keff(x).astype(np.float64)
+    return np.max(np.abs(y - ref)) / np.max(np.abs(ref))
+
+
+def permuted_block(nx, ny, nz, h=0.1, **kw):
+    """A Kuhn block with randomly permuted node and element order and no jitter: still a lattice."""
+    tm = meshgen.jitter_and_permute(meshgen.kuhn_block(nx, ny, nz, h), h, jitter=0.0)
+    mesh = pack.from_tetmesh(tm)
+    cfg = scenarios.make_config(**kw)
+    return scenarios.Case(f"perm{nx}x{ny}x{nz}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
+
+
+def test_lattice_detected(case):
+    assert _kernel(_system(case)).startswith("k_keff_lattice")
+
+
+def test_jittered_mesh_is_not_a_lattice():
+    case = scenarios.block_case(7, 6, 5, h=0.1, jitter=True, tol=1e-6)
+    assert _kernel(_system(case)).startswith("k_keff_groups_pipe")
+
+
+def test_lattice_apply_close(case):
+    assert _apply_err(case, _system(case)) <= 2e-5
+
+
+def test_lattice_off_runs_the_fan_groups(case, monkeypatch):
+    monkeypatch.setenv("CWF_LATTICE", "0")
+    s = _system(case)
+    assert _kernel(s).startswith("k_keff_groups_pipe")
+    assert _apply_err(case, s) <= 2e-5
+
+
+@pytest.mark.parametrize("L", ["2", "3", "64"])
+def test_lattice_work_item_lengths(L, monkeypatch):
+    """Planes per work item (CWF_LAT_L): chunk boundaries inside the block and one chunk over all planes."""
+    monkeypatch.setenv("CWF_LAT_L", L)
+    case = scenarios.block_case(40, 17, 9, h=0.1, tol=1e-6)
+    assert _apply_err(case, _system(case), seed=11) <= 2e-5
+
+
+def test_lattice_permuted_node_order():
+    case = permuted_block(9, 7, 6, tol=1e-6, max_iterations=800)
+    s = _system(case)
+    assert _kernel(s).startswith("k_keff_lattice")
+    assert _apply_err(case, s) <= 2e-5
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(800, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, 800, 1e-6)
+    assert t.converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+
+
+def test_lattice_solve_close(case):
+    s = _system(case)
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    mi = case.cfg.solver.max_iterations
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(mi, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, mi, 1e-6)
+    assert t.converged and ref["telemetry"].converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
+
+
+def test_lattice_stepper_steps():
+    case = scenarios.block_case(10, 5, 6, h=0.1, xi=0.05, w=(10.0, 100.0), tol=1e-6, max_iterations=1500)
+    P = case.packing
+    ref = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_PARITY)
+    fast = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST)
+    for k in range(3):
+        tr = ref.step(0.01 * k).value()
+        tf = fast.step(0.01 * k).value()
+        assert tf.pcg.converged and tr.pcg.converged
+        assert abs(tf.pcg.iterations - tr.pcg.iterations) <= max(3, tr.pcg.iterations // 10)
+    for what in (Stepper.DISPLACEMENT, Stepper.VELOCITY):
+        ur, uf = ref.get_state(what), fast.get_state(what)
+        assert np.linalg.norm(uf - ur) <= 1e-4 * np.linalg.norm(ur)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_lattice_slab_shards(nranks):
+    """Slab sub-meshes (scenarios.slab_case_shape, the bench's decomposition) keep the lattice on every shard
+    (local order: owned planes, then the ghost planes): before attach a shard's owned rows are the one-handle
+    lattice rows (the same stencil arithmetic; its blocks come from the sub-mesh's own gradients, equal to 1e-6),
+    and the attached shards' FAST solve converges to the oracle solution."""
+    shape = (11, 7, 3)
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=1e-6, max_iterations=800)
+    P = glob.packing
+    sK, sM = glob.scalars()
+    single = _system(glob)
+    assert _kernel(single).startswith("k_keff_lattice")
+    rng = np.random.Generator(np.random.PCG64(7))
+    x = rng.uniform(-1, 1, P.dof_count).astype(np.float32)
+    y1 = np.zeros_like(x)
+    pcg.apply_keff(single, x, y1).value()
+    y1 = y1.reshape(-1, 3)
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs = [], [], [], []
+    for r in range(nranks):
+        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, tol=1e-6)
+        src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
+        sh = shard.build_shard(src, begin, r, node_global)
+        s = sh.system(glob.materials, sK, sM)
+        assert _kernel(s).startswith("k_keff_lattice")
+        gid = sh.node_global.astype(np.int64)
+        own = sh.owned_nodes
+        yl = np.zeros(3 * sh.local_nodes, np.float32)
+        pcg.apply_keff(s, np.ascontiguousarray(x.reshape(-1, 3)[gid].reshape(-1)), yl).value()
+        d = np.abs(yl.reshape(-1, 3)[:own].astype(np.float64) - y1[gid[:own]])
+        assert np.max(d) <= 1e-6 * np.max(np.abs(y1))
+        comm.attach(s, sh)
+        systems.append(s)
+        shards.append(sh)
+        rhs.append(sh.local_dofs(case.static_rhs()))
+        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    tel = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(800, 1e-6), xs).value()
+    xg = np.zeros((P.node_count, 3), np.float32)
+    for sh, xl in zip(shards, xs):
+        xg[sh.node_global[: sh.owned_nodes].astype(np.int64)] = xl.reshape(-1, 3)[: sh.owned_nodes]
+    comm.close()
+    ref = oracle_system(P, glob.materials, sK, sM).solve_pcg(glob.static_rhs(), 800, 1e-6)
+    assert tel.converged
+    assert np.linalg.norm(xg.reshape(-1) - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    n_ref = ref["telemetry"].iterations
+    assert abs(tel.iterations - n_ref) <= max(3, n_ref // 10)
