@@ -860,6 +860,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.lk1 = lat.nz;
         t.lplane = dpl;
         t.lcoef = dcf;
+        t.lsym = lat.sym ? 1 : 0;
         t.node_part_off = dnpo;
         t.off_mask = 1;
         t.node_major = 1;

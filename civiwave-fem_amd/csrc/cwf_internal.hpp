@@ -86,9 +86,13 @@ struct DevTiles
     int lat = 0;
     uint32_t lnx = 0, lny = 0, lnz = 0;  // lattice nodes per axis (a shard: its local planes)
     uint32_t lk0 = 0, lk1 = 0;           // planes holding the rows this handle computes (a shard: its owned planes)
-    uint32_t lnbx = 0, lnby = 0, lL = 0, lnwork = 0;  // 32 x 8 column bricks, planes per work item, work items
+    // work items (lattice_plan): lnsb shell workgroups (a multiple of 8: one thread per surface node of the
+    // computed planes, lnshell of them), then lnbx * lnby * ceil((lkI1 - lkI0) / lL) interior bricks (32 x 8
+    // columns of the strict interior i, j in [1, n - 1) times lL planes of [lkI0, lkI1)); lnwork = all of them
+    uint32_t lnbx = 0, lnby = 0, lL = 0, lnwork = 0, lnwm = 0, lnsb = 0, lnshell = 0, lkI0 = 0, lkI1 = 0;
     const uint32_t *lplane = nullptr;    // [lnz] storage index of node (0, 0, k)
-    const float *lcoef = nullptr;        // [kLatCoef] stencil blocks, then cell-pair blocks (unscaled by s_K)
+    const float *lcoef = nullptr;        // [kLatCoef] stencil, cell-pair and face blocks (unscaled by s_K)
+    int lsym = 0;                        // S_(-d) == S_d: the paired-direction instantiation
 };
 // lattice work items for planes [lk0, lk1) (lattice.cpp): sets lnbx, lnby, lL, lnwork, ntiles
 void lattice_plan(DevTiles &t);
@@ -169,7 +173,9 @@ constexpr int kLatPairOff[kLatPairs] = {0,  1,  3,  7,  5,  9,  11, 13,  // 0 ->
                                         10, 6,  2,  0,  3,               // 5 -> 0 1 4 5 7
                                         12, 6,  4,  0,  1,               // 6 -> 0 2 4 6 7
                                         14, 12, 10, 6,  8,  4,  2,  0};  // 7 -> 0..7
-constexpr int kLatCoef = 9 * (kLatOffsets + kLatPairs);  // f32: [15][3][3] stencil, then [46][3][3] cell blocks
+// f32 coefficient table: [15][3][3] stencil blocks, then [46][3][3] cell blocks
+constexpr int kLatCoefPairs = 9 * kLatOffsets;
+constexpr int kLatCoef = kLatCoefPairs + 9 * kLatPairs;
 
 struct Lattice
 {
@@ -177,6 +183,7 @@ struct Lattice
     std::vector<uint32_t> plane;      // [nz] storage index of node (0, 0, k)
     std::vector<uint32_t> perm;       // when renumbered: internal (lexicographic) index -> caller's node
     float coef[kLatCoef] = {};
+    bool sym = false;  // S_(-d) == S_d for every direction (k_keff_lattice's paired form)
 };
 // true when the desc is a Kuhn-split box lattice with one gradient / volume set per Kuhn type (lattice.cpp);
 // allow_perm: the handle may renumber (otherwise the nodes must already be lexicographic within planes)

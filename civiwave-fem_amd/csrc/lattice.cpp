@@ -11,10 +11,9 @@
 //   (K u)_n = sum_d S_d u_(n+d),  S_d = sum over the cell corners c with c + d a corner of Kc[c][c + d].
 // The kernel (lattice.inc) forms it in difference form, sum_(d != 0) S_d (u_(n+d) - u_n) (rigid translations
 // are in the null space of every row), so each fp32 term is strain-sized as in the element loop. A node on the
-// block's surface misses some of its 8 cells; the kernel subtracts a missing cell's row-c blocks Kc[c][.] (in the
-// same difference form) from the interior row, with positions outside the block clamped to the nearest node (their
-// differences cancel). The regrouping changes the fp32 summation order only (FAST's tolerance contract,
-// tests/test_lattice.py on the CPU, tests/test_gpu_lattice.py).
+// block's surface misses some of its 8 cells: its row is formed in the cell form instead, each existing cell's
+// blocks Kc[c][c'] on the same differences. The regrouping changes the fp32 summation order only (FAST's
+// tolerance contract, tests/test_lattice.py on the CPU, tests/test_gpu_lattice.py).
 //
 // detect_lattice() decides it for a desc: integer lattice coordinates of every node (from the first tet's cell
 // size), a bijection onto an nx * ny * nz lattice, every tet one Kuhn tet of one cell (each of a cell's 6 types
@@ -284,24 +283,44 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
             for (int k = 0; k < 3; ++k)
                 L.coef[9 * (kLatOffsets + p) + 3 * r + k] = (float)Kc[kLatPair[p][0]][kLatPair[p][1]][r][k];
     // every block outside the Kuhn pattern is structurally zero (never accumulated): nothing to check
+    // paired directions: S_(-d) = S_d (an isotropic Kuhn block's blocks are symmetric and S_(-d) = S_d^T)
+    L.sym = true;
+    for (int o = 1; o < kLatOffsets; o += 2)
+        L.sym = L.sym && std::memcmp(L.coef + 9 * o, L.coef + 9 * (o + 1), 9 * sizeof(float)) == 0;
     return true;
 }
 
-// Work items: 32 x 8 column bricks times L planes, L sized for about kLatTargetItems workgroups (about six
-// resident 256-thread workgroups per CU on 256 CUs) and at least 2 (each item reads L + 2 planes)
+// Work items: the surface shell of the computed planes [lk0, lk1), one node per thread (256-thread workgroups,
+// rounded up to whole XCD groups so the bricks after them keep the XCD mapping), then 32 x 8 column bricks of the
+// strict interior times L planes, L sized for about kLatTargetItems bricks (one round of resident workgroups: three
+// or four per CU on 256 CUs) and at least 4 (each brick reads L + 2 planes). Measured (k_keff_lattice in the PCG
+// loop, one MI355X): C2 L = 2 / 4 / 8 / 16: 18.5 / 16.4 / 17.5 / 20.6 us; C3 L = 4 / 8 / 16 / 24: 76 / 69 / 70 / 73 us
 void lattice_plan(DevTiles &t)
 {
-    constexpr uint64_t kLatTargetItems = 1536;
-    t.lnbx = (t.lnx + 31u) / 32u;
-    t.lnby = (t.lny + 7u) / 8u;
-    const uint64_t planes = t.lk1 > t.lk0 ? t.lk1 - t.lk0 : 0u, cols = (uint64_t)t.lnbx * t.lnby;
+    constexpr uint64_t kLatTargetItems = 1024;
+    const uint64_t nx = t.lnx, ny = t.lny, nz = t.lnz;
+    const uint64_t k0 = t.lk0, k1 = std::max(t.lk1, t.lk0);
+    t.lkI0 = (uint32_t)std::max<uint64_t>(k0, 1);
+    t.lkI1 = (uint32_t)std::max<uint64_t>(std::min<uint64_t>(k1, nz - 1), t.lkI0);
+    uint64_t shell = 0;
+    if (k0 == 0 && k1 > 0)
+        shell += nx * ny;
+    if (k1 == nz && nz > 1 && k1 > k0)
+        shell += nx * ny;
+    shell += (uint64_t)(t.lkI1 - t.lkI0) * (2 * nx + 2 * (ny - 2));
+    t.lnshell = (uint32_t)shell;
+    t.lnsb = (uint32_t)(((shell + 255) / 256 + 7) / 8 * 8);
+    t.lnbx = (uint32_t)((nx - 2 + 31) / 32);
+    t.lnby = (uint32_t)((ny - 2 + 7) / 8);
+    const uint64_t planes = t.lkI1 - t.lkI0, cols = (uint64_t)t.lnbx * t.lnby;
     uint64_t L = (planes * cols + kLatTargetItems - 1) / kLatTargetItems;
     const char *lk = knob("CWF_LAT_L");
     if (lk && atoi(lk) > 0)
         L = (uint64_t)atoi(lk);
-    L = std::max<uint64_t>(2, std::min<uint64_t>(L, 64));
+    L = std::max<uint64_t>(lk && atoi(lk) > 0 ? 2 : 4, std::min<uint64_t>(L, 64));
     t.lL = (uint32_t)L;
-    t.lnwork = planes ? (uint32_t)(cols * ((planes + L - 1) / L)) : 0u;
+    t.lnwm = (uint32_t)(cols * ((planes + L - 1) / L));
+    t.lnwork = t.lnsb + t.lnwm;
     t.ntiles = t.lnwork;
 }
 
@@ -331,6 +350,7 @@ extern "C" int cwf_lattice_describe(const cwf_system_desc *desc, int renumber, u
     dims[1] = L.ny;
     dims[2] = L.nz;
     std::memcpy(coef, L.coef, sizeof L.coef);
+    dims[0] |= L.sym ? 0x80000000u : 0u;
     if (plane)
         std::memcpy(plane, L.plane.data(), L.plane.size() * sizeof(uint32_t));
     return 1;

@@ -2,8 +2,8 @@
 it derives, through the C-ABI introspection entry cwf_lattice_describe (no device needed).
 
 The blocks are applied here in numpy (fp64 over the f32 blocks), with the kernel's algorithm (lattice.inc): the 14
-off-centre interior stencil blocks on the differences u_(n+d) - u_n (positions outside the block clamped to the
-nearest node), minus the row blocks of every cell a surface node does not have. That must reproduce the pinned oracle's apply_keff (the reference's element loop) to the f32 rounding of
+off-centre interior stencil blocks on the differences u_(n+d) - u_n for the nodes inside the block, and for the
+nodes on its surface each existing cell's blocks on the differences to the node's own value. That must reproduce the pinned oracle's apply_keff (the reference's element loop) to the f32 rounding of
 the blocks: 1e-6 of the operator scale (max |row|)."""
 import ctypes as C
 
@@ -27,7 +27,11 @@ def describe(system, renumber=True):
     plane = np.zeros(1 << 16, np.uint32)
     st = L.cwf_lattice_describe(C.byref(desc), int(renumber), dims, coef.ctypes.data, plane.ctypes.data)
     assert st in (0, 1), st
-    return (tuple(dims), coef, plane[: dims[2]].copy()) if st == 1 else None
+    if st != 1:
+        return None
+    sym = bool(dims[0] >> 31)
+    d = (dims[0] & 0x7FFFFFFF, dims[1], dims[2])
+    return d, coef, plane[: d[2]].copy(), sym
 
 
 def fast_system(case):
@@ -36,12 +40,13 @@ def fast_system(case):
 
 
 def lattice_apply(dims, coef, x3, sK):
-    """K x (no mass, no Dirichlet) on an nx*ny*nz lattice in lexicographic order, the kernel's algorithm: the
-    difference form sum_(d != 0) S_d (u_(n+d) - u_n), positions outside the block clamped to the nearest node."""
+    """K x (no mass, no Dirichlet) on an nx*ny*nz lattice in lexicographic order, the kernel's algorithm
+    (lattice.inc): interior nodes by the difference-form stencil sum_(d != 0) S_d (u_(n+d) - u_n), surface nodes by
+    the cell form (each existing cell's blocks on the differences to the node's own value)."""
     nx, ny, nz = dims
     u = np.pad(x3.reshape(nz, ny, nx, 3), ((1, 1), (1, 1), (1, 1), (0, 0)), mode="edge")
     S = coef[:135].astype(np.float64).reshape(15, 3, 3)
-    Kp = coef[135:].astype(np.float64).reshape(46, 3, 3)
+    Kp = coef[135:549].astype(np.float64).reshape(46, 3, 3)
     u0 = u[1:nz + 1, 1:ny + 1, 1:nx + 1]
 
     def nb(d):
@@ -52,16 +57,19 @@ def lattice_apply(dims, coef, x3, sK):
     for o in range(1, 15):
         y += nb(OFF[o]) @ S[o].T
     k, j, i = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    surface = (i == 0) | (i == nx - 1) | (j == 0) | (j == ny - 1) | (k == 0) | (k == nz - 1)
+    ys = np.zeros_like(y)
     for c in range(8):
         cx, cy, cz = c & 1, (c >> 1) & 1, (c >> 2) & 1
         has = ((i >= 1) if cx else (i + 1 < nx)) & ((j >= 1) if cy else (j + 1 < ny)) & \
               ((k >= 1) if cz else (k + 1 < nz))
         t = np.zeros_like(y)
         for p, (a, b) in enumerate(PAIRS):
-            if a == c:
+            if a == c and b != c:
                 d = ((b & 1) - cx, ((b >> 1) & 1) - cy, ((b >> 2) & 1) - cz)
                 t += nb(d) @ Kp[p].T
-        y -= np.where(has[..., None], 0.0, t)
+        ys += np.where(has[..., None], t, 0.0)
+    y = np.where(surface[..., None], ys, y)
     return sK * y.reshape(-1, 3)
 
 
@@ -74,7 +82,8 @@ def test_stencil_reproduces_the_oracle_operator(name):
     P = case.packing
     out = describe(fast_system(case))
     assert out is not None
-    dims, coef, plane = out
+    dims, coef, plane, sym = out
+    assert sym  # isotropic: S_(-d) == S_d
     assert dims == tuple(int(v) + 1 for v in meshgen_shape(case))
     assert np.array_equal(plane, np.arange(dims[2]) * dims[0] * dims[1])
     sK, sM = case.scalars()
@@ -105,7 +114,7 @@ def test_permuted_lattice_needs_renumbering():
     case = scenarios.Case("perm", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
     s = fast_system(case)
     assert describe(s, renumber=False) is None
-    dims, _, plane = describe(s, renumber=True)
+    dims, _, plane, _ = describe(s, renumber=True)
     assert dims == (6, 5, 4) and np.array_equal(plane, np.arange(4) * 30)
 
 
@@ -118,7 +127,7 @@ def test_slab_shard_local_order_is_a_lattice():
     src = fast_system(case)
     sh = shard.build_shard(src, begin, r, node_global)
     s = sh.system(case.materials, sK, sM)
-    dims, _, plane = describe(s, renumber=False)
+    dims, _, plane, _ = describe(s, renumber=False)
     A = (shape[0] + 1) * (shape[1] + 1)
     nplanes = dims[2]
     assert dims[:2] == (shape[0] + 1, shape[1] + 1) and nplanes * A == sh.local_nodes
