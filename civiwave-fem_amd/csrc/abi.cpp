@@ -870,6 +870,53 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.total_tile_nodes = (uint32_t)N;
         const char *wt = knob("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
         t.wt_part = wt ? (wt[0] == '1') : 0;
+        // per-class preconditioner (the update pass reads one byte per node instead of the 16-B record and the
+        // partial-run bounds) when the lumped mass is a function of the boundary type
+        {
+            std::vector<uint8_t> cls(N);
+            std::vector<uint32_t> rep(kLatClasses, 0xFFFFFFFFu);
+            std::vector<float> tmass(27, 0.f);
+            std::vector<uint8_t> tseen(27, 0);
+            bool uniform = true;
+            for (uint32_t k = 0; k < lat.nz && uniform; ++k)
+                for (uint32_t j = 0; j < lat.ny; ++j)
+                    for (uint32_t i = 0; i < lat.nx; ++i)
+                    {
+                        const uint32_t n = lat.plane[k] + j * lat.nx + i;
+                        const auto side = [](uint32_t a, uint32_t na) { return a == 0 ? 0u : a + 1 == na ? 2u : 1u; };
+                        const uint32_t ty = side(i, lat.nx) + 3 * side(j, lat.ny) + 9 * side(k, lat.nz);
+                        const uint32_t c = ty << 3 | (d->bc_mask[n] & 7u);
+                        cls[n] = (uint8_t)c;
+                        if (rep[c] == 0xFFFFFFFFu || n < rep[c])
+                            rep[c] = n;
+                        if (!tseen[ty])
+                        {
+                            tseen[ty] = 1;
+                            tmass[ty] = d->lumped_mass[n];
+                        }
+                        else if (std::memcmp(&tmass[ty], &d->lumped_mass[n], sizeof(float)) != 0)
+                            uniform = false;
+                    }
+            if (uniform)
+            {
+                uint8_t *dcls;
+                uint32_t *drep;
+                uint4 *dci6;
+                float *dci9;
+                if (int st = upload(h, &dcls, cls.data(), N))
+                    return bail(st);
+                if (int st = upload(h, &drep, rep.data(), kLatClasses))
+                    return bail(st);
+                if (int st = dalloc(h, &dci6, kLatClasses))
+                    return bail(st);
+                if (int st = dalloc(h, &dci9, 9 * kLatClasses))
+                    return bail(st);
+                t.lcls = dcls;
+                t.lrep = drep;
+                t.lcinv6 = dci6;
+                t.lcinv9 = dci9;
+            }
+        }
         h->lat_plane.swap(lat.plane);
         lattice_plan(t);
     }

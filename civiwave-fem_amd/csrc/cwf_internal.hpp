@@ -93,6 +93,13 @@ struct DevTiles
     const uint32_t *lplane = nullptr;    // [lnz] storage index of node (0, 0, k)
     const float *lcoef = nullptr;        // [kLatCoef] stencil, cell-pair and face blocks (unscaled by s_K)
     int lsym = 0;                        // S_(-d) == S_d: the paired-direction instantiation
+    // the update pass's preconditioner by node class (when the lumped mass is uniform per boundary class): class =
+    // (27 boundary types) << 3 | Dirichlet mask per node, one representative node per class, its packed block
+    // inverse and 9-float operator (rebuilt with the per-node inverse)
+    const uint8_t *lcls = nullptr;  // [N]
+    const uint32_t *lrep = nullptr;  // [kLatClasses], 0xFFFFFFFF: no node of the class
+    uint4 *lcinv6 = nullptr;         // [kLatClasses]
+    float *lcinv9 = nullptr;         // [9 kLatClasses]
 };
 // lattice work items for planes [lk0, lk1) (lattice.cpp): sets lnbx, lnby, lL, lnwork, ntiles
 void lattice_plan(DevTiles &t);
@@ -176,6 +183,7 @@ constexpr int kLatPairOff[kLatPairs] = {0,  1,  3,  7,  5,  9,  11, 13,  // 0 ->
 // f32 coefficient table: [15][3][3] stencil blocks, then [46][3][3] cell blocks
 constexpr int kLatCoefPairs = 9 * kLatOffsets;
 constexpr int kLatCoef = kLatCoefPairs + 9 * kLatPairs;
+constexpr uint32_t kLatClasses = 27 * 8;  // (boundary type along x, y, z: lo / inside / hi) x Dirichlet mask
 
 struct Lattice
 {

@@ -1397,6 +1397,23 @@ __global__ __launch_bounds__(256) void k_sym_inverse(uint32_t N, const uint32_t 
     reinterpret_cast<uint4 *>(inv6)[n] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// a lattice handle's per-class block inverse (packed record and the 9-float operator) from one representative node
+// of each class (every node of a class has the same diagonal blocks and mass: lattice.cpp)
+__global__ __launch_bounds__(256) void k_lat_class_inverse(const uint32_t *__restrict__ rep,
+                                                           const float *__restrict__ inv6, const float *__restrict__ inv9,
+                                                           uint4 *__restrict__ cinv6, float *__restrict__ cinv9)
+{
+    for (uint32_t c = threadIdx.x; c < kLatClasses; c += 256)
+    {
+        const uint32_t n = rep[c];
+        if (n == 0xFFFFFFFFu)
+            continue;
+        cinv6[c] = reinterpret_cast<const uint4 *>(inv6)[n];
+        for (int q = 0; q < 9; ++q)
+            cinv9[9 * c + q] = inv9[9ull * n + q];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_halo_pack(const uint32_t *__restrict__ idx, uint64_t n,
                                                    const float *__restrict__ v, float *__restrict__ out)
 {
@@ -1456,7 +1473,7 @@ struct UpdNode
 // r -= alpha Ap, Dirichlet, z = M^-1 r (16-B Jacobi-scaled block, blockinv_pack.hpp), r.r / r.z shares;
 // x += alpha_j p_j for the last `lag` iterations every lag-th iteration (lazy x, 1 = every iteration; the
 // FMA chain in iteration order is bitwise the eager update), fast_flush_x applies the rest after the solve.
-template <int U, bool XF>
+template <int U, bool XF, bool LAT>
 __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, const float *__restrict__ inv9,
     float *__restrict__ x, float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold,
@@ -1464,9 +1481,16 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     double *__restrict__ prr, double *__restrict__ prz, unsigned it, int wt, PBufs pbuf, unsigned lag)
 {
     __shared__ double red[kUpdThreads / 64];
+    __shared__ uint4 cinv[LAT ? kLatClasses : 1];
     if (!ctl->active)
         return;
     const DevTiles &T = s.t;
+    if constexpr (LAT)  // structured block: the packed block inverse of each (boundary class, mask), lattice.cpp
+    {
+        for (uint32_t c = threadIdx.x; c < kLatClasses; c += kUpdThreads)
+            cinv[c] = T.lcinv6[c];
+        __syncthreads();
+    }
     const float beta = (float)ctl->beta;  // this iteration's (the tiles kernel's residual step wrote it)
     const float sM = (float)s.sM;
     const __amdgpu_buffer_rsrc_t rpart = whole_rsrc(T.part);
@@ -1485,10 +1509,19 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             v[u].n = b0 + u * kUpdThreads;
             v[u].ok = v[u].n < s.Nown;
             const uint32_t n = v[u].ok ? v[u].n : 0u;
-            const uint32_t o0 = T.node_part_off[n], o1 = T.node_part_off[n + 1];
-            v[u].q0 = o0 & kPartOffBits;
-            v[u].q1 = o1 & kPartOffBits;
-            v[u].mk = T.off_mask ? o0 >> 29 : s.mask[n];
+            if constexpr (LAT)  // one row value per node; the mask and the block inverse from the node's class
+            {
+                v[u].q0 = n;
+                v[u].q1 = n + 1u;
+                v[u].mk = T.lcls[n];  // class << 3 | mask
+            }
+            else
+            {
+                const uint32_t o0 = T.node_part_off[n], o1 = T.node_part_off[n + 1];
+                v[u].q0 = o0 & kPartOffBits;
+                v[u].q1 = o1 & kPartOffBits;
+                v[u].mk = T.off_mask ? o0 >> 29 : s.mask[n];
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1498,18 +1531,23 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
 #pragma unroll
             for (int k = 0; k < 3; ++k)
                 w.rv0[k] = r[3u * n + k];
-            w.iw = reinterpret_cast<const uint4 *>(inv)[n];
-            // first two partials unconditionally (the part buffer carries 2 padding slots)
-            if (T.node_major)
+            if constexpr (LAT)
+                load3(rpart, n, w.pa);
+            else
             {
-                load3(rpart, w.q0, w.pa);
-                load3(rpart, w.q0 + 1, w.pb);
+                w.iw = reinterpret_cast<const uint4 *>(inv)[n];
+                // first two partials unconditionally (the part buffer carries 2 padding slots)
+                if (T.node_major)
+                {
+                    load3(rpart, w.q0, w.pa);
+                    load3(rpart, w.q0 + 1, w.pb);
+                }
             }
             // a node of no element forms p_it here (Ap = m s_M p); the tiles kernel folded the mass term
             // into every other node's owner partial
             w.m = 0.f;
             w.pv[0] = w.pv[1] = w.pv[2] = 0.f;
-            if (w.q0 == w.q1)
+            if (!LAT && w.q0 == w.q1)
             {
                 w.m = s.mass[n] * sM;
 #pragma unroll
@@ -1576,8 +1614,10 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             UpdNode &w = v[u];
             if (!w.ok)
                 continue;
-            const uint32_t n = w.n, mk = w.mk;
-            if (w.q0 == w.q1)
+            const uint32_t n = w.n, mk = LAT ? w.mk & 7u : w.mk;
+            if constexpr (LAT)
+                w.iw = cinv[w.mk];
+            if (!LAT && w.q0 == w.q1)
                 store3(pnew, whole_rsrc(pnew), n, w.pv[0], w.pv[1], w.pv[2], false);
             if (xflush)  // x and the lag p_j were loaded with the rest; the FMA chain in iteration order
             {
@@ -1595,7 +1635,13 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
             }
             float a0 = 0.f, a1 = 0.f, a2 = 0.f;
             const uint32_t cnt = w.q1 - w.q0;
-            if (T.node_major)
+            if (LAT)
+            {
+                a0 = w.pa[0];
+                a1 = w.pa[1];
+                a2 = w.pa[2];
+            }
+            else if (T.node_major)
             {
                 if (cnt > 0)
                 {
@@ -1642,7 +1688,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
                 unpack_block_inverse(w.iw.y, w.iw.z, w.iw.w, __uint_as_float(w.iw.x), bv);
             else
             {
-                const float *a9 = inv9 + 9ull * n;
+                const float *a9 = LAT ? T.lcinv9 + 9u * w.mk : inv9 + 9ull * n;
                 bv[0] = a9[0];
                 bv[1] = a9[1];
                 bv[2] = a9[2];
@@ -1849,7 +1895,7 @@ unsigned update_resident()
     int dev = 0, bpc = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<U, XF>, kUpdThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_pcg_update_tiles<U, XF, false>, kUpdThreads, 0);
     const unsigned r = (unsigned)((bpc > 0 ? bpc : 1) * (cus > 0 ? cus : 1));
     return r < kMaxUpdateBlocks ? r : kMaxUpdateBlocks;
 }
@@ -1977,7 +2023,9 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
     const DevSys &s = h->ds;
     const bool direct = fast_direct_fold(h);
     const bool xf = x_flush_iter(it);
-    const auto k = xf ? k_pcg_update_tiles<1, true> : k_pcg_update_tiles<1, false>;
+    const bool lat = s.t.lcls != nullptr;
+    const auto k = lat ? (xf ? k_pcg_update_tiles<1, true, true> : k_pcg_update_tiles<1, false, true>)
+                       : (xf ? k_pcg_update_tiles<1, true, false> : k_pcg_update_tiles<1, false, false>);
     k<<<fast_update_blocks(s, xf), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
         direct ? h->part0 : h->g_pap, direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it,
@@ -2025,6 +2073,8 @@ void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
         parity_block_jacobi(h, h->inv, st);
     if (h->ds.N)
         k_sym_inverse<<<grid_for(h->ds.N, 256), 256, 0, st>>>(h->ds.N, h->ds.mask, h->inv, h->inv6);
+    if (h->ds.t.lcls)  // structured block: one representative node per (boundary class, mask)
+        k_lat_class_inverse<<<1, 256, 0, st>>>(h->ds.t.lrep, h->inv6, h->inv, h->ds.t.lcinv6, h->ds.t.lcinv9);
 }
 
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st)

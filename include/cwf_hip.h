@@ -151,7 +151,7 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
  * created from `desc` runs the structured Kuhn-block stencil (lattice.cpp). Returns 1 and fills dims (nodes per
  * axis; bit 31 of dims[0]: the stencil pairs S_(-d) = S_d), coef (CWF_LATTICE_COEFS floats, row-major 3x3 blocks
  * unscaled by stiffness_scale: the 15 interior stencil blocks, then the 46 cell-pair blocks) and plane ([dims[2]] storage index of node (0, 0, k); NULL: not wanted) when it does, 0 when it
- * does not, a cwf_status (< 0) on bad arguments. `renumber` != 0 allows the lexicographic renumbering a handle
+ * does not, a negative cwf_status code on bad arguments. `renumber` != 0 allows the lexicographic renumbering a handle
  * without CWF_DESC_KEEP_NODE_ORDER may apply. */
 #define CWF_LATTICE_COEFS 549
 int cwf_lattice_describe(const cwf_system_desc *desc, int renumber, uint32_t dims[3], float *coef, uint32_t *plane);
