@@ -53,6 +53,8 @@ def parse():
                          "period (4): every 4th update also writes x, and sampling every 4th launch timed only the "
                          "launches right after those (C3: 105 us against rocprofv3's 98 us average)")
     ap.add_argument("--cpu-iterations", type=int, default=40)
+    ap.add_argument("--no-general-roofline", action="store_true",
+                    help="skip roofline_general (the fan-group tiles kernel on C3 with the lattice stencil off)")
     ap.add_argument("--no-hbm-roofline", action="store_true",
                     help="skip the live configs[2] K_eff roofline (N=1 runs of configs other than c3 add it)")
     ap.add_argument("--traffic", default="auto",
@@ -112,13 +114,26 @@ def cpu_baseline(case, sK, sM, iters):
                                "converged": bool(o1["telemetry"].converged)})
 
 
-def hbm_roofline(L, device, key="c3", steps=2, sample=5):
+def c3_pmc_traffic(kname):
+    """HBM bytes per launch of kernel `kname` from the newest committed C3 FAST PMC summary that profiled it."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_fast*_pmc.json")), reverse=True):
+        pmc = json.load(open(path))
+        if any(same_kernel(kname, k) for k in pmc.get("kernels", {})):
+            return pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def hbm_roofline(L, device, key="c3", steps=2, sample=5, general=False):
     """The same PCG-mode K_eff kernel, live, on the configs[2] block (C2's working set sits in
     the 256 MB MALL, so its roofline is not an HBM figure; C3 moves 0.38 GB per launch): `steps` FAST Newmark
     steps of C3 after one untimed step, every `sample`-th K_eff launch hipEvent-timed on the handle's stream
     exactly as in the main timed steps (coprime with the lazy-x period). Round 2 timed a 200-iteration solve
     from x = 0 instead, which read ~10% above rocprofv3's average of the same kernel (109 vs 98 us); a C3
-    Newmark step's launches read within 1% of it. Outside the timed Newmark steps, so it changes no other field."""
+    Newmark step's launches read within 1% of it. Outside the timed Newmark steps, so it changes no other field.
+    general=True: the same with the structured-block stencil switched off (CWF_LATTICE=0), i.e. the fan-group
+    tiles kernel every unstructured mesh runs (C4's), on the same C3 block."""
     import ctypes as C
 
     from cwf import _lib, scenarios
@@ -126,9 +141,19 @@ def hbm_roofline(L, device, key="c3", steps=2, sample=5):
 
     case = scenarios.config_case(key)
     P = case.packing
-    st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST,
-                 device=device)
-    h = st.system.handle()
+    prev = os.environ.get("CWF_LATTICE")
+    if general:
+        os.environ["CWF_LATTICE"] = "0"
+    try:
+        st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST,
+                     device=device)
+        h = st.system.handle()
+    finally:
+        if general:
+            if prev is None:
+                os.environ.pop("CWF_LATTICE", None)
+            else:
+                os.environ["CWF_LATTICE"] = prev
     t = 0.0
     st.step(t).value()
     t += case.cfg.time.initial_dt
@@ -148,6 +173,7 @@ def hbm_roofline(L, device, key="c3", steps=2, sample=5):
            "kernel": (L.cwf_hip_system_keff_kernel(h) or b"").decode(), "avg_launch_ms": avg,
            "launches": int(n.value), "algorithmic_bytes_per_launch": float(lay_b.value),
            "reference_layout_equiv_gbs": ref_b.value / (avg * 1e-3) / 1e9}
+    out["traffic"], out["traffic_source"] = c3_pmc_traffic(out["kernel"])
     st.close()
     st.system.close()
     return out
@@ -316,34 +342,30 @@ def main():
         import glob
 
         tag = f"{args.config}_{args.mode}" + ("_hex8" if args.element == "hex8" else "")
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc.json")))
-        tpath = cands[-1] if cands and world == 1 else None
-    if tpath and os.path.exists(tpath):
-        pmc = json.load(open(tpath))
-        # only a profile of the same kernel counts (a committed profile of an older kernel is not this one's)
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc.json")), reverse=True)
+    else:
+        cands = [tpath] if tpath and os.path.exists(tpath) else []
+    for path in cands if world == 1 else []:
+        pmc = json.load(open(path))
+        # only a profile of the same kernel counts (a committed profile of an older kernel is not this one's):
+        # the newest that profiled it
         if any(same_kernel(kname, k) for k in pmc.get("kernels", {})):
             traffic = pmc.get("hbm_bytes_per_launch")
-            traffic_src = os.path.relpath(tpath, ROOT)
+            traffic_src = os.path.relpath(path, ROOT)
+            break
     result = None
     stepper.close()
     stepper.system.close()
-    hbm = None
+    hbm = hbm_general = None
     if (rank == 0 and world == 1 and not args.no_hbm_roofline and args.mode == "fast" and args.element == "tet4"
             and args.config != "c3"):
         hbm = hbm_roofline(L, device)
+        if not args.no_general_roofline:
+            hbm_general = hbm_roofline(L, device, general=True)
     copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
-    if hbm:
-        if copy_gbs:
-            hbm["frac_of_measured_copy"] = hbm["achieved"] / copy_gbs
-        hbm["traffic"], hbm["traffic_source"] = None, None
-        import glob
-
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_fast_pmc.json")))
-        if cands:
-            pmc = json.load(open(cands[-1]))
-            if any(same_kernel(hbm["kernel"], k) for k in pmc.get("kernels", {})):
-                hbm["traffic"] = pmc.get("hbm_bytes_per_launch")
-                hbm["traffic_source"] = os.path.relpath(cands[-1], ROOT)
+    for rl in (hbm, hbm_general):
+        if rl and copy_gbs:
+            rl["frac_of_measured_copy"] = rl["achieved"] / copy_gbs
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1 and args.element == "tet4":  # rank 0 at N=1 only
@@ -391,6 +413,8 @@ def main():
                          "frac_of_measured_copy": (achieved / copy_gbs) if achieved and copy_gbs else None},
             "cpu_baseline": cpu,
             "roofline_hbm": hbm,
+            # the unstructured-mesh SpMV (fan-group tiles, what C4 and any non-lattice mesh run) on the same C3 block
+            "roofline_general": hbm_general,
         }
         if args.mode == "parity":
             # the events bracket both PARITY K_eff passes: the element pass and the node fold that also forms
