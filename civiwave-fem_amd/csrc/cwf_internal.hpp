@@ -183,6 +183,11 @@ constexpr int kLatPairOff[kLatPairs] = {0,  1,  3,  7,  5,  9,  11, 13,  // 0 ->
 // f32 coefficient table: [15][3][3] stencil blocks, then [46][3][3] cell blocks
 constexpr int kLatCoefPairs = 9 * kLatOffsets;
 constexpr int kLatCoef = kLatCoefPairs + 9 * kLatPairs;
+// k_keff_lattice bricks: kLatBrickX x kLatBrickY columns of the strict interior, one thread per column
+#ifndef CWF_LAT_BY
+#define CWF_LAT_BY 8
+#endif
+constexpr int kLatBrickX = 32, kLatBrickY = CWF_LAT_BY, kLatThreads = kLatBrickX * kLatBrickY;
 constexpr uint32_t kLatClasses = 27 * 8;  // (boundary type along x, y, z: lo / inside / hi) x Dirichlet mask
 
 struct Lattice

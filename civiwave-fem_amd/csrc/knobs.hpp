@@ -29,8 +29,9 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_HEX_NT", "128|256: lanes of the hex8 tiles (tests/test_hex8.py)"},
     {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
     {"CWF_LATTICE", "0: no structured-block stencil (lattice.cpp); structured Kuhn blocks then run the fan groups"},
-    {"CWF_LAT_L", "n: planes per lattice work item (default: about 1536 work items)"},
+    {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     // PCG schedule (spmv_tiles.hip)
+    {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
     // multi-GPU (comm.cpp)
     {"CWF_RCCL_LIB", "path: load this NCCL-API library instead of librccl (tests/transport: the host-staged "

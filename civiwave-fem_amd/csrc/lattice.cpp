@@ -297,7 +297,7 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
 // loop, one MI355X): C2 L = 2 / 4 / 8 / 16: 18.5 / 16.4 / 17.5 / 20.6 us; C3 L = 4 / 8 / 16 / 24: 76 / 69 / 70 / 73 us
 void lattice_plan(DevTiles &t)
 {
-    constexpr uint64_t kLatTargetItems = 1024;
+    constexpr uint64_t kLatTargetItems = 262144 / kLatThreads;  // 1024 bricks of 256 threads, 512 of 512
     const uint64_t nx = t.lnx, ny = t.lny, nz = t.lnz;
     const uint64_t k0 = t.lk0, k1 = std::max(t.lk1, t.lk0);
     t.lkI0 = (uint32_t)std::max<uint64_t>(k0, 1);
@@ -309,9 +309,9 @@ void lattice_plan(DevTiles &t)
         shell += nx * ny;
     shell += (uint64_t)(t.lkI1 - t.lkI0) * (2 * nx + 2 * (ny - 2));
     t.lnshell = (uint32_t)shell;
-    t.lnsb = (uint32_t)(((shell + 255) / 256 + 7) / 8 * 8);
-    t.lnbx = (uint32_t)((nx - 2 + 31) / 32);
-    t.lnby = (uint32_t)((ny - 2 + 7) / 8);
+    t.lnsb = (uint32_t)(((shell + kLatThreads - 1) / kLatThreads + 7) / 8 * 8);
+    t.lnbx = (uint32_t)((nx - 2 + kLatBrickX - 1) / kLatBrickX);
+    t.lnby = (uint32_t)((ny - 2 + kLatBrickY - 1) / kLatBrickY);
     const uint64_t planes = t.lkI1 - t.lkI0, cols = (uint64_t)t.lnbx * t.lnby;
     uint64_t L = (planes * cols + kLatTargetItems - 1) / kLatTargetItems;
     const char *lk = knob("CWF_LAT_L");
