@@ -183,8 +183,9 @@ def same_kernel(kname: str, profiled: str) -> bool:
     """rocprofv3 names a kernel 'ns::name<args>' (optionally with its parameter list): the base name and the
     template arguments must both match, so 'k_keff_tiles' is not taken for 'k_keff_tiles_pipe<...>'."""
     def split(k):
-        k = k.split("(")[0].replace(" ", "")
+        k = k.replace("(anonymous namespace)::", "").split("(")[0].replace(" ", "")
         base, _, args = k.partition("<")
+        args = ",".join(a.split("::")[-1] for a in args.rstrip(">").split(","))  # template args less namespaces
         return base.split("::")[-1], args
 
     return split(kname) == split(profiled)

@@ -538,7 +538,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     bool is_lat = false;
     {
         const char *lv = knob("CWF_LATTICE");
-        if (d->mode == CWF_MODE_FAST && !hex && E && N && N < 0x15555555ull && d->node_coords && !(lv && lv[0] == '0'))
+        if (d->mode == CWF_MODE_FAST && E && N && N < 0x15555555ull && d->node_coords && !(lv && lv[0] == '0'))
         {
             std::string why;
             try
@@ -846,7 +846,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         float *dcf, *part;
         if (int st = upload(h, &dpl, lat.plane.data(), lat.plane.size()))
             return bail(st);
-        if (int st = upload(h, &dcf, lat.coef, (uint64_t)kLatCoef))
+        if (int st = upload(h, &dcf, lat.coef, (uint64_t)(lat.hex ? kLatHexCoef : kLatCoef)))
             return bail(st);
         if (int st = upload(h, &dnpo, npo.data(), npo.size()))
             return bail(st);
@@ -861,6 +861,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.lplane = dpl;
         t.lcoef = dcf;
         t.lsym = lat.sym ? 1 : 0;
+        t.lhex = lat.hex ? 1 : 0;
         t.node_part_off = dnpo;
         t.off_mask = 1;
         t.node_major = 1;
@@ -1442,8 +1443,13 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
         return h->ds.iso ? "k_keff_parity_elem<true, false>" : "k_keff_parity_elem<false, false>";
-    if (t.lat)
-        return "k_keff_lattice<1, false>";
+    if (t.lat)  // as rocprofv3 names it, less the namespaces
+    {
+        static const char *const names[2][2] = {
+            {"k_keff_lattice<1, false, false, LatKuhn>", "k_keff_lattice<1, false, true, LatKuhn>"},
+            {"k_keff_lattice<1, false, false, LatHex>", "k_keff_lattice<1, false, true, LatHex>"}};
+        return names[t.lhex != 0][t.lsym != 0];
+    }
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
     {
         static thread_local char name[96];

@@ -93,6 +93,7 @@ struct DevTiles
     const uint32_t *lplane = nullptr;    // [lnz] storage index of node (0, 0, k)
     const float *lcoef = nullptr;        // [kLatCoef] stencil, cell-pair and face blocks (unscaled by s_K)
     int lsym = 0;                        // S_(-d) == S_d: the paired-direction instantiation
+    int lhex = 0;                        // native hex8 cells: the 27-point instantiation
     // the update pass's preconditioner by node class (when the lumped mass is uniform per boundary class): class =
     // (27 boundary types) << 3 | Dirichlet mask per node, one representative node per class, its packed block
     // inverse and 9-float operator (rebuilt with the per-node inverse)
@@ -180,9 +181,21 @@ constexpr int kLatPairOff[kLatPairs] = {0,  1,  3,  7,  5,  9,  11, 13,  // 0 ->
                                         10, 6,  2,  0,  3,               // 5 -> 0 1 4 5 7
                                         12, 6,  4,  0,  1,               // 6 -> 0 2 4 6 7
                                         14, 12, 10, 6,  8,  4,  2,  0};  // 7 -> 0..7
-// f32 coefficient table: [15][3][3] stencil blocks, then [46][3][3] cell blocks
+// Structured native hex8 blocks (one trilinear hex per cell): all 26 neighbours and the node, the offsets as
+// (+d, -d) pairs after the node itself, and all 64 corner pairs (c, c') of a cell in (c, c') order
+constexpr int kLatHexOffsets = 27, kLatHexPairs = 64;
+constexpr int kLatHexOff[kLatHexOffsets][3] = {
+    {0, 0, 0},   {1, 0, 0},  {-1, 0, 0},  {-1, 1, 0}, {1, -1, 0},  {0, 1, 0},   {0, -1, 0},  {1, 1, 0},  {-1, -1, 0},
+    {-1, -1, 1}, {1, 1, -1}, {0, -1, 1},  {0, 1, -1}, {1, -1, 1},  {-1, 1, -1}, {-1, 0, 1},  {1, 0, -1}, {0, 0, 1},
+    {0, 0, -1},  {1, 0, 1},  {-1, 0, -1}, {-1, 1, 1}, {1, -1, -1}, {0, 1, 1},   {0, -1, -1}, {1, 1, 1},  {-1, -1, -1}};
+constexpr int kLatHexPairOff[kLatHexPairs] = {0,  1,  5,  7,  17, 19, 23, 25, 2,  0,  3,  5,  15, 17, 21, 23,
+                                              6,  4,  0,  1,  11, 13, 17, 19, 8,  6,  2,  0,  9,  11, 15, 17,
+                                              18, 16, 12, 10, 0,  1,  5,  7,  20, 18, 14, 12, 2,  0,  3,  5,
+                                              24, 22, 18, 16, 6,  4,  0,  1,  26, 24, 20, 18, 8,  6,  2,  0};
+// f32 coefficient table: [15][3][3] stencil blocks, then [46][3][3] cell blocks (hex8: [27] and [64])
 constexpr int kLatCoefPairs = 9 * kLatOffsets;
 constexpr int kLatCoef = kLatCoefPairs + 9 * kLatPairs;
+constexpr int kLatHexCoef = 9 * (kLatHexOffsets + kLatHexPairs);
 // k_keff_lattice bricks: kLatBrickX x kLatBrickY columns of the strict interior, one thread per column
 #ifndef CWF_LAT_BY
 #define CWF_LAT_BY 8
@@ -195,8 +208,9 @@ struct Lattice
     uint32_t nx = 0, ny = 0, nz = 0;  // nodes per axis
     std::vector<uint32_t> plane;      // [nz] storage index of node (0, 0, k)
     std::vector<uint32_t> perm;       // when renumbered: internal (lexicographic) index -> caller's node
-    float coef[kLatCoef] = {};
+    float coef[kLatHexCoef] = {};  // Kuhn: the first kLatCoef
     bool sym = false;  // S_(-d) == S_d for every direction (k_keff_lattice's paired form)
+    bool hex = false;  // native hex8 cells (27-point stencil)
 };
 // true when the desc is a Kuhn-split box lattice with one gradient / volume set per Kuhn type (lattice.cpp);
 // allow_perm: the handle may renumber (otherwise the nodes must already be lexicographic within planes)

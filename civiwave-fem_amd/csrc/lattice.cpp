@@ -81,6 +81,191 @@ bool lattice_tables_ok()
     return q == kLatPairs;
 }
 
+// storage order: lexicographic inside every k plane (the caller's order: plane[k] = its node (0, 0, k)), or, when
+// the handle may renumber, the lexicographic order (perm = at)
+bool storage_order(uint64_t N, const uint32_t nn[3], const std::vector<uint32_t> &at, bool allow_perm, Lattice &L)
+{
+    const uint64_t nx = nn[0], ny = nn[1], nz = nn[2];
+    L.nx = (uint32_t)nx;
+    L.ny = (uint32_t)ny;
+    L.nz = (uint32_t)nz;
+    L.plane.assign(nz, 0);
+    L.perm.clear();
+    bool caller_order = true;
+    for (uint64_t k = 0; k < nz && caller_order; ++k)
+    {
+        const uint32_t base = at[k * nx * ny];
+        L.plane[k] = base;
+        if ((uint64_t)base + nx * ny > N)
+            caller_order = false;
+        for (uint64_t j = 0; j < ny && caller_order; ++j)
+            for (uint64_t i = 0; i < nx; ++i)
+                if (at[(k * ny + j) * nx + i] != base + j * nx + i)
+                {
+                    caller_order = false;
+                    break;
+                }
+    }
+    if (caller_order)
+        return true;
+    if (!allow_perm)
+        return false;
+    L.perm = at;
+    for (uint64_t k = 0; k < nz; ++k)
+        L.plane[k] = (uint32_t)(k * nx * ny);
+    return true;
+}
+
+// stencil blocks S_d = sum over the corners c with c + d a corner of Kc[c][c + d], then the cell-pair blocks
+template <int NOFF, int NPAIR>
+void stencil_tables(const double Kc[8][8][3][3], const int (&off)[NOFF][3], const int (&pair)[NPAIR][2], Lattice &L)
+{
+    double S[NOFF][9] = {};
+    double smax = 0.0;
+    for (int o = 0; o < NOFF; ++o)
+    {
+        for (int c = 0; c < 8; ++c)
+        {
+            const int cx = (c & 1) + off[o][0], cy = ((c >> 1) & 1) + off[o][1], cz = ((c >> 2) & 1) + off[o][2];
+            if (cx < 0 || cx > 1 || cy < 0 || cy > 1 || cz < 0 || cz > 1)
+                continue;
+            const int c2 = cx | cy << 1 | cz << 2;
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k)
+                    S[o][3 * r + k] += Kc[c][c2][r][k];
+        }
+        for (double v : S[o])
+            smax = std::max(smax, std::fabs(v));
+    }
+    // paired directions: S_(-d) = S_d^T always; S_d symmetric (S_(-d) = S_d) for an isotropic block. The two are
+    // summed over the cells in different orders, so they agree to fp64 rounding: within 1e-10 of the largest
+    // entry they are taken as equal and both set to their fp64 mean before the f32 rounding
+    L.sym = true;
+    for (int o = 1; o < NOFF; o += 2)
+        for (int j = 0; j < 9; ++j)
+            L.sym = L.sym && std::fabs(S[o][j] - S[o + 1][j]) <= 1e-10 * smax;
+    if (L.sym)
+        for (int o = 1; o < NOFF; o += 2)
+            for (int j = 0; j < 9; ++j)
+                S[o][j] = S[o + 1][j] = 0.5 * (S[o][j] + S[o + 1][j]);
+    for (int o = 0; o < NOFF; ++o)
+        for (int j = 0; j < 9; ++j)
+            L.coef[9 * o + j] = (float)S[o][j];
+    for (int p = 0; p < NPAIR; ++p)
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k)
+                L.coef[9 * (NOFF + p) + 3 * r + k] = (float)Kc[pair[p][0]][pair[p][1]][r][k];
+}
+
+constexpr int kHexPair[kLatHexPairs][2] = {
+#define P8(c) {c, 0}, {c, 1}, {c, 2}, {c, 3}, {c, 4}, {c, 5}, {c, 6}, {c, 7}
+    P8(0), P8(1), P8(2), P8(3), P8(4), P8(5), P8(6), P8(7)
+#undef P8
+};
+
+// native hex8 cells (Gmsh / VTK corner order; slot s sits at corner bits kHexSlotBits[s]): one hex per cell, the
+// cell stiffness from the first hex's corner coordinates (the lattice's, to 1e-6 of the cell: every cell is a
+// translate), 2 x 2 x 2 Gauss in fp64 (the textbook element of oracle/hex8_oracle.c and k_keff_hex_tiles)
+bool detect_hex_cells(const cwf_system_desc *d, const std::vector<uint32_t> &q, const uint32_t nn[3],
+                      const std::vector<uint32_t> &at, bool allow_perm, Lattice &L, std::string *why)
+{
+    const auto fail = [&](const char *m) {
+        if (why)
+            *why = m;
+        return false;
+    };
+    constexpr int kHexSlotBits[8] = {0, 1, 3, 2, 4, 5, 7, 6};
+    const uint64_t N = d->node_count, E = d->element_count, nx = nn[0], ny = nn[1], nz = nn[2];
+    if (E != (nx - 1) * (ny - 1) * (nz - 1))
+        return fail("element count is not one hex per cell");
+    const uint32_t *conn = d->element_connectivity;
+    std::vector<uint8_t> seen(E, 0);
+    for (uint64_t e = 0; e < E; ++e)
+    {
+        const uint32_t *c = &q[3ull * conn[8 * e]];  // slot 0 is the cell's corner (0, 0, 0)
+        if (c[0] >= nx - 1 || c[1] >= ny - 1 || c[2] >= nz - 1)
+            return fail("a hex is not a cell");
+        for (int s = 1; s < 8; ++s)
+        {
+            const uint32_t *qs = &q[3ull * conn[8 * e + s]];
+            const uint32_t ox = qs[0] - c[0], oy = qs[1] - c[1], oz = qs[2] - c[2];
+            if (ox > 1 || oy > 1 || oz > 1 || (int)(ox | oy << 1 | oz << 2) != kHexSlotBits[s])
+                return fail("a hex is not a cell in Gmsh corner order");
+        }
+        const uint64_t cell = ((uint64_t)c[2] * (ny - 1) + c[1]) * (nx - 1) + c[0];
+        if (seen[cell])
+            return fail("two hexes on one cell");
+        seen[cell] = 1;
+    }
+    if (!storage_order(N, nn, at, allow_perm, L))
+        return fail("node order is not lexicographic within planes");
+    double Xc[8][3];  // corner coordinates of the first hex by corner bits
+    for (int s = 0; s < 8; ++s)
+        for (int k = 0; k < 3; ++k)
+            Xc[kHexSlotBits[s]][k] = d->node_coords[3ull * conn[s] + k];
+    const double *D = d->material_stiffness + 36ull * d->element_material_index[0];
+    double Kc[8][8][3][3];
+    std::memset(Kc, 0, sizeof Kc);
+    const double gq = 1.0 / std::sqrt(3.0);
+    for (int gp = 0; gp < 8; ++gp)
+    {
+        const double qp[3] = {(gp & 1) ? gq : -gq, (gp & 2) ? gq : -gq, (gp & 4) ? gq : -gq};
+        double dN[8][3], J[3][3] = {};
+        for (int a = 0; a < 8; ++a)
+        {
+            const double sg[3] = {(a & 1) ? 1.0 : -1.0, (a & 2) ? 1.0 : -1.0, (a & 4) ? 1.0 : -1.0};
+            const double f[3] = {1.0 + sg[0] * qp[0], 1.0 + sg[1] * qp[1], 1.0 + sg[2] * qp[2]};
+            dN[a][0] = 0.125 * sg[0] * f[1] * f[2];
+            dN[a][1] = 0.125 * f[0] * sg[1] * f[2];
+            dN[a][2] = 0.125 * f[0] * f[1] * sg[2];
+            for (int m = 0; m < 3; ++m)
+                for (int l = 0; l < 3; ++l)
+                    J[m][l] += Xc[a][m] * dN[a][l];
+        }
+        double A[3][3];  // adjugate
+        A[0][0] = J[1][1] * J[2][2] - J[1][2] * J[2][1];
+        A[0][1] = J[0][2] * J[2][1] - J[0][1] * J[2][2];
+        A[0][2] = J[0][1] * J[1][2] - J[0][2] * J[1][1];
+        A[1][0] = J[1][2] * J[2][0] - J[1][0] * J[2][2];
+        A[1][1] = J[0][0] * J[2][2] - J[0][2] * J[2][0];
+        A[1][2] = J[0][2] * J[1][0] - J[0][0] * J[1][2];
+        A[2][0] = J[1][0] * J[2][1] - J[1][1] * J[2][0];
+        A[2][1] = J[0][1] * J[2][0] - J[0][0] * J[2][1];
+        A[2][2] = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+        const double det = J[0][0] * A[0][0] + J[0][1] * A[1][0] + J[0][2] * A[2][0];
+        if (!(std::fabs(det) > 0.0))
+            return fail("degenerate hex");
+        double g[8][3];
+        for (int a = 0; a < 8; ++a)
+            for (int m = 0; m < 3; ++m)
+            {
+                double sum = 0.0;
+                for (int l = 0; l < 3; ++l)
+                    sum += dN[a][l] * A[l][m];
+                g[a][m] = sum / det;
+            }
+        for (int a = 0; a < 8; ++a)
+            for (int b = 0; b < 8; ++b)
+            {
+                double Ba[6][3], Bb[6][3];
+                b_block(g[a], Ba);
+                b_block(g[b], Bb);
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k)
+                    {
+                        double sum = 0.0;
+                        for (int i = 0; i < 6; ++i)
+                            for (int j = 0; j < 6; ++j)
+                                sum += Ba[i][r] * D[6 * i + j] * Bb[j][k];
+                        Kc[a][b][r][k] += std::fabs(det) * sum;
+                    }
+            }
+    }
+    stencil_tables(Kc, kLatHexOff, kHexPair, L);
+    L.hex = true;
+    return true;
+}
+
 bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::string *why)
 {
     const auto fail = [&](const char *m) {
@@ -94,20 +279,20 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
         return fail("lattice tables inconsistent");
     if (!E || N < 8 || !d->node_coords)
         return fail("no elements or no node coordinates");
-    if (d->element_connectivity[4] != 0xFFFFFFFFu)
-        return fail("hex8 elements");
+    const bool hex = d->element_connectivity[4] != 0xFFFFFFFFu;
+    const int K = hex ? 8 : 4;
     const uint32_t *conn = d->element_connectivity;
     const double *X = d->node_coords;
     const uint32_t m0 = d->element_material_index[0];
     for (uint64_t e = 0; e < E; ++e)
         if (d->element_material_index[e] != m0)
             return fail("more than one material");
-    // cell size from the first tet (a Kuhn tet spans its whole cell: it holds corners 0 and 7)
+    // cell size from the first element (a Kuhn tet spans its whole cell: it holds corners 0 and 7)
     double h[3], lo[3];
     for (int k = 0; k < 3; ++k)
     {
         double a = X[3ull * conn[0] + k], b = a;
-        for (int s = 1; s < 4; ++s)
+        for (int s = 1; s < K; ++s)
         {
             a = std::min(a, X[3ull * conn[s] + k]);
             b = std::max(b, X[3ull * conn[s] + k]);
@@ -125,9 +310,11 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
     for (uint64_t n = 0; n < N; ++n)
         for (int k = 0; k < 3; ++k)
         {
+            // tets: the element records define the operator (checked below), so coordinates only place the nodes;
+            // hex8: the operator is formed from the coordinates, so they must be the lattice's
             const double f = (X[3 * n + k] - lo[k]) / h[k];
             const double r = std::nearbyint(f);
-            if (!(std::fabs(f - r) <= 1e-3) || r >= 1048576.0)
+            if (!(std::fabs(f - r) <= (hex ? 1e-6 : 1e-3)) || r >= 1048576.0)
                 return fail("nodes off the lattice");
             q[3 * n + k] = (uint32_t)r;
             nn[k] = std::max(nn[k], (uint32_t)r + 1u);
@@ -144,6 +331,8 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
         at[li] = (uint32_t)n;
     }
     const uint64_t C = (nx - 1) * (ny - 1) * (nz - 1);
+    if (hex)
+        return detect_hex_cells(d, q, nn, at, allow_perm, L, why);
     if (E != 6 * C)
         return fail("element count is not 6 per cell");
     // every tet a Kuhn tet of one cell, each of a cell's 6 types once; gradients / volume per type
@@ -208,35 +397,9 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
                 if (!(std::fabs((double)g[3 * s + k] - G[t][bits[s]][k]) <= 1e-6 * gmax[t]))
                     return fail("element gradients differ within a Kuhn type");
     }
-    // storage order: lexicographic inside every k plane (caller order), or renumbered
-    L.nx = (uint32_t)nx;
-    L.ny = (uint32_t)ny;
-    L.nz = (uint32_t)nz;
-    L.plane.assign(nz, 0);
-    L.perm.clear();
-    bool caller_order = true;
-    for (uint64_t k = 0; k < nz && caller_order; ++k)
-    {
-        const uint32_t base = at[k * nx * ny];
-        L.plane[k] = base;
-        if ((uint64_t)base + nx * ny > N)
-            caller_order = false;
-        for (uint64_t j = 0; j < ny && caller_order; ++j)
-            for (uint64_t i = 0; i < nx; ++i)
-                if (at[(k * ny + j) * nx + i] != base + j * nx + i)
-                {
-                    caller_order = false;
-                    break;
-                }
-    }
-    if (!caller_order)
-    {
-        if (!allow_perm)
-            return fail("node order is not lexicographic within planes");
-        L.perm = at;
-        for (uint64_t k = 0; k < nz; ++k)
-            L.plane[k] = (uint32_t)(k * nx * ny);
-    }
+    if (!storage_order(N, nn, at, allow_perm, L))
+        return fail("node order is not lexicographic within planes");
+    L.hex = false;
     // cell stiffness Kc[c][c'] = sum over the cell's tets of vol B_c^T D B_c' (fp64, pcg.cpp:622-651 products)
     const double *D = d->material_stiffness + 36ull * m0;
     double Kc[8][8][3][3];
@@ -259,34 +422,8 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
                         Kc[a][b][r][k] += V[t] * sum;
                     }
             }
-    // interior stencil, offsets in lattice.inc's order; then the cell-pair blocks
-    for (int o = 0; o < kLatOffsets; ++o)
-    {
-        const int dx = kLatOff[o][0], dy = kLatOff[o][1], dz = kLatOff[o][2];
-        double S[3][3] = {};
-        for (int c = 0; c < 8; ++c)
-        {
-            const int cx = (c & 1) + dx, cy = ((c >> 1) & 1) + dy, cz = ((c >> 2) & 1) + dz;
-            if (cx < 0 || cx > 1 || cy < 0 || cy > 1 || cz < 0 || cz > 1)
-                continue;
-            const int c2 = cx | cy << 1 | cz << 2;
-            for (int r = 0; r < 3; ++r)
-                for (int k = 0; k < 3; ++k)
-                    S[r][k] += Kc[c][c2][r][k];
-        }
-        for (int r = 0; r < 3; ++r)
-            for (int k = 0; k < 3; ++k)
-                L.coef[9 * o + 3 * r + k] = (float)S[r][k];
-    }
-    for (int p = 0; p < kLatPairs; ++p)
-        for (int r = 0; r < 3; ++r)
-            for (int k = 0; k < 3; ++k)
-                L.coef[9 * (kLatOffsets + p) + 3 * r + k] = (float)Kc[kLatPair[p][0]][kLatPair[p][1]][r][k];
     // every block outside the Kuhn pattern is structurally zero (never accumulated): nothing to check
-    // paired directions: S_(-d) = S_d (an isotropic Kuhn block's blocks are symmetric and S_(-d) = S_d^T)
-    L.sym = true;
-    for (int o = 1; o < kLatOffsets; o += 2)
-        L.sym = L.sym && std::memcmp(L.coef + 9 * o, L.coef + 9 * (o + 1), 9 * sizeof(float)) == 0;
+    stencil_tables(Kc, kLatOff, kLatPair, L);
     return true;
 }
 
@@ -333,7 +470,9 @@ extern "C" int cwf_lattice_describe(const cwf_system_desc *desc, int renumber, u
     if (!desc || !dims || !coef || !desc->element_connectivity || !desc->element_gradients || !desc->element_volume ||
         !desc->element_material_index || !desc->material_stiffness)
         return CWF_ERR_ARGUMENT;
-    if (desc->mode != CWF_MODE_FAST || desc->node_count >= 0x15555555ull)  // 12-B rows addressable by 32-bit offsets
+    // tet4 blocks (the reference's element; native hex8 blocks run the 27-point instantiation and are not described)
+    if (desc->mode != CWF_MODE_FAST || desc->node_count >= 0x15555555ull || !desc->element_count ||
+        desc->element_connectivity[4] != 0xFFFFFFFFu)
         return 0;
     for (uint64_t e = 0; e < desc->element_count; ++e)
     {
@@ -349,7 +488,7 @@ extern "C" int cwf_lattice_describe(const cwf_system_desc *desc, int renumber, u
     dims[0] = L.nx;
     dims[1] = L.ny;
     dims[2] = L.nz;
-    std::memcpy(coef, L.coef, sizeof L.coef);
+    std::memcpy(coef, L.coef, sizeof(float) * cwf::kLatCoef);
     dims[0] |= L.sym ? 0x80000000u : 0u;
     if (plane)
         std::memcpy(plane, L.plane.data(), L.plane.size() * sizeof(uint32_t));

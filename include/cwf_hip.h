@@ -148,7 +148,8 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
  * "k_keff_tiles_pipe", "k_keff_tiles", "k_keff_hex_tiles" or "k_keff_parity"); NULL for a NULL handle. */
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
 /* Structured-block introspection (host only, no device; not a reference interface): whether a FAST handle
- * created from `desc` runs the structured Kuhn-block stencil (lattice.cpp). Returns 1 and fills dims (nodes per
+ * created from the tet4 `desc` runs the structured Kuhn-block stencil (lattice.cpp; native hex8 blocks run their
+ * own 27-point stencil and are not described here). Returns 1 and fills dims (nodes per
  * axis; bit 31 of dims[0]: the stencil pairs S_(-d) = S_d), coef (CWF_LATTICE_COEFS floats, row-major 3x3 blocks
  * unscaled by stiffness_scale: the 15 interior stencil blocks, then the 46 cell-pair blocks) and plane ([dims[2]] storage index of node (0, 0, k); NULL: not wanted) when it does, 0 when it
  * does not, a negative cwf_status code on bad arguments. `renumber` != 0 allows the lexicographic renumbering a handle

@@ -172,10 +172,28 @@ def test_gpu_hex8_apply_keff_matches_oracle(hcase):
     assert np.array_equal(y[mask != 0], x[mask != 0])  # Dirichlet rows pass x through
 
 
+def _keff_kernel(s):
+    return (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
+
+
+@pytest.mark.gpu
+def test_gpu_hex8_structured_blocks_run_the_lattice_stencil(hcase):
+    """A structured hex block (every hex a cell of one box lattice) runs the 27-point stencil of the shared
+    trilinear cell stiffness (lattice.cpp); a jittered one the hex tiles. Either way the apply test above holds."""
+    kern = _keff_kernel(gpu_hex_system(hcase))
+    # an isotropic block's stencil is point-symmetric (S_-d = S_d): the paired-direction instantiation
+    assert kern == ("k_keff_hex_tiles" if hcase.name.endswith("-jitter") else "k_keff_lattice<1, false, true, LatHex>")
+
+
 @pytest.mark.gpu
 def test_gpu_hex8_256_lane_tiles_apply_and_solve(hcase, monkeypatch):
-    """The 256-lane hex tiles (the default from 1M hexes; CWF_HEX_NT=256 forces them here) keep the apply
-    tolerance and the PCG solution of the 128-lane tiles."""
+    """The 256-lane hex tiles (the default from 1M hexes; CWF_HEX_NT=256 forces them here, with the structured-block
+    stencil off) keep the apply tolerance and the PCG solution of the 128-lane tiles, and the lattice stencil's."""
+    rhs = hcase.static_rhs()
+    xl = np.zeros_like(rhs)
+    pcg.solve_pcg(gpu_hex_system(hcase), rhs, pcg.PcgSettings(2000, 1e-6),
+                  pcg.PcgVectors(xl, np.zeros_like(rhs))).value()
+    monkeypatch.setenv("CWF_LATTICE", "0")
     monkeypatch.setenv("CWF_HEX_NT", "256")
     s = gpu_hex_system(hcase)
     P = hcase.packing
@@ -193,9 +211,11 @@ def test_gpu_hex8_256_lane_tiles_apply_and_solve(hcase, monkeypatch):
     assert t.converged
     monkeypatch.setenv("CWF_HEX_NT", "128")
     x128 = np.zeros_like(rhs)
-    pcg.solve_pcg(gpu_hex_system(hcase), rhs, pcg.PcgSettings(2000, 1e-6),
-                  pcg.PcgVectors(x128, np.zeros_like(rhs))).value()
+    s128 = gpu_hex_system(hcase)
+    assert _keff_kernel(s128).startswith("k_keff_hex_tiles")
+    pcg.solve_pcg(s128, rhs, pcg.PcgSettings(2000, 1e-6), pcg.PcgVectors(x128, np.zeros_like(rhs))).value()
     assert np.linalg.norm(x256 - x128) <= 1e-4 * np.linalg.norm(x128)
+    assert np.linalg.norm(xl - x128) <= 1e-4 * np.linalg.norm(x128)
 
 
 @pytest.mark.gpu
