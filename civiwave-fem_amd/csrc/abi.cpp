@@ -898,6 +898,12 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                         else if (std::memcmp(&tmass[ty], &d->lumped_mass[n], sizeof(float)) != 0)
                             uniform = false;
                     }
+            const char *lm = knob("CWF_LAT_MASS");
+            if (uniform && tseen[13] && !(lm && lm[0] == '0'))  // type 13: inside along x, y and z (the bricks' nodes)
+            {
+                t.lmu = 1;
+                t.lmass = tmass[13];
+            }
             if (uniform)
             {
                 uint8_t *dcls;
@@ -1416,9 +1422,9 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
-        if (s.t.lat)  // per owned node: z and p_old read, mass read, the new p and the row value written
-        {
-            *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 4 + 12 + 12);
+        if (s.t.lat)  // per owned node: z and p_old read, the new p and the row value written; the mass read
+        {             // (only the shell's when the strict interior's is one value, lmu)
+            *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 12 + 12) + 4ull * (s.t.lmu ? s.t.lnshell : s.Nown);
             return 0;
         }
         if (s.t.grp)
@@ -1445,10 +1451,10 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
         return h->ds.iso ? "k_keff_parity_elem<true, false>" : "k_keff_parity_elem<false, false>";
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {
-        static const char *const names[2][2] = {
-            {"k_keff_lattice<1, false, false, LatKuhn>", "k_keff_lattice<1, false, true, LatKuhn>"},
-            {"k_keff_lattice<1, false, false, LatHex>", "k_keff_lattice<1, false, true, LatHex>"}};
-        return names[t.lhex != 0][t.lsym != 0];
+        static thread_local char name[96];
+        snprintf(name, sizeof name, "k_keff_lattice<1, false, %s, %s, %s>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false");
+        return name;
     }
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
     {

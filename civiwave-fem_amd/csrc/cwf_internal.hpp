@@ -90,6 +90,8 @@ struct DevTiles
     // computed planes, lnshell of them), then lnbx * lnby * ceil((lkI1 - lkI0) / lL) interior bricks (32 x 8
     // columns of the strict interior i, j in [1, n - 1) times lL planes of [lkI0, lkI1)); lnwork = all of them
     uint32_t lnbx = 0, lnby = 0, lL = 0, lnwork = 0, lnwm = 0, lnsb = 0, lnshell = 0, lkI0 = 0, lkI1 = 0;
+    int lmu = 0;                         // every strict-interior node's lumped mass is lmass (the bricks read none)
+    float lmass = 0.f;
     const uint32_t *lplane = nullptr;    // [lnz] storage index of node (0, 0, k)
     const float *lcoef = nullptr;        // [kLatCoef] stencil, cell-pair and face blocks (unscaled by s_K)
     int lsym = 0;                        // S_(-d) == S_d: the paired-direction instantiation
@@ -197,10 +199,7 @@ constexpr int kLatCoefPairs = 9 * kLatOffsets;
 constexpr int kLatCoef = kLatCoefPairs + 9 * kLatPairs;
 constexpr int kLatHexCoef = 9 * (kLatHexOffsets + kLatHexPairs);
 // k_keff_lattice bricks: kLatBrickX x kLatBrickY columns of the strict interior, one thread per column
-#ifndef CWF_LAT_BY
-#define CWF_LAT_BY 8
-#endif
-constexpr int kLatBrickX = 32, kLatBrickY = CWF_LAT_BY, kLatThreads = kLatBrickX * kLatBrickY;
+constexpr int kLatBrickX = 32, kLatBrickY = 8, kLatThreads = kLatBrickX * kLatBrickY;
 constexpr uint32_t kLatClasses = 27 * 8;  // (boundary type along x, y, z: lo / inside / hi) x Dirichlet mask
 
 struct Lattice

@@ -29,6 +29,7 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_HEX_NT", "128|256: lanes of the hex8 tiles (tests/test_hex8.py)"},
     {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
     {"CWF_LATTICE", "0: no structured-block stencil (lattice.cpp); structured Kuhn (hex8) blocks then run the fan groups (hex tiles)"},
+    {"CWF_LAT_MASS", "0: the lattice bricks read the per-node mass even when the strict interior's is uniform"},
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},

@@ -429,12 +429,12 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
 
 // Work items: the surface shell of the computed planes [lk0, lk1), one node per thread (256-thread workgroups,
 // rounded up to whole XCD groups so the bricks after them keep the XCD mapping), then 32 x 8 column bricks of the
-// strict interior times L planes, L sized for about kLatTargetItems bricks (one round of resident workgroups: three
-// or four per CU on 256 CUs) and at least 4 (each brick reads L + 2 planes). Measured (k_keff_lattice in the PCG
-// loop, one MI355X): C2 L = 2 / 4 / 8 / 16: 18.5 / 16.4 / 17.5 / 20.6 us; C3 L = 4 / 8 / 16 / 24: 76 / 69 / 70 / 73 us
+// strict interior times L planes, L sized for about kLatTargetItems bricks (one round of resident workgroups: four
+// per CU on 256 CUs) and at least 4 (each brick reads L + 2 planes). Measured (k_keff_lattice in the PCG loop, one
+// MI355X): C2 L = 2 / 4 / 8 / 16: 18.5 / 16.4 / 17.5 / 20.6 us; C3 L = 4 / 8 / 16 / 24: 76 / 69 / 70 / 73 us
 void lattice_plan(DevTiles &t)
 {
-    constexpr uint64_t kLatTargetItems = 262144 / kLatThreads;  // 1024 bricks of 256 threads, 512 of 512
+    constexpr uint64_t kLatTargetItems = 262144 / kLatThreads;  // 1024 bricks of 256 threads
     const uint64_t nx = t.lnx, ny = t.lny, nz = t.lnz;
     const uint64_t k0 = t.lk0, k1 = std::max(t.lk1, t.lk0);
     t.lkI0 = (uint32_t)std::max<uint64_t>(k0, 1);

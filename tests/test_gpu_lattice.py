@@ -115,6 +115,29 @@ def test_lattice_solve_close(case):
     assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
 
 
+@pytest.mark.parametrize("mass", ["uniform", "per-node"])
+def test_lattice_mass_sources_solve(mass, monkeypatch):
+    """The PCG-loop bricks with both mass sources (the strict interior's one lumped mass as a kernel argument, or
+    the per-node mass through LDS: CWF_LAT_MASS=0) solve to the oracle's solution; bricks cut by the faces in x, y
+    and k."""
+    if mass == "per-node":
+        monkeypatch.setenv("CWF_LAT_MASS", "0")
+    monkeypatch.setenv("CWF_LAT_L", "3")
+    case = scenarios.block_case(40, 19, 9, h=0.1, tol=1e-6, max_iterations=1500)
+    s = _system(case)
+    assert _kernel(s).endswith(f", {'true' if mass == 'uniform' else 'false'}>")
+    assert _apply_err(case, s, seed=5) <= 2e-5
+    o = oracle_system(case.packing, case.materials, *case.scalars())
+    rhs = case.static_rhs()
+    x = np.zeros_like(rhs)
+    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(1500, 1e-6), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
+    ref = o.solve_pcg(rhs, 1500, 1e-6)
+    assert t.converged and ref["telemetry"].converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    n_ref = ref["telemetry"].iterations
+    assert abs(t.iterations - n_ref) <= max(3, n_ref // 10)
+
+
 def test_lattice_stepper_steps():
     case = scenarios.block_case(10, 5, 6, h=0.1, xi=0.05, w=(10.0, 100.0), tol=1e-6, max_iterations=1500)
     P = case.packing

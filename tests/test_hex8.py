@@ -182,7 +182,8 @@ def test_gpu_hex8_structured_blocks_run_the_lattice_stencil(hcase):
     trilinear cell stiffness (lattice.cpp); a jittered one the hex tiles. Either way the apply test above holds."""
     kern = _keff_kernel(gpu_hex_system(hcase))
     # an isotropic block's stencil is point-symmetric (S_-d = S_d): the paired-direction instantiation
-    assert kern == ("k_keff_hex_tiles" if hcase.name.endswith("-jitter") else "k_keff_lattice<1, false, true, LatHex>")
+    want = "k_keff_hex_tiles" if hcase.name.endswith("-jitter") else "k_keff_lattice<1, false, true, LatHex,"
+    assert kern.startswith(want), kern
 
 
 @pytest.mark.gpu
