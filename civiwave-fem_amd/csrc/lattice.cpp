@@ -429,9 +429,12 @@ bool detect_lattice(const cwf_system_desc *d, bool allow_perm, Lattice &L, std::
 
 // Work items: the surface shell of the computed planes [lk0, lk1), one node per thread (256-thread workgroups,
 // rounded up to whole XCD groups so the bricks after them keep the XCD mapping), then 32 x 8 column bricks of the
-// strict interior times L planes, L sized for about kLatTargetItems bricks (one round of resident workgroups: four
-// per CU on 256 CUs) and at least 4 (each brick reads L + 2 planes). Measured (k_keff_lattice in the PCG loop, one
-// MI355X): C2 L = 2 / 4 / 8 / 16: 18.5 / 16.4 / 17.5 / 20.6 us; C3 L = 4 / 8 / 16 / 24: 76 / 69 / 70 / 73 us
+// strict interior times L planes. L = 6 while the brick columns are fewer than one round of resident workgroups
+// (1024: four per CU), else one column's planes per brick (about kLatTargetItems bricks). Measured (PCG it/s, same
+// box, two passes, k_keff_lattice with the uniform mass): C2 (27 columns) L = 3 / 4 / 5 / 6 / 7 / 8: 40.2k / 40.1k
+// / 41.6k / 41.6k / 39.3k / 39.5k; C3 (95 columns) L = 5 / 6 / 7 / 8 / 9 / 11 / 14 / 20 / 28: 58.8-60.9 / 54.3-57.9
+// / 56.4-61.0 / 54.0-58.0 / 55.1-55.9 / 56.0-59.8 / 55.4-59.9 / 60.1-62.4 / 67.0-69.0 us; C3 hex8 L = 6 / 12 /
+// 14 / 24: 65.4 / 66.6 / 68.0 / 75.4 us; C5 (1250 columns) L = 6 / 12 / 24 / 48 (all): 252 / 242 / 267 / 224 us
 void lattice_plan(DevTiles &t)
 {
     constexpr uint64_t kLatTargetItems = 262144 / kLatThreads;  // 1024 bricks of 256 threads
@@ -450,7 +453,7 @@ void lattice_plan(DevTiles &t)
     t.lnbx = (uint32_t)((nx - 2 + kLatBrickX - 1) / kLatBrickX);
     t.lnby = (uint32_t)((ny - 2 + kLatBrickY - 1) / kLatBrickY);
     const uint64_t planes = t.lkI1 - t.lkI0, cols = (uint64_t)t.lnbx * t.lnby;
-    uint64_t L = (planes * cols + kLatTargetItems - 1) / kLatTargetItems;
+    uint64_t L = cols < kLatTargetItems ? 6 : (planes * cols + kLatTargetItems - 1) / kLatTargetItems;
     const char *lk = knob("CWF_LAT_L");
     if (lk && atoi(lk) > 0)
         L = (uint64_t)atoi(lk);
