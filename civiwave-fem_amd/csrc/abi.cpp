@@ -903,6 +903,12 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             {
                 t.lmu = 1;
                 t.lmass = tmass[13];
+                // z from r in the K_eff pass, no z store in the update pass (attach turns it off, comm.cpp): from
+                // 2M nodes, where the iteration's vectors leave the 256 MB MALL and the 12 B per node the update
+                // pass no longer writes are HBM bytes (C3 +4-5% PCG it/s); on C2 the K_eff pass's class-table fill
+                // and the 3 x 3 products per halo entry sit on its latency-bound critical path (-8%), same box
+                const char *zr = knob("CWF_LAT_ZR");
+                t.lzr = zr ? (zr[0] == '1' ? 1 : 0) : (N >= (1ull << 21) ? 1 : 0);
             }
             if (uniform)
             {
@@ -1424,7 +1430,8 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
         if (s.t.lat)  // per owned node: z and p_old read, the new p and the row value written; the mass read
         {             // (only the shell's when the strict interior's is one value, lmu)
-            *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 12 + 12) + 4ull * (s.t.lmu ? s.t.lnshell : s.Nown);
+            *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 12 + 12 + (s.t.lmu && s.t.lzr ? 1 : 0)) +
+                            4ull * (s.t.lmu ? s.t.lnshell : s.Nown);
             return 0;
         }
         if (s.t.grp)
@@ -1452,8 +1459,8 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {
         static thread_local char name[96];
-        snprintf(name, sizeof name, "k_keff_lattice<1, false, %s, %s, %s>", t.lsym ? "true" : "false",
-                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false");
+        snprintf(name, sizeof name, "k_keff_lattice<1, false, %s, %s, %s, %s>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lmu && t.lzr ? "true" : "false");
         return name;
     }
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)

@@ -589,6 +589,7 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
             }
         t.lk0 = k0 < k1 ? k0 : 0;
         t.lk1 = k0 < k1 ? k1 : 1;
+        t.lzr = 0;  // the update pass stores z: the halo exchange carries z, and a ghost's class is a local one
         lattice_plan(t);
     }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;

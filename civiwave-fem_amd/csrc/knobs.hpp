@@ -30,6 +30,8 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
     {"CWF_LATTICE", "0: no structured-block stencil (lattice.cpp); structured Kuhn (hex8) blocks then run the fan groups (hex tiles)"},
     {"CWF_LAT_MASS", "0: the lattice bricks read the per-node mass even when the strict interior's is uniform"},
+    {"CWF_LAT_ZR", "0|1: the lattice update pass stores z / the K_eff pass forms z from r and the node class "
+                   "(default: the latter from 2M nodes)"},
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},

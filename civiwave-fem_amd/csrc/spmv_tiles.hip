@@ -1473,7 +1473,7 @@ struct UpdNode
 // r -= alpha Ap, Dirichlet, z = M^-1 r (16-B Jacobi-scaled block, blockinv_pack.hpp), r.r / r.z shares;
 // x += alpha_j p_j for the last `lag` iterations every lag-th iteration (lazy x, 1 = every iteration; the
 // FMA chain in iteration order is bitwise the eager update), fast_flush_x applies the rest after the solve.
-template <int U, bool XF, bool LAT>
+template <int U, bool XF, bool LAT, bool NOZ = false>
 __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, const float *__restrict__ inv9,
     float *__restrict__ x, float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold,
@@ -1707,7 +1707,8 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
                 rr += (double)rv[k] * (double)rv[k];
                 rz += (double)rv[k] * (double)zk;
             }
-            store3(z, whole_rsrc(z), n, zs[0], zs[1], zs[2], wt);
+            if constexpr (!NOZ)  // NOZ (lattice lzr): the K_eff pass forms z from r itself
+                store3(z, whole_rsrc(z), n, zs[0], zs[1], zs[2], wt);
         }
     }
     // ghost nodes of a shard: only the search direction (the tiles kernel's p) is kept
@@ -2010,11 +2011,13 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e
     const unsigned abl = 0u;
     // beta / convergence: a single handle folds the update kernel's per-workgroup {r.r, r.z} shares
     // directly; a shard reads the all-gathered per-rank pairs
+    // lzr: the lattice kernel forms z from r (pa.z carries r)
+    const float *pz = s.t.lzr ? h->r : h->z;
     PcgArgs pa = fast_direct_fold(h)
-                     ? PcgArgs{h->z, h->ctl, h->part0, h->part1, h->part2,
+                     ? PcgArgs{pz, h->ctl, h->part0, h->part1, h->part2,
                                fast_update_blocks(s, it && x_flush_iter(it - 1u)), 1u, it, h->hist, abl,
                                fast_p_new(h, it)}
-                     : PcgArgs{h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
+                     : PcgArgs{pz, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
                                (unsigned)h->nranks, 2u, it, h->hist, abl, fast_p_new(h, it)};
     if (s.iso)
         launch_tiles<true, false, 1>(s, fast_p_old(h, it), pa, tile_threads(), st, e0, e1);
@@ -2028,8 +2031,9 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
     const bool direct = fast_direct_fold(h);
     const bool xf = x_flush_iter(it);
     const bool lat = s.t.lcls != nullptr;
-    const auto k = lat ? (xf ? k_pcg_update_tiles<1, true, true> : k_pcg_update_tiles<1, false, true>)
-                       : (xf ? k_pcg_update_tiles<1, true, false> : k_pcg_update_tiles<1, false, false>);
+    const auto k = lat && s.t.lzr ? (xf ? k_pcg_update_tiles<1, true, true, true> : k_pcg_update_tiles<1, false, true, true>)
+                   : lat ? (xf ? k_pcg_update_tiles<1, true, true> : k_pcg_update_tiles<1, false, true>)
+                         : (xf ? k_pcg_update_tiles<1, true, false> : k_pcg_update_tiles<1, false, false>);
     k<<<fast_update_blocks(s, xf), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
         direct ? h->part0 : h->g_pap, direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it,
@@ -2049,7 +2053,7 @@ void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st)
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    PcgArgs pa{h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
+    PcgArgs pa{s.t.lzr ? h->r : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
                h->hist, abl | 32u};
     for (int i = 0; i < reps; ++i)
         launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);

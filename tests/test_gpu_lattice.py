@@ -115,17 +115,21 @@ def test_lattice_solve_close(case):
     assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
 
 
-@pytest.mark.parametrize("mass", ["uniform", "per-node"])
-def test_lattice_mass_sources_solve(mass, monkeypatch):
-    """The PCG-loop bricks with both mass sources (the strict interior's one lumped mass as a kernel argument, or
-    the per-node mass through LDS: CWF_LAT_MASS=0) solve to the oracle's solution; bricks cut by the faces in x, y
-    and k."""
-    if mass == "per-node":
+@pytest.mark.parametrize("variant", ["z-from-r", "z-stored", "per-node-mass"])
+def test_lattice_pcg_variants_solve(variant, monkeypatch):
+    """The PCG-loop bricks in their three forms solve to the oracle's solution (bricks cut by the faces in x, y and
+    k): the strict interior's one lumped mass as a kernel argument with z = M^-1 r formed from r and the node
+    class in the K_eff pass and no z stored by the update pass (CWF_LAT_ZR=1, the default from 2M nodes), or with z
+    stored by the update pass (CWF_LAT_ZR=0, the default below), and the per-node mass through LDS
+    (CWF_LAT_MASS=0, which also stores z)."""
+    monkeypatch.setenv("CWF_LAT_ZR", "1" if variant == "z-from-r" else "0")
+    if variant == "per-node-mass":
         monkeypatch.setenv("CWF_LAT_MASS", "0")
     monkeypatch.setenv("CWF_LAT_L", "3")
     case = scenarios.block_case(40, 19, 9, h=0.1, tol=1e-6, max_iterations=1500)
     s = _system(case)
-    assert _kernel(s).endswith(f", {'true' if mass == 'uniform' else 'false'}>")
+    tail = {"z-from-r": ", true, true>", "z-stored": ", true, false>", "per-node-mass": ", false, false>"}[variant]
+    assert _kernel(s).endswith(tail)
     assert _apply_err(case, s, seed=5) <= 2e-5
     o = oracle_system(case.packing, case.materials, *case.scalars())
     rhs = case.static_rhs()
