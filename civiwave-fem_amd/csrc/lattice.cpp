@@ -461,6 +461,11 @@ void lattice_plan(DevTiles &t)
     t.lL = (uint32_t)L;
     t.lnwm = (uint32_t)(cols * ((planes + L - 1) / L));
     t.lnwork = t.lnsb + t.lnwm;
+    // the shell workgroups lead the bricks when the grid takes several rounds of resident workgroups (C3: 2.8
+    // rounds, shell last -2.6%) and follow them when it fits in one (C2: 436 workgroups, shell last +6.2%, keff 14.2
+    // -> 12.9 us; same box, two passes)
+    const char *sl = knob("CWF_LAT_SHELL_LAST");
+    t.lshl = sl ? (sl[0] == '1' ? 1 : 0) : (t.lnwork <= kLatTargetItems ? 1 : 0);
     t.ntiles = t.lnwork;
 }
 

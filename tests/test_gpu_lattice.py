@@ -80,10 +80,13 @@ def test_lattice_off_runs_the_fan_groups(case, monkeypatch):
     assert _apply_err(case, s) <= 2e-5
 
 
+@pytest.mark.parametrize("shell", ["lead", "follow"])
 @pytest.mark.parametrize("L", ["2", "3", "64"])
-def test_lattice_work_item_lengths(L, monkeypatch):
-    """Planes per work item (CWF_LAT_L): chunk boundaries inside the block and one chunk over all planes."""
+def test_lattice_work_item_lengths(L, shell, monkeypatch):
+    """Planes per work item (CWF_LAT_L): chunk boundaries inside the block and one chunk over all planes; the shell
+    workgroups before or after the bricks (CWF_LAT_SHELL_LAST)."""
     monkeypatch.setenv("CWF_LAT_L", L)
+    monkeypatch.setenv("CWF_LAT_SHELL_LAST", "1" if shell == "follow" else "0")
     case = scenarios.block_case(40, 17, 9, h=0.1, tol=1e-6)
     assert _apply_err(case, _system(case), seed=11) <= 2e-5
 
