@@ -846,7 +846,17 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         float *dcf, *part;
         if (int st = upload(h, &dpl, lat.plane.data(), lat.plane.size()))
             return bail(st);
-        if (int st = upload(h, &dcf, lat.coef, (uint64_t)(lat.hex ? kLatHexCoef : kLatCoef)))
+        // the device copy's stencil blocks are stored row-pair interleaved for the packed rows of k_keff_lattice:
+        // per offset {S00 S10 S01 S11 S02 S12 S20 S21 S22}; the cell-pair blocks after them keep row-major order
+        std::vector<float> cdev(lat.coef, lat.coef + (lat.hex ? kLatHexCoef : kLatCoef));
+        for (int o = 0; o < (lat.hex ? kLatHexOffsets : kLatOffsets); ++o)
+            for (int c = 0; c < 3; ++c)
+            {
+                cdev[9 * o + 2 * c] = lat.coef[9 * o + c];
+                cdev[9 * o + 2 * c + 1] = lat.coef[9 * o + 3 + c];
+                cdev[9 * o + 6 + c] = lat.coef[9 * o + 6 + c];
+            }
+        if (int st = upload(h, &dcf, cdev.data(), (uint64_t)cdev.size()))
             return bail(st);
         if (int st = upload(h, &dnpo, npo.data(), npo.size()))
             return bail(st);
