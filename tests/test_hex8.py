@@ -187,6 +187,23 @@ def test_gpu_hex8_structured_blocks_run_the_lattice_stencil(hcase):
 
 
 @pytest.mark.gpu
+def test_gpu_hex8_lattice_z_from_r_solve(monkeypatch):
+    """The hex8 lattice with z formed from r in the K_eff pass (CWF_LAT_ZR=1, the default from 2M nodes) solves to
+    the stored-z solution (the same p bit for bit; the iteration count equal up to the initial z's source)."""
+    case = GPU_CASES["tiles"]()
+    rhs = case.static_rhs()
+    xs = {}
+    for zr in ("0", "1"):
+        monkeypatch.setenv("CWF_LAT_ZR", zr)
+        s = gpu_hex_system(case)
+        assert _keff_kernel(s).endswith(", true, true>" if zr == "1" else ", true, false>")
+        xs[zr] = np.zeros_like(rhs)
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(2000, 1e-6), pcg.PcgVectors(xs[zr], np.zeros_like(rhs))).value()
+        assert t.converged
+    assert np.linalg.norm(xs["1"] - xs["0"]) <= 1e-4 * np.linalg.norm(xs["0"])
+
+
+@pytest.mark.gpu
 def test_gpu_hex8_256_lane_tiles_apply_and_solve(hcase, monkeypatch):
     """The 256-lane hex tiles (the default from 1M hexes; CWF_HEX_NT=256 forces them here, with the structured-block
     stencil off) keep the apply tolerance and the PCG solution of the 128-lane tiles, and the lattice stencil's."""
