@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-iterations", type=int, default=40)
     ap.add_argument("--no-general-roofline", action="store_true",
                     help="skip roofline_general (the fan-group tiles kernel on C3 with the lattice stencil off)")
+    ap.add_argument("--no-general", action="store_true",
+                    help="skip the 'general' block (the same workload on the fan-group tiles, CWF_LATTICE=0)")
     ap.add_argument("--no-hbm-roofline", action="store_true",
                     help="skip the live configs[2] K_eff roofline (N=1 runs of configs other than c3 add it)")
     ap.add_argument("--traffic", default="auto",
@@ -174,6 +176,70 @@ def hbm_roofline(L, device, key="c3", steps=2, sample=5, general=False):
            "launches": int(n.value), "algorithmic_bytes_per_launch": float(lay_b.value),
            "reference_layout_equiv_gbs": ref_b.value / (avg * 1e-3) / 1e9}
     out["traffic"], out["traffic_source"] = c3_pmc_traffic(out["kernel"])
+    st.close()
+    st.system.close()
+    return out
+
+
+def operator_of(kname: str) -> str:
+    """Which operator a K_eff kernel name is: the structured-block stencil (reached only by exact structured Kuhn /
+    hex8 boxes of one material, lattice.cpp) or the general element tiles every other mesh runs."""
+    if kname.startswith("k_cg_lattice"):
+        return "structured-block stencil, single-launch (Chronopoulos-Gear) PCG iteration"
+    if kname.startswith("k_keff_lattice"):
+        return "structured-block stencil, two-kernel PCG iteration"
+    if kname.startswith("k_keff_groups_pipe"):
+        return "general mesh: fan-group element tiles"
+    if kname.startswith("k_keff_parity"):
+        return "bit-exact PARITY element pass + node fold"
+    return "general mesh: element tiles (" + kname.split("<")[0] + ")"
+
+
+def general_line(L, device, key, steps, warmup=1, sample=5):
+    """The same workload with the structured-block stencil switched off (CWF_LATTICE=0): the fan-group tiles that
+    any gmsh mesh, C4 and every non-lattice scenario run, timed the same way as the headline (whole Newmark steps,
+    K_eff hipEvent-sampled), after the headline's timed region, so the two are never conflated."""
+    import ctypes as C
+
+    from cwf import _lib, scenarios
+    from cwf.stepper import Stepper
+
+    case = scenarios.config_case(key)
+    P = case.packing
+    prev = os.environ.get("CWF_LATTICE")
+    os.environ["CWF_LATTICE"] = "0"
+    try:
+        st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST,
+                     device=device)
+        h = st.system.handle()
+    finally:
+        if prev is None:
+            os.environ.pop("CWF_LATTICE", None)
+        else:
+            os.environ["CWF_LATTICE"] = prev
+    import torch
+
+    t = 0.0
+    for _ in range(warmup):
+        st.step(t).value()
+        t += case.cfg.time.initial_dt
+    L.cwf_hip_system_set_timing(h, sample)
+    torch.cuda.synchronize()
+    iters = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        iters += st.step(t).value().pcg.iterations
+        t += case.cfg.time.initial_dt
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ms, n = C.c_double(), C.c_uint64()
+    L.cwf_hip_system_timing(h, C.byref(ms), C.byref(n))
+    L.cwf_hip_system_set_timing(h, 0)
+    kname = (L.cwf_hip_system_keff_kernel(h) or b"").decode()
+    out = {"workload": case.name + " with CWF_LATTICE=0", "operator": operator_of(kname), "kernel": kname,
+           "steps": steps, "pcg_iterations": int(iters), "pcg_iterations_per_sec": iters / el,
+           "dof_iterations_per_sec": P.dof_count * iters / el, "ms_per_step": 1e3 * el / steps,
+           "keff_avg_launch_ms": ms.value / max(1, n.value)}
     st.close()
     st.system.close()
     return out
@@ -363,6 +429,10 @@ def main():
         hbm = hbm_roofline(L, device)
         if not args.no_general_roofline:
             hbm_general = hbm_roofline(L, device, general=True)
+    general = None
+    if (rank == 0 and world == 1 and not args.no_general and args.mode == "fast" and args.element == "tet4"
+            and operator_of(kname).startswith("structured")):
+        general = general_line(L, device, args.config, min(args.steps, 5))
     copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
     for rl in (hbm, hbm_general):
         if rl and copy_gbs:
@@ -389,6 +459,7 @@ def main():
                      "F0 sin(2 pi 5 t) from a 64-point curve, rewritten on the device every step)"
                      if load_pattern is not None else
                      "synthetic (structured hex block -> Kuhn tets, gravity + tip load)"),
+            "operator": operator_of(kname),
             "config": {"workload": case.name, "nodes_per_gpu": local_nodes,
                        ("hexes_per_gpu" if args.element == "hex8" else "tets_per_gpu"): local_tets,
                        "dofs": int(dofs_sum), "mode": args.mode,
@@ -416,6 +487,8 @@ def main():
             "roofline_hbm": hbm,
             # the unstructured-mesh SpMV (fan-group tiles, what C4 and any non-lattice mesh run) on the same C3 block
             "roofline_general": hbm_general,
+            # the same workload on the general operator (fan-group tiles), timed after the headline's region
+            "general": general,
         }
         if args.mode == "parity":
             # the events bracket both PARITY K_eff passes: the element pass and the node fold that also forms

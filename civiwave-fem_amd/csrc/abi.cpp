@@ -105,10 +105,62 @@ bool iso_pattern(const double *D)
 
 // the per-incidence fp64 force planes of the element-centric PARITY K_eff (3 x fslots doubles, ~96 B per tet),
 // allocated once a handle runs PARITY
+// Built on first use (a PARITY create or set_mode(PARITY)), from the node -> incidence CSR already on the device:
+// node n's k-th incidence (ascending element) goes to slot fblk[n / 64] + 64 k + n % 64 of the force planes, so a
+// wave of 64 consecutive nodes folds slot k of all its nodes with one coalesced load; ipos maps every (tet, corner)
+// to its slot. FAST handles never build it (16 B per tet, and its 2^32-slot limit is a PARITY limit only).
+int parity_incidence_slots(cwf_hip_system *h)
+{
+    DevSys &s = h->ds;
+    const uint64_t N = s.N, E = s.E, nb = (N + 63) / 64;
+    std::vector<uint32_t> off, inc, ipos, fblk;
+    try
+    {
+        off.resize(N + 1);
+        inc.resize(4 * E);
+        ipos.assign(4 * E, 0xFFFFFFFFu);
+        fblk.resize(nb + 1);
+    }
+    catch (const std::bad_alloc &)
+    {
+        return set_error(h, CWF_ERR_ALLOC, "host allocation failed");
+    }
+    HIPTRY(h, hipMemcpy(off.data(), s.off, (N + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPTRY(h, hipMemcpy(inc.data(), s.inc, 4 * E * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint64_t slots = 0;
+    for (uint64_t b = 0; b < nb; ++b)
+    {
+        fblk[b] = (uint32_t)slots;
+        uint32_t kmax = 0;
+        for (uint64_t n = 64 * b; n < std::min<uint64_t>(N, 64 * b + 64); ++n)
+            kmax = std::max(kmax, off[n + 1] - off[n]);
+        slots += 64ull * kmax;
+    }
+    if (slots >= (1ull << 32))
+        return set_error(h, CWF_ERR_UNSUPPORTED, "mesh too large for one PARITY handle (shard it)",
+                         "force_slots=" + std::to_string(slots));
+    fblk[nb] = (uint32_t)slots;
+    for (uint64_t n = 0; n < N; ++n)
+        for (uint32_t j = off[n]; j < off[n + 1]; ++j)
+            ipos[inc[j]] = fblk[n / 64] + 64u * (j - off[n]) + (uint32_t)(n % 64);  // inc = element << 2 | corner
+    uint32_t *dp, *db;
+    if (int st = upload(h, &dp, ipos.data(), 4 * E))
+        return st;
+    if (int st = upload(h, &db, fblk.data(), nb + 1))
+        return st;
+    s.ipos = dp;
+    s.fblk = db;
+    s.fslots = slots;
+    return 0;
+}
+
 int parity_force_buffer(cwf_hip_system *h)
 {
-    if (h->ds.pforce || !h->ds.ipos || !h->ds.E)
+    if (h->ds.pforce || h->ds.hex || !h->ds.E)
         return 0;
+    if (!h->ds.ipos)
+        if (int st = parity_incidence_slots(h))
+            return st;
     double *f = nullptr;
     if (int st = dalloc(h, &f, 3ull * h->ds.fslots))
         return st;
@@ -294,7 +346,10 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (cwf_hip_system *m : g)
             HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
-    if (sharded)
+    const bool cg = fast && fast_cg_enabled(h);  // one launch per iteration (structured blocks)
+    if (cg)
+        fast_cg_init(h, rhs[0], set.relative_tolerance, st);
+    else if (sharded)
     {
         if (int e = fast ? sharded_pcg_init(g, rhs, set.relative_tolerance)
                          : sharded_parity_init(g, rhs, set.relative_tolerance))
@@ -361,7 +416,9 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         {
             const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
             hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
-            if (fast)
+            if (cg)
+                fast_cg_iteration(h, (unsigned)(enq + i), st, e0, e1);
+            else if (fast)
             {
                 if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
                     return e;
@@ -374,7 +431,9 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             else
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
-        if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
+        if (cg)
+            fast_cg_check(h, (unsigned)(enq + nb), st);
+        else if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
             for (cwf_hip_system *m : g)
                 fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
         HIPTRY(h, hipGetLastError());
@@ -387,6 +446,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
         for (size_t i = 0; i < g.size(); ++i)
             fast_flush_x(g[i], rhs[i], g[i]->stream);
+    if (cg && (h->ctl_host->iterations & 1u))  // r_n lives in the second buffer for odd n
+        HIPTRY(h, hipMemcpyAsync(h->r, h->cg_r2, h->ds.D * sizeof(float), hipMemcpyDeviceToDevice, st));
     if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows
     {
         if (int e = comm_halo(g, &cwf_hip_system::x))
@@ -760,11 +821,26 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         if (d->adjacency_offsets && d->adjacency_elements && d->adjacency_local)
         {
             std::memcpy(off.data(), d->adjacency_offsets, (N + 1) * sizeof(uint32_t));
-            if (off[N] != E * K)
+            if (off[N] != E * K || off[0] != 0)
                 return bail(set_error(h, CWF_ERR_SIZE, "adjacency size mismatch",
                                       "expected=" + std::to_string(E * K) + "\nactual=" + std::to_string(off[N])));
-            for (uint64_t j = 0; j < E * K; ++j)
-                inc[j] = (d->adjacency_elements[j] << sh) | (d->adjacency_local[j] & (uint32_t)(K - 1));
+            // the caller's CSR must be exactly the node -> (element, corner) incidences in ascending element order
+            // (preprocess.cpp:389-400): every later pass indexes through it without bounds checks
+            for (uint64_t n = 0; n < N; ++n)
+            {
+                if (off[n] > off[n + 1])
+                    return bail(set_error(h, CWF_ERR_ARGUMENT, "adjacency offsets must be non-decreasing",
+                                          "node=" + std::to_string(n)));
+                for (uint32_t j = off[n]; j < off[n + 1]; ++j)
+                {
+                    const uint32_t e = d->adjacency_elements[j], a = d->adjacency_local[j];
+                    if (e >= E || a >= (uint32_t)K || d->element_connectivity[8ull * e + a] != n ||
+                        (j > off[n] && d->adjacency_elements[j - 1] >= e))
+                        return bail(set_error(h, CWF_ERR_ARGUMENT, "adjacency does not match the connectivity",
+                                              "node=" + std::to_string(n) + "\nentry=" + std::to_string(j)));
+                    inc[j] = (e << sh) | a;
+                }
+            }
         }
         else
         {
@@ -794,46 +870,6 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(st);
         s.off = doff;
         s.inc = dinc;
-        if (!hex)  // where the element-centric PARITY K_eff stores every incidence's force (kernels_parity.hip)
-        {
-            // node n's k-th incidence (ascending element) goes to slot fblk[n / 64] + 64 k + n % 64 of the
-            // force planes: a wave of 64 consecutive nodes folds slot k of all its nodes with one coalesced load
-            const uint64_t nb = (N + 63) / 64;
-            std::vector<uint32_t> ipos, fblk;
-            try
-            {
-                ipos.resize(4 * E);
-                fblk.resize(nb + 1);
-            }
-            catch (const std::bad_alloc &)
-            {
-                return bail(set_error(h, CWF_ERR_ALLOC, "host allocation failed"));
-            }
-            uint64_t slots = 0;
-            for (uint64_t b = 0; b < nb; ++b)
-            {
-                fblk[b] = (uint32_t)slots;
-                uint32_t kmax = 0;
-                for (uint64_t n = 64 * b; n < std::min<uint64_t>(N, 64 * b + 64); ++n)
-                    kmax = std::max(kmax, off[n + 1] - off[n]);
-                slots += 64ull * kmax;
-            }
-            if (slots >= (1ull << 32))
-                return bail(set_error(h, CWF_ERR_UNSUPPORTED, "mesh too large for one PARITY handle (shard it)",
-                                      "force_slots=" + std::to_string(slots)));
-            fblk[nb] = (uint32_t)slots;
-            for (uint64_t n = 0; n < N; ++n)
-                for (uint32_t j = off[n]; j < off[n + 1]; ++j)
-                    ipos[inc[j]] = fblk[n / 64] + 64u * (j - off[n]) + (uint32_t)(n % 64);  // inc = element << 2 | corner
-            uint32_t *dp, *db;
-            if (int st = upload(h, &dp, ipos.data(), 4 * E))
-                return bail(st);
-            if (int st = upload(h, &db, fblk.data(), nb + 1))
-                return bail(st);
-            s.ipos = dp;
-            s.fblk = db;
-            s.fslots = slots;
-        }
     }
     // structured Kuhn block: the stencil blocks, the plane table and one row value per node (lattice.inc)
     if (E && is_lat)
@@ -934,6 +970,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     return bail(st);
                 if (int st = dalloc(h, &dci9, 9 * kLatClasses))
                     return bail(st);
+                // classes without a node keep zero inverses (k_lat_class_inverse fills only represented ones; halo
+                // lanes of the z-from-r and single-launch passes may read any class)
+                HIPTRY(h, hipMemset(dci6, 0, kLatClasses * sizeof(uint4)));
+                HIPTRY(h, hipMemset(dci9, 0, 9 * kLatClasses * sizeof(float)));
                 t.lcls = dcls;
                 t.lrep = drep;
                 t.lcinv6 = dci6;
@@ -1250,10 +1290,20 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         return bail(st);
     if (int st = dalloc(h, &h->inv6, 4 * N))
         return bail(st);
+    // the single-launch PCG of a structured block with the class preconditioner (spmv_tiles.hip: fast_cg_*)
+    const char *lcg = knob("CWF_LAT_CG");
+    if (h->mode == CWF_MODE_FAST && s.t.lat && s.t.lcls && s.t.lmu && !(lcg && lcg[0] == '0'))
+    {
+        for (float **v : {&h->cg_r2, &h->cg_w2, &h->cg_s0, &h->cg_s1})
+            if (int st = dalloc(h, v, D))
+                return bail(st);
+    }
     const uint64_t chunks = (D + d->reduction_block - 1) / d->reduction_block;
+    // the PARITY chunk partials, the FAST dot partials, and 4 doubles per workgroup of the FAST PCG kernels'
+    // shares (fold_publish: K_eff and single-launch grids in part0, the update pass's in part1)
     h->part_cap = std::max<uint64_t>(
-        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), (uint64_t)s.t.ntiles,
-         (uint64_t)s.t.pipe_grid, 1});
+        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), 4ull * s.t.ntiles,
+         4ull * s.t.pipe_grid, 4ull * 2048, 1});
     if (int st = dalloc(h, &h->part0, h->part_cap))
         return bail(st);
     if (int st = dalloc(h, &h->part1, h->part_cap))
@@ -1262,6 +1312,11 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         return bail(st);
     if (int st = dalloc(h, &h->ctl, 1))
         return bail(st);
+    if (int st = dalloc(h, &h->gsum, 4 * 32 * 4))
+        return bail(st);
+    if (int st = dalloc(h, &h->gcnt, 2 * 32 * 16))
+        return bail(st);
+    HIPTRY(h, hipMemset(h->gcnt, 0, 2 * 32 * 16 * sizeof(unsigned)));
     if (int st = dalloc(h, &h->scal, 8))
         return bail(st);
     // folded per-rank scalars (one rank until cwf_hip_system_attach): p.Ap, {r.r, r.z}, {rhs.rhs, r0.r0}, r0.z0
@@ -1438,6 +1493,12 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
+        if (fast_cg_enabled(h))  // the single-launch iteration: per owned node r, w, s, p_old read + the class
+        {                        // byte, p, s, r, w written; the shell's mass; the lazy x (x and three older
+                                 // directions read, x written) every x_lag-th launch, amortised over four
+            *layout_bytes = (uint64_t)s.Nown * (48 + 1 + 48) + 4ull * s.t.lnshell + (uint64_t)s.Nown * (12 + 36 + 12) / 4;
+            return 0;
+        }
         if (s.t.lat)  // per owned node: z and p_old read, the new p and the row value written; the mass read
         {             // (only the shell's when the strict interior's is one value, lmu)
             *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 12 + 12 + (s.t.lmu && s.t.lzr ? 1 : 0)) +
@@ -1466,6 +1527,13 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
         return h->ds.iso ? "k_keff_parity_elem<true, false>" : "k_keff_parity_elem<false, false>";
+    if (fast_cg_enabled(h))  // the launches without the lazy x update (three in four)
+    {
+        static thread_local char name[96];
+        snprintf(name, sizeof name, "k_cg_lattice<%s, %s, false>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn");
+        return name;
+    }
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {
         static thread_local char name[96];

@@ -312,13 +312,27 @@ int parity_setup(const std::vector<cwf_hip_system *> &g)
                                                      "contiguous global order", "rank=" + std::to_string(h->rank));
         if (h->pstride == stride && h->gp0)
             continue;
-        void *q = nullptr;
+        // (re)size the slot block: an attach resets pstride, so a re-attached handle reuses its block when it is
+        // large enough and frees it otherwise (repeated attach / solve cycles do not grow device memory)
         const size_t bytes = 2 * (size_t)n * stride * sizeof(double);
-        if (hipMalloc(&q, bytes) != hipSuccess)
-            return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer", "bytes=" + std::to_string(bytes));
-        h->owned.push_back(q);
-        h->bytes += bytes;
-        h->gp0 = static_cast<double *>(q);
+        if (h->gp0 && h->gp_bytes < bytes)
+        {
+            (void)hipFree(h->gp0);
+            h->owned.erase(std::remove(h->owned.begin(), h->owned.end(), static_cast<void *>(h->gp0)), h->owned.end());
+            h->bytes -= h->gp_bytes;
+            h->gp0 = h->gp1 = nullptr;
+            h->gp_bytes = 0;
+        }
+        if (!h->gp0)
+        {
+            void *q = nullptr;
+            if (hipMalloc(&q, bytes) != hipSuccess)
+                return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer", "bytes=" + std::to_string(bytes));
+            h->owned.push_back(q);
+            h->bytes += bytes;
+            h->gp0 = static_cast<double *>(q);
+            h->gp_bytes = bytes;
+        }
         h->gp1 = h->gp0 + (size_t)n * stride;
         HIPTRY(h, hipMemset(h->gp0, 0, bytes));  // the +0.0 padding of every slot
         h->pstride = (uint32_t)stride;

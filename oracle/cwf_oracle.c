@@ -13,8 +13,10 @@
  *   - structural zeros of the B matrix are skipped: 0*u = +-0 and a running sum that
  *     starts at +0.0 is never -0.0, so adding +-0 is an exact no-op (finite inputs).
  *
- * Pinning: the outputs are checked in tests/test_oracle_pins.py against the reference's
- * own test fixtures (tests/pcg_test.cpp, physics_test.cpp, preprocess_test.cpp) and the
+ * PARITY UNPINNED: no stand-in-free build of the reference is possible in this image
+ * (its sources need C++23 <expected>/<format>/<print>, absent from libstdc++ 11), so no
+ * reference output was produced here.  The outputs are checked in tests/test_oracle_pins.py
+ * against the reference's own test fixtures (tests/pcg_test.cpp, physics_test.cpp, preprocess_test.cpp) and the
  * reference outputs recorded in SURVEY.md section 8c (single tet apply_keff, 1-iteration
  * PCG, and the n=16 Kuhn block solve: 162 iterations, |r| = 0.14640172515227148,
  * FNV-1a(x) = f10c27935f2e7a58).

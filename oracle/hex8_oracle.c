@@ -14,7 +14,7 @@
  *     (pcg.cpp:592-651): f_a = sum_gp |det J| B_a^T D B u * s_K.
  * The GPU kernel (spmv_tiles.hip, k_keff_hex_tiles) evaluates the same integrals with sum
  * factorisation in fp32; tests compare both and check the operator's physics (patch test, rigid
- * modes, symmetry, convergence towards the pinned Kuhn-tet solution).
+ * modes, symmetry, convergence towards the oracle Kuhn-tet solution).
  */
 #include <math.h>
 #include <stdint.h>
