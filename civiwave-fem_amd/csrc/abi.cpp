@@ -346,8 +346,15 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (cwf_hip_system *m : g)
             HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
-    const bool cg = fast && fast_cg_enabled(h);  // one launch per iteration (structured blocks)
-    if (cg)
+    bool cg = fast;  // one launch per iteration (structured blocks, every member)
+    for (cwf_hip_system *m : g)
+        cg = cg && fast_cg_enabled(m);
+    if (cg && sharded)
+    {
+        if (int e = sharded_cg_init(g, rhs, set.relative_tolerance))
+            return e;
+    }
+    else if (cg)
         fast_cg_init(h, rhs[0], set.relative_tolerance, st);
     else if (sharded)
     {
@@ -416,7 +423,12 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         {
             const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
             hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
-            if (cg)
+            if (cg && sharded)
+            {
+                if (int e = sharded_cg_iteration(g, (unsigned)(enq + i), e0, e1))
+                    return e;
+            }
+            else if (cg)
                 fast_cg_iteration(h, (unsigned)(enq + i), st, e0, e1);
             else if (fast)
             {
@@ -432,7 +444,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
         if (cg)
-            fast_cg_check(h, (unsigned)(enq + nb), st);
+            for (cwf_hip_system *m : g)
+                fast_cg_check(m, (unsigned)(enq + nb), m->stream);
         else if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
             for (cwf_hip_system *m : g)
                 fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
@@ -447,7 +460,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (size_t i = 0; i < g.size(); ++i)
             fast_flush_x(g[i], rhs[i], g[i]->stream);
     if (cg && (h->ctl_host->iterations & 1u))  // r_n lives in the second buffer for odd n
-        HIPTRY(h, hipMemcpyAsync(h->r, h->cg_r2, h->ds.D * sizeof(float), hipMemcpyDeviceToDevice, st));
+        for (cwf_hip_system *m : g)
+            HIPTRY(m, hipMemcpyAsync(m->r, m->cg_r2, m->ds.D * sizeof(float), hipMemcpyDeviceToDevice, m->stream));
     if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows
     {
         if (int e = comm_halo(g, &cwf_hip_system::x))

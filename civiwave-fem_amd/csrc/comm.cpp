@@ -119,20 +119,23 @@ int nccl_fail(cwf_hip_system *h, ncclResult_t e, const char *what)
 }  // namespace
 
 // One exchange step of a sharded solve: in-place all-gathers of per-rank double slots (slot r of buf is
-// [r * count, (r + 1) * count)) and, optionally, the halo of one vector (ghost rows <- the owners' values). Over
-// RCCL every operation of the step is one ncclGroupStart/End, so the all-gathers and the halo send/recv pairs
-// of an iteration go out as one launch.
-int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
-                  float *cwf_hip_system::*vec)
+// [r * count, (r + 1) * count)) and the halos of up to kMaxHaloVecs vectors (ghost rows <- the owners' values;
+// vecs[m] lists member m's vectors, the same count for every member). Over RCCL every operation of the step is one
+// ncclGroupStart/End, so the all-gathers and the halo send/recv pairs of an iteration go out as one launch.
+int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
+                       const std::vector<std::vector<float *>> &vecs)
 {
     cwf_hip_system *h0 = g[0];
-    if (vec)
-        for (cwf_hip_system *h : g)
-            halo_pack(h, h->*vec, h->stream);
+    const size_t nv = vecs.empty() ? 0 : vecs[0].size();
+    if (nv > kMaxHaloVecs)
+        return set_error(h0, CWF_ERR_ARGUMENT, "too many halo vectors in one exchange");
+    for (size_t i = 0; i < g.size(); ++i)  // vector j's send segment at sendbuf + 3 nsend j
+        for (size_t j = 0; j < nv; ++j)
+            halo_pack(g[i], vecs[i][j], g[i]->stream, g[i]->sendbuf + 3 * g[i]->nsend * j);
     const bool gather = h0->nranks > 1;
     if (h0->comm && h0->comm->kind == 1)
     {
-        if (!gather && !vec)
+        if (!gather && !nv)
             return 0;
         const Rccl *r = rccl(nullptr);
         ncclComm_t c = static_cast<ncclComm_t>(h0->comm->nccl);
@@ -143,17 +146,16 @@ int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<
                 double *b = h0->*(q.buf);
                 NCCLTRY(h0, r->AllGather(b + (size_t)h0->rank * q.count, b, q.count, ncclFloat64, c, h0->stream));
             }
-        if (vec)
+        for (size_t k = 0; k < h0->nbr.size(); ++k)
         {
-            float *v = h0->*vec;
-            for (size_t k = 0; k < h0->nbr.size(); ++k)
+            const size_t ns = h0->send_off[k + 1] - h0->send_off[k], nr = h0->recv_off[k + 1] - h0->recv_off[k];
+            for (size_t j = 0; j < nv; ++j)
             {
-                const size_t ns = h0->send_off[k + 1] - h0->send_off[k], nr = h0->recv_off[k + 1] - h0->recv_off[k];
                 if (ns)
-                    NCCLTRY(h0, r->Send(h0->sendbuf + 3 * h0->send_off[k], 3 * ns, ncclFloat32, h0->nbr[k], c,
-                                        h0->stream));
+                    NCCLTRY(h0, r->Send(h0->sendbuf + 3 * (h0->nsend * j + h0->send_off[k]), 3 * ns, ncclFloat32,
+                                        h0->nbr[k], c, h0->stream));
                 if (nr)
-                    NCCLTRY(h0, r->Recv(v + 3 * ((size_t)h0->ds.Nown + h0->recv_off[k]), 3 * nr, ncclFloat32,
+                    NCCLTRY(h0, r->Recv(vecs[0][j] + 3 * ((size_t)h0->ds.Nown + h0->recv_off[k]), 3 * nr, ncclFloat32,
                                         h0->nbr[k], c, h0->stream));
             }
         }
@@ -169,10 +171,12 @@ int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<
                         HIPTRY(dst, hipMemcpyAsync(dst->*(q.buf) + (size_t)src->rank * q.count,
                                                    src->*(q.buf) + (size_t)src->rank * q.count,
                                                    q.count * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
-    if (!vec)
+    if (!nv)
         return 0;
     // member m's ghosts from q = q's send segment for m
-    for (cwf_hip_system *m : g)
+    for (size_t mi = 0; mi < g.size(); ++mi)
+    {
+        cwf_hip_system *m = g[mi];
         for (size_t k = 0; k < m->nbr.size(); ++k)
         {
             cwf_hip_system *q = g[m->nbr[k]];
@@ -185,11 +189,23 @@ int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<
                 return set_error(m, CWF_ERR_COMM, "halo plans disagree",
                                  "rank=" + std::to_string(m->rank) + "\npeer=" + std::to_string(q->rank));
             if (nr)
-                HIPTRY(m, hipMemcpyAsync((m->*vec) + 3 * ((size_t)m->ds.Nown + m->recv_off[k]),
-                                         q->sendbuf + 3 * q->send_off[j], 3 * nr * sizeof(float),
-                                         hipMemcpyDeviceToDevice, m->stream));
+                for (size_t v = 0; v < nv; ++v)
+                    HIPTRY(m, hipMemcpyAsync(vecs[mi][v] + 3 * ((size_t)m->ds.Nown + m->recv_off[k]),
+                                             q->sendbuf + 3 * (q->nsend * v + q->send_off[j]), 3 * nr * sizeof(float),
+                                             hipMemcpyDeviceToDevice, m->stream));
         }
+    }
     return 0;
+}
+
+int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
+                  float *cwf_hip_system::*vec)
+{
+    std::vector<std::vector<float *>> vecs;
+    if (vec)
+        for (cwf_hip_system *h : g)
+            vecs.push_back({h->*vec});
+    return comm_exchange_vecs(g, gathers, vecs);
 }
 
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count)
@@ -242,6 +258,42 @@ int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<c
         launch_p_init(h, h->stream);
     }
     return 0;
+}
+
+// The single-launch (Chronopoulos-Gear) iteration of structured-block shards (lattice_cg.inc): one exchange step
+// per iteration instead of two. Launch i needs, on its ghost planes, r_i, w_i and s_(i-1) (it recomputes u_(i+1)
+// there from them, as it does for every halo entry) and every rank's {r.r, r.u, w.u} of launch i - 1, so after
+// each launch a rank folds its group totals into its slot and one grouped step all-gathers the slots (4 f64 per
+// rank, folded in rank order by every rank: identical scalars everywhere) and sends the three halos.
+int sharded_cg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+{
+    if (int st = sharded_pcg_init(g, rhs, rel_tol))  // r_0, norms, u_0 = z (+ its halo), rho, p_(-1)
+        return st;
+    for (cwf_hip_system *h : g)
+    {
+        const uint32_t Down = 3u * h->ds.Nown;
+        fast_keff(h, h->z, h->Ap, false, nullptr, nullptr, h->stream);  // w_0 on the owned rows
+        fast_dot(h->z, h->r, h->Ap, Down, h->part0, h->part1, h->stream);
+        HIPTRY(h, hipMemsetAsync(h->g_cg + 4 * h->rank, 0, 4 * sizeof(double), h->stream));
+        fold_pair(h->part0, h->part1, fast_dot_blocks(Down), h->g_cg + 4 * h->rank + 1, h->stream);  // gamma, delta
+    }
+    std::vector<std::vector<float *>> vecs;
+    for (cwf_hip_system *h : g)
+        vecs.push_back({fast_cg_vec(h, 'r', 0), fast_cg_vec(h, 'w', 0)});
+    return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);
+}
+
+int sharded_cg_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1)
+{
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        fast_cg_iteration(g[i], it, g[i]->stream, i ? nullptr : e0, i ? nullptr : e1);
+        fast_cg_fold_rank(g[i], it, g[i]->stream);
+    }
+    std::vector<std::vector<float *>> vecs;
+    for (cwf_hip_system *h : g)
+        vecs.push_back({fast_cg_vec(h, 'r', it + 1), fast_cg_vec(h, 'w', it + 1), fast_cg_vec(h, 's', it)});
+    return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);
 }
 
 // one FAST PCG iteration of every member (a single unsharded handle is the group {h} with one rank): two
@@ -525,6 +577,54 @@ void cwf_hip_comm_destroy(cwf_hip_comm *cm)
     delete cm;
 }
 
+}  // extern "C"
+
+namespace cwf
+{
+// The single-launch iteration on a structured-block shard forms u = M^-1 r on its ghost planes from each node's
+// class byte. A ghost plane is globally interior along z, but its local class says "surface" (the shard's mesh
+// stops one cell layer past its owned planes), and its local diagonal blocks and lumped mass are partial. So at
+// attach every ghost-plane node takes the class of its global position (z inside), whose block inverse then comes
+// from an owned representative node (complete rows) at the next block-Jacobi build. A shard whose classes have no
+// owned representative keeps the two-kernel iteration (cg_shard stays false).
+int attach_ghost_classes(cwf_hip_system *h)
+{
+    DevTiles &t = h->ds.t;
+    h->cg_shard = false;
+    if (!t.lcls || !t.lmu || !h->cg_r2 || h->mode != CWF_MODE_FAST)
+        return 0;
+    const uint64_t N = h->ds.N, Nown = h->ds.Nown, per = (uint64_t)t.lnx * t.lny;
+    std::vector<uint8_t> cls(N);
+    HIPTRY(h, hipMemcpy(cls.data(), t.lcls, N, hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < t.lnz; ++k)
+    {
+        const uint64_t b = h->lat_plane[k];
+        if (b < Nown)
+            continue;
+        for (uint64_t q = 0; q < per && b + q < N; ++q)
+        {
+            const uint32_t c = cls[b + q], ty = c >> 3, tz = ty / 9;
+            cls[b + q] = (uint8_t)((ty - 9 * tz + 9) << 3 | (c & 7u));
+        }
+    }
+    std::vector<uint32_t> rep(kLatClasses, 0xFFFFFFFFu);
+    for (uint64_t n = 0; n < Nown; ++n)
+        if (rep[cls[n]] == 0xFFFFFFFFu)
+            rep[cls[n]] = (uint32_t)n;
+    for (uint64_t n = Nown; n < N; ++n)
+        if (rep[cls[n]] == 0xFFFFFFFFu)
+            return 0;  // a ghost class without an owned representative
+    HIPTRY(h, hipMemcpy(const_cast<uint8_t *>(t.lcls), cls.data(), N, hipMemcpyHostToDevice));
+    HIPTRY(h, hipMemcpy(const_cast<uint32_t *>(t.lrep), rep.data(), kLatClasses * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+    h->inv_fast = false;  // rebuild the class inverses from the new representatives
+    h->cg_shard = true;
+    return 0;
+}
+}  // namespace cwf
+
+extern "C" {
+
 int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, const cwf_shard_info *plan)
 {
     if (!h || !cm || !plan)
@@ -566,19 +666,20 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         return 0;
     };
     void *p = nullptr;
-    if (int st = alloc(&p, 6 * (size_t)n * sizeof(double)))
+    if (int st = alloc(&p, 10 * (size_t)n * sizeof(double)))
         return st;
     h->g_pap = static_cast<double *>(p);
     h->g_rrz = h->g_pap + n;
     h->g_init = h->g_rrz + 2 * n;
     h->g_rz0 = h->g_init + 2 * n;
-    HIPTRY(h, hipMemset(h->g_pap, 0, 6 * (size_t)n * sizeof(double)));
+    h->g_cg = h->g_rz0 + n;
+    HIPTRY(h, hipMemset(h->g_pap, 0, 10 * (size_t)n * sizeof(double)));
     if (int st = alloc(&p, nsend * sizeof(uint32_t)))
         return st;
     h->send_idx = static_cast<uint32_t *>(p);
     if (nsend)
         HIPTRY(h, hipMemcpy(h->send_idx, plan->send_nodes, nsend * sizeof(uint32_t), hipMemcpyHostToDevice));
-    if (int st = alloc(&p, 3 * nsend * sizeof(float)))
+    if (int st = alloc(&p, 3 * kMaxHaloVecs * nsend * sizeof(float)))  // one segment per halo vector of a step
         return st;
     h->sendbuf = static_cast<float *>(p);
     h->nsend = nsend;
@@ -605,6 +706,8 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         t.lk1 = k0 < k1 ? k1 : 1;
         t.lzr = 0;  // the update pass stores z: the halo exchange carries z, and a ghost's class is a local one
         lattice_plan(t);
+        if (int st = attach_ghost_classes(h))
+            return st;
     }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
     h->owned_contiguous = true;  // PARITY shards fold chunk partials in global order (comm.cpp parity_setup)

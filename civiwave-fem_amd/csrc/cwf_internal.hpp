@@ -340,13 +340,15 @@ struct cwf_hip_system
     std::vector<int32_t> nbr;
     std::vector<uint64_t> send_off, recv_off;
     uint32_t *send_idx = nullptr;  // [nsend] owned local node ids, per neighbour
-    float *sendbuf = nullptr;      // [3 nsend]
+    float *sendbuf = nullptr;      // [kMaxHaloVecs][3 nsend]
     uint64_t nsend = 0;
     // all-gathered per-rank scalars, slot of rank r at [r * count]
     double *g_pap = nullptr;   // [nranks]      p.Ap
     double *g_rrz = nullptr;   // [2 nranks]    {r.r, r.z}
     double *g_init = nullptr;  // [2 nranks]    {rhs.rhs, r0.r0}
     double *g_rz0 = nullptr;   // [nranks]      r0.z0
+    double *g_cg = nullptr;    // [4 nranks]    the single-launch iteration's {r.r, r.u, w.u, -} per rank
+    bool cg_shard = false;     // an attached structured-block shard whose ghost planes carry global node classes
     // sharded PARITY: every rank's 256-DOF chunk partials all-gathered into slot [r * pstride, (r+1) * pstride)
     // (zero-padded past the rank's own chunk count) and folded in that order on every rank = the global chunk
     // order of pcg.cpp:170-207, since the owned node ranges are ascending by rank and aligned to whole chunks
@@ -426,6 +428,10 @@ bool fast_cg_enabled(const cwf_hip_system *h);
 void fast_cg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
 void fast_cg_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 void fast_cg_check(cwf_hip_system *h, unsigned it, hipStream_t st);
+void fast_cg_fold_rank(cwf_hip_system *h, unsigned it, hipStream_t st);  // this rank's triple -> g_cg[4 rank]
+float *fast_cg_vec(cwf_hip_system *h, char which, unsigned i);         // 'r' r_i, 'w' w_i, 's' s_i buffers
+int sharded_cg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
+int sharded_cg_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1);
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
 unsigned fast_update_blocks(const DevSys &s, bool flush);  // grid of update pass (lazy-x iteration or not)
@@ -435,7 +441,7 @@ void derived_fields(cwf_hip_system *h, const float *u, float *elem_out, float *n
 bool fast_direct_fold(const cwf_hip_system *h);  // unsharded: consumers fold per-workgroup shares
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> g_pap[rank]
 void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
-void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st);
+void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st, float *dst = nullptr);  // dst: sendbuf
 void fast_block_inverse(cwf_hip_system *h, hipStream_t st);  // parity BJ, symmetrised + packed to inv6
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st, uint32_t stride = 1);
 void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count,
@@ -449,6 +455,9 @@ struct Gather
 };
 int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                   float *cwf_hip_system::*vec);
+constexpr size_t kMaxHaloVecs = 3;  // halo vectors of one exchange step (the single-launch iteration's r, w, s)
+int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
+                       const std::vector<std::vector<float *>> &vecs);
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);
 int comm_halo(const std::vector<cwf_hip_system *> &g, float *cwf_hip_system::*vec);
 int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);

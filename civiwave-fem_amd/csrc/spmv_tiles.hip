@@ -2141,7 +2141,14 @@ void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st)
 bool fast_cg_enabled(const cwf_hip_system *h)
 {
     const DevTiles &t = h->ds.t;
-    return h->mode == CWF_MODE_FAST && !h->sharded() && t.lat && t.lcls && t.lmu && h->cg_r2 != nullptr;
+    return h->mode == CWF_MODE_FAST && (!h->sharded() || h->cg_shard) && t.lat && t.lcls && t.lmu &&
+           h->cg_r2 != nullptr;
+}
+
+float *fast_cg_vec(cwf_hip_system *h, char which, unsigned i)
+{
+    float *R[2] = {h->r, h->cg_r2}, *W[2] = {h->Ap, h->cg_w2}, *S[2] = {h->cg_s0, h->cg_s1};
+    return (which == 'r' ? R : which == 'w' ? W : S)[i & 1u];
 }
 
 // solve_pcg prologue (pcg.cpp:744-828) plus the Chronopoulos-Gear start: w_0 = K u_0, gamma_0 = r_0.u_0,
@@ -2165,22 +2172,22 @@ void fast_cg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream
 
 static CgArgs cg_args(cwf_hip_system *h, unsigned it)
 {
-    float *R[2] = {h->r, h->cg_r2}, *W[2] = {h->Ap, h->cg_w2}, *S[2] = {h->cg_s0, h->cg_s1};
     CgArgs a{};
     a.ctl = h->ctl;
-    a.rin = R[it & 1u];
-    a.rout = R[(it + 1u) & 1u];
-    a.win = W[it & 1u];
-    a.wout = W[(it + 1u) & 1u];
-    a.sin = it ? S[(it - 1u) & 1u] : nullptr;
-    a.sout = S[it & 1u];
+    a.rin = fast_cg_vec(h, 'r', it);
+    a.rout = fast_cg_vec(h, 'r', it + 1u);
+    a.win = fast_cg_vec(h, 'w', it);
+    a.wout = fast_cg_vec(h, 'w', it + 1u);
+    a.sin = it ? fast_cg_vec(h, 's', it - 1u) : nullptr;
+    a.sout = fast_cg_vec(h, 's', it);
     a.pold = fast_p_old(h, it);
     a.pnew = fast_p_new(h, it);
     a.x = h->x;
     a.pb = fast_p_bufs(h);
     a.lag = x_lag();
-    a.gin = h->gsum + 128u * (2u + (it & 1u));
-    a.ngin = it ? fold_groups(h->ds.t.lnwork) : kFoldGroups;
+    // a shard folds the all-gathered per-rank triples (rank order), a single handle its own group totals
+    a.gin = h->sharded() ? h->g_cg : h->gsum + 128u * (2u + (it & 1u));
+    a.ngin = h->sharded() ? (unsigned)h->nranks : it ? fold_groups(h->ds.t.lnwork) : kFoldGroups;
     a.fo = FoldOut{h->part0, h->gsum + 128u * (2u + ((it + 1u) & 1u)), h->gcnt};
     a.it = it;
     a.hist = h->hist;
@@ -2220,6 +2227,13 @@ void fast_cg_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_
 void fast_cg_check(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
     k_cg_check<<<1, 64, 0, st>>>(cg_args(h, it));
+}
+
+// a shard's {r.r, r.u, w.u} of launch `it` (its group totals, folded in group order) into its all-gather slot
+void fast_cg_fold_rank(cwf_hip_system *h, unsigned it, hipStream_t st)
+{
+    k_fold_triple<<<1, 64, 0, st>>>(h->ctl, h->gsum + 128u * (2u + ((it + 1u) & 1u)), fold_groups(h->ds.t.lnwork),
+                                    h->g_cg + 4 * h->rank);
 }
 
 // diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
@@ -2284,12 +2298,12 @@ void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st)
               st, 4u);
 }
 
-void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st)
+void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st, float *dst)
 {
     if (!h->nsend)
         return;
     const uint64_t g = std::min<uint64_t>((h->nsend + 255) / 256, 1024);
-    k_halo_pack<<<(unsigned)g, 256, 0, st>>>(h->send_idx, h->nsend, v, h->sendbuf);
+    k_halo_pack<<<(unsigned)g, 256, 0, st>>>(h->send_idx, h->nsend, v, dst ? dst : h->sendbuf);
 }
 
 }  // namespace cwf

@@ -322,3 +322,46 @@ def test_cg_stepper_steps():
     for what in (Stepper.DISPLACEMENT, Stepper.VELOCITY):
         ur, uf = ref.get_state(what), fast.get_state(what)
         assert np.linalg.norm(uf - ur) <= 1e-4 * np.linalg.norm(ur)
+
+
+def _slab_solve(shape, nranks, mi=800):
+    """FAST solve of a Kuhn block cut into `nranks` slab sub-meshes (LOCAL communicator, one process)."""
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=1e-6, max_iterations=mi)
+    sK, sM = glob.scalars()
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs, kerns = [], [], [], [], []
+    for r in range(nranks):
+        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, tol=1e-6)
+        src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
+        sh = shard.build_shard(src, begin, r, node_global)
+        s = sh.system(glob.materials, sK, sM)
+        comm.attach(s, sh)
+        kerns.append(_kernel(s))
+        systems.append(s)
+        shards.append(sh)
+        rhs.append(sh.local_dofs(case.static_rhs()))
+        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    tel = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(mi, 1e-6), xs).value()
+    xg = np.zeros((glob.packing.node_count, 3), np.float32)
+    for sh, xl in zip(shards, xs):
+        xg[sh.node_global[: sh.owned_nodes].astype(np.int64)] = xl.reshape(-1, 3)[: sh.owned_nodes]
+    comm.close()
+    return glob, tel, xg.reshape(-1), kerns
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_cg_slab_shards(nranks, monkeypatch):
+    """Structured-block shards run the single-launch iteration too (one exchange step per iteration: the rank's
+    {r.r, r.u, w.u} all-gathered and the r, w, s halos; ghost planes take the class of their global position): the
+    oracle's solution, and the two-kernel sharded iteration's (CWF_LAT_CG=0) iteration count within 3%."""
+    shape = (13, 9, 4)
+    glob, tel, x, kerns = _slab_solve(shape, nranks)
+    assert all(k.startswith("k_cg_lattice") for k in kerns), kerns
+    ref = oracle_system(glob.packing, glob.materials, *glob.scalars()).solve_pcg(glob.static_rhs(), 800, 1e-6)
+    assert tel.converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    monkeypatch.setenv("CWF_LAT_CG", "0")
+    _, tel0, x0, kerns0 = _slab_solve(shape, nranks)
+    assert all(k.startswith("k_keff_lattice") for k in kerns0), kerns0
+    assert abs(tel.iterations - tel0.iterations) <= max(2, tel0.iterations * 3 // 100)
+    assert np.linalg.norm(x - x0) <= 1e-5 * np.linalg.norm(x0)

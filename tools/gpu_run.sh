@@ -14,6 +14,8 @@
 #   prof:NAME[:ARGS]        rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes (tools/profile.sh) and the
 #                           K_eff kernel's summary (tools/pmc_summary.py) -> <TAG>_NAME_{summary.txt,pmc.json,...}
 #   sq:NAME[:ARGS]          the SQ counter pass of the same (tools/profile.sh SQ_PMC=1)
+#   calib                   FETCH_SIZE / WRITE_SIZE against known byte counts (tools/pmc_calib, built in-tree
+#                           beforehand) -> <TAG>_calib.json
 # e.g. bash tools/gpu_run.sh r04c tests:tests/test_gpu_lattice.py bench:c2 bench:c3:--config,c3,--steps,3 \
 #        ab:c2cg:CWF_LAT_CG=0 prof:c3:--config,c3,--steps,2,--warmup,1,--no-cpu-baseline
 set -o pipefail
@@ -67,6 +69,14 @@ for step in "$@"; do
       if [ $kind = sq ]; then python3 tools/sq_summary.py gpurun_out/prof_${TAG}_$a --kernel "$K" > $O/${a}_sq_summary.txt; unset SQ_PMC; fi
       rm -rf gpurun_out/prof_${TAG}_$a
       head -6 $O/${a}_summary.txt ;;
+    calib)
+      C=$R/gpurun_out/calib_$TAG; mkdir -p $C
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -k 10 120 $R/tools/pmc_calib > $C/known.json &&
+       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $C/fetch -o fetch -- $R/tools/pmc_calib > /dev/null &&
+       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $C/write -o write -- $R/tools/pmc_calib > /dev/null) || exit 4
+      python3 tools/pmc_calib.py $C > $O/calib.txt && cp $C/calib.json $O/calib.json && cat $O/calib.txt || exit 4
+      rm -rf $C ;;
     *) echo "unknown step $step"; exit 64 ;;
   esac
 done
