@@ -133,6 +133,8 @@ int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_
         for (size_t j = 0; j < nv; ++j)
             halo_pack(g[i], vecs[i][j], g[i]->stream, g[i]->sendbuf + 3 * g[i]->nsend * j);
     const bool gather = h0->nranks > 1;
+    if (h0->comm && h0->comm->kind == 2)
+        return (gather || nv) ? peer_exchange(h0, gathers, vecs.empty() ? std::vector<float *>{} : vecs[0]) : 0;
     if (h0->comm && h0->comm->kind == 1)
     {
         if (!gather && !nv)
@@ -574,6 +576,11 @@ void cwf_hip_comm_destroy(cwf_hip_comm *cm)
         (void)hipStreamSynchronize(cm->stream);
         (void)hipStreamDestroy(cm->stream);
     }
+    if (cm->kind == 2)
+    {
+        (void)hipDeviceSynchronize();
+        peer_release(cm);
+    }
     delete cm;
 }
 
@@ -722,6 +729,13 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
     h->comm = cm;
     h->rank = rank;
     h->nranks = n;
+    if (cm->kind == 2)
+    {
+        if (cm->peer_member || rank != cm->rank)
+            return set_error(h, CWF_ERR_ARGUMENT, "a peer communicator holds this process's rank only");
+        if (int st = peer_attach(h))
+            return st;
+    }
     if (cm->kind == 0)
     {
         HIPTRY(h, hipStreamSynchronize(h->stream));

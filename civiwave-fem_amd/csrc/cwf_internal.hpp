@@ -362,12 +362,22 @@ struct cwf_hip_system
 
 struct cwf_hip_comm
 {
-    int kind = 0;  // 0 = LOCAL (one process, one device, shared stream), 1 = RCCL
+    int kind = 0;  // 0 = LOCAL (one process, one device, shared stream), 1 = RCCL, 2 = PEER (peer.hip)
     int nranks = 1;
+    int rank = 0;  // RCCL / PEER: this process's rank
     int device = 0;
     void *nccl = nullptr;
     hipStream_t stream = nullptr;                // LOCAL: the stream every member enqueues on
     std::vector<cwf_hip_system *> members;       // LOCAL: by rank
+    // PEER: this rank's IPC-exported mailbox, the peers' mapped ones, their ghost counts and where my ghosts go
+    // in them, the exchange-step epoch and the push kernel's ticket
+    cwf_hip_system *peer_member = nullptr;
+    void *mbox = nullptr;
+    size_t mbox_bytes = 0;
+    uint32_t *ticket = nullptr;
+    std::vector<void *> peer_mbox;
+    std::vector<uint64_t> peer_nghost, peer_recv_off;
+    uint32_t epoch = 0;
 };
 
 namespace cwf
@@ -456,6 +466,11 @@ struct Gather
 int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                   float *cwf_hip_system::*vec);
 constexpr size_t kMaxHaloVecs = 3;  // halo vectors of one exchange step (the single-launch iteration's r, w, s)
+constexpr int kMaxPeers = 16;       // ranks of a PEER communicator
+// peer.hip: the PEER communicator's mailbox (at attach), its exchange step, and its teardown
+int peer_attach(cwf_hip_system *h);
+int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs);
+void peer_release(cwf_hip_comm *cm);
 int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                        const std::vector<std::vector<float *>> &vecs);
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);

@@ -1,0 +1,411 @@
+// peer.hip -- the PEER communicator: device-initiated exchange steps over IPC-mapped mailboxes (SURVEY.md 8e,
+// VERDICT r3 item 4). One process per rank, as RCCL; an exchange step (the all-gathers of per-rank scalar slots
+// and the halos of up to three vectors, comm_exchange_vecs) is three launches on the rank's stream instead of an
+// RCCL group:
+//
+//   k_peer_push    every workgroup stores its share of the packed send segments straight into the neighbours'
+//                  mailboxes (remote stores over xGMI; the same device's memory under IPC on one GPU) and
+//                  workgroup 0 this rank's scalar slots into every peer's; each workgroup releases at system
+//                  scope and takes a ticket; the last one stores the step's epoch into every peer's flag for
+//                  this rank (system-scope atomic store);
+//   k_peer_wait    one wave polls this rank's flags, one lane per peer, until every peer has reached the epoch
+//                  (bounded: a peer that never arrives ends the solve with CWF_ERR_COMM instead of a hang), then
+//                  acquires at system scope;
+//   k_peer_unpack  the received ghost rows and scalar slots into their vectors / slots (system-scope loads).
+//
+// A mailbox (one hipMalloc per rank, exported with hipIpcGetMemHandle) is a header with the rank's receive layout
+// (where each neighbour's ghosts go, read once by the peers at connect), one 64-B flag line per peer, and two
+// copies (by epoch parity) of the scalar-slot area and of the ghost receive area. Two copies suffice: a rank can
+// only push step e + 2 after waiting on step e + 1 of the receiver, which the receiver pushes after unpacking step
+// e. Only the FAST schedule goes through it (slots of <= 4 doubles); PARITY's chunk-partial all-gathers stay on
+// RCCL / LOCAL.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cwf_internal.hpp"
+
+#define HIPTRY(h, expr)                                                                                        \
+    do                                                                                                         \
+    {                                                                                                          \
+        hipError_t e__ = (expr);                                                                               \
+        if (e__ != hipSuccess)                                                                                 \
+            return hip_fail((h), e__, #expr);                                                                  \
+    } while (0)
+
+namespace cwf
+{
+namespace
+{
+constexpr uint64_t kPeerMagic = 0x43574650454552ull;  // "CWFPEER"
+constexpr size_t kHdrBytes = 4096, kFlagLine = 64, kSlot = 4;  // kSlot doubles per rank and gather
+constexpr int kMaxPeerGathers = 2;
+
+struct MboxHeader  // at offset 0 of every mailbox
+{
+    uint64_t magic, nranks, nghost, recv_off[kMaxPeers], recv_cnt[kMaxPeers];
+};
+static_assert(sizeof(MboxHeader) <= kHdrBytes, "mailbox header");
+
+inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+inline size_t off_flags() { return kHdrBytes; }
+inline size_t off_gath(int n) { return align256(off_flags() + kFlagLine * (size_t)n); }
+inline size_t gath_bytes(int n) { return (size_t)kMaxPeerGathers * n * kSlot * sizeof(double); }  // one parity
+inline size_t off_recv(int n) { return align256(off_gath(n) + 2 * gath_bytes(n)); }
+inline size_t recv_bytes(uint64_t nghost) { return kMaxHaloVecs * 3 * nghost * sizeof(float); }  // one parity
+
+struct PeerPush
+{
+    const float *send;  // [nv][3 nsend] packed segments
+    uint64_t nsend;
+    uint32_t nv, nnbr;
+    float *dst[kMaxPeers];       // per neighbour k: its receive area (this parity), my ghosts' first float
+    uint64_t dst_vstride[kMaxPeers];  // floats between vectors there (3 nghost of the neighbour)
+    uint64_t src_off[kMaxPeers], cnt[kMaxPeers];  // my send segment for k (nodes)
+    uint64_t total;              // sum over k of 3 cnt
+    uint32_t ng, gcount[kMaxPeerGathers];
+    const double *gsrc[kMaxPeerGathers];  // my slot of gather q
+    double *gdst[kMaxPeers];     // per rank p: p's gather area (this parity), my slot of gather 0
+    uint32_t *flag[kMaxPeers];   // per rank p: p's flag line for my rank
+    uint32_t nranks, rank, epoch;
+    uint32_t *cnt_ticket;
+};
+
+__global__ __launch_bounds__(256) void k_peer_push(PeerPush a)
+{
+    // halo rows: item t of the flattened (neighbour, vector, float) space, workgroup-strided
+    const uint64_t items = a.total * a.nv;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < items; t += (uint64_t)gridDim.x * 256)
+    {
+        uint64_t r = t % a.total;
+        const uint32_t v = (uint32_t)(t / a.total);
+        uint32_t k = 0;
+        while (k + 1 < a.nnbr && r >= 3 * a.cnt[k])
+            r -= 3 * a.cnt[k++];
+        a.dst[k][a.dst_vstride[k] * v + r] = a.send[3 * (a.nsend * v + a.src_off[k]) + r];
+    }
+    if (blockIdx.x == 0 && threadIdx.x < a.nranks * kMaxPeerGathers * kSlot)
+    {
+        const uint32_t p = threadIdx.x / (kMaxPeerGathers * kSlot), q = (threadIdx.x / kSlot) % kMaxPeerGathers,
+                       j = threadIdx.x % kSlot;
+        if (p != a.rank && q < a.ng && j < a.gcount[q])
+            a.gdst[p][(size_t)q * a.nranks * kSlot + j] = a.gsrc[q][j];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(a.cnt_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == gridDim.x)
+        {
+            __threadfence_system();
+            for (uint32_t p = 0; p < a.nranks; ++p)
+                if (p != a.rank)
+                    __hip_atomic_store(a.flag[p], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.cnt_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// one wave; lane p polls this rank's flag line of peer p
+__global__ __launch_bounds__(64) void k_peer_wait(const uint32_t *flags, uint32_t nranks, uint32_t rank, uint32_t epoch,
+                                                  Ctl *ctl)
+{
+    const uint32_t p = threadIdx.x;
+    bool ok = true;
+    if (p < nranks && p != rank)
+    {
+        const uint32_t *f = flags + (kFlagLine / 4) * p;
+        uint32_t spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch)
+        {
+            __builtin_amdgcn_s_sleep(8);
+            if (++spins > (1u << 24))  // ~seconds: the peer is gone
+            {
+                ok = false;
+                break;
+            }
+        }
+    }
+    if (!__all(ok) && threadIdx.x == 0)
+    {
+        ctl->error = CWF_ERR_COMM;
+        ctl->error_iter = (int)epoch;
+        ctl->active = 0;
+    }
+    __threadfence_system();
+}
+
+struct PeerUnpack
+{
+    const float *recv;  // this parity's receive area
+    uint64_t nghost, ghost0;  // ghosts are local nodes ghost0 .. ghost0 + nghost
+    uint32_t nv;
+    float *vec[kMaxHaloVecs];
+    const double *gath;  // this parity's gather area
+    uint32_t ng, gcount[kMaxPeerGathers], nranks, rank;
+    double *gbuf[kMaxPeerGathers];
+};
+
+__global__ __launch_bounds__(256) void k_peer_unpack(PeerUnpack a)
+{
+    const uint64_t per = 3 * a.nghost;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < per * a.nv; t += (uint64_t)gridDim.x * 256)
+    {
+        const uint32_t v = (uint32_t)(t / per);
+        const uint64_t i = t % per;
+        a.vec[v][3 * a.ghost0 + i] =
+            __hip_atomic_load(a.recv + per * v + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < a.nranks * kMaxPeerGathers * kSlot)
+    {
+        const uint32_t p = threadIdx.x / (kMaxPeerGathers * kSlot), q = (threadIdx.x / kSlot) % kMaxPeerGathers,
+                       j = threadIdx.x % kSlot;
+        if (p != a.rank && q < a.ng && j < a.gcount[q])
+            a.gbuf[q][(size_t)p * a.gcount[q] + j] =
+                __hip_atomic_load(a.gath + ((size_t)q * a.nranks + p) * kSlot + j, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+}  // namespace
+
+// attach of a PEER comm's member: the mailbox with this rank's receive layout in its header
+int peer_attach(cwf_hip_system *h)
+{
+    cwf_hip_comm *cm = h->comm;
+    const int n = cm->nranks;
+    const uint64_t nghost = h->ds.N - h->ds.Nown;
+    const size_t bytes = off_recv(n) + 2 * recv_bytes(nghost);
+    if (hipMalloc(&cm->mbox, bytes) != hipSuccess)
+        return set_error(h, CWF_ERR_ALLOC, "failed to allocate the peer mailbox", "bytes=" + std::to_string(bytes));
+    cm->mbox_bytes = bytes;
+    if (hipMalloc(reinterpret_cast<void **>(&cm->ticket), 64) != hipSuccess)
+        return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer");
+    HIPTRY(h, hipMemset(cm->mbox, 0, bytes));
+    HIPTRY(h, hipMemset(cm->ticket, 0, 64));
+    MboxHeader hd{};
+    hd.magic = kPeerMagic;
+    hd.nranks = (uint64_t)n;
+    hd.nghost = nghost;
+    for (int p = 0; p < kMaxPeers; ++p)
+        hd.recv_off[p] = ~0ull;
+    for (size_t k = 0; k < h->nbr.size(); ++k)
+    {
+        hd.recv_off[h->nbr[k]] = h->recv_off[k];
+        hd.recv_cnt[h->nbr[k]] = h->recv_off[k + 1] - h->recv_off[k];
+    }
+    HIPTRY(h, hipMemcpy(cm->mbox, &hd, sizeof hd, hipMemcpyHostToDevice));
+    cm->peer_member = h;
+    return 0;
+}
+
+void peer_release(cwf_hip_comm *cm)
+{
+    for (void *p : cm->peer_mbox)
+        if (p)
+            (void)hipIpcCloseMemHandle(p);
+    cm->peer_mbox.clear();
+    if (cm->mbox)
+        (void)hipFree(cm->mbox);
+    if (cm->ticket)
+        (void)hipFree(cm->ticket);
+    cm->mbox = nullptr;
+    cm->ticket = nullptr;
+}
+
+int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs)
+{
+    cwf_hip_comm *cm = h->comm;
+    const int n = cm->nranks;
+    if (cm->peer_mbox.size() != (size_t)n)
+        return set_error(h, CWF_ERR_COMM, "peer communicator not connected (cwf_hip_comm_peer_connect)");
+    if (gathers.size() > (size_t)kMaxPeerGathers)
+        return set_error(h, CWF_ERR_UNSUPPORTED, "the peer communicator carries at most two scalar all-gathers a step");
+    for (const Gather &q : gathers)
+        if (q.count > kSlot)
+            return set_error(h, CWF_ERR_UNSUPPORTED, "the peer communicator carries the FAST schedule only",
+                             "PARITY's chunk-partial all-gathers need RCCL or LOCAL");
+    const uint32_t epoch = ++cm->epoch;
+    const uint32_t par = epoch & 1u;
+    PeerPush a{};
+    a.send = h->sendbuf;
+    a.nsend = h->nsend;
+    a.nv = (uint32_t)vecs.size();
+    a.nnbr = (uint32_t)h->nbr.size();
+    for (uint32_t k = 0; k < a.nnbr; ++k)
+    {
+        const int q = h->nbr[k];
+        const uint64_t qg = cm->peer_nghost[q], qoff = cm->peer_recv_off[q];
+        char *base = static_cast<char *>(cm->peer_mbox[q]) + off_recv(n) + par * recv_bytes(qg);
+        a.dst[k] = reinterpret_cast<float *>(base) + 3 * qoff;
+        a.dst_vstride[k] = 3 * qg;
+        a.src_off[k] = h->send_off[k];
+        a.cnt[k] = h->send_off[k + 1] - h->send_off[k];
+        a.total += 3 * a.cnt[k];
+    }
+    a.ng = 0;
+    for (const Gather &q : gathers)
+    {
+        a.gcount[a.ng] = (uint32_t)q.count;
+        a.gsrc[a.ng] = h->*(q.buf) + (size_t)h->rank * q.count;
+        ++a.ng;
+    }
+    for (int p = 0; p < n; ++p)
+    {
+        char *pb = static_cast<char *>(p == h->rank ? cm->mbox : cm->peer_mbox[p]);
+        a.gdst[p] = reinterpret_cast<double *>(pb + off_gath(n) + par * gath_bytes(n)) + (size_t)h->rank * kSlot;
+        a.flag[p] = reinterpret_cast<uint32_t *>(pb + off_flags() + kFlagLine * (size_t)h->rank);
+    }
+    a.nranks = (uint32_t)n;
+    a.rank = (uint32_t)h->rank;
+    a.epoch = epoch;
+    a.cnt_ticket = cm->ticket;
+    // (comm_exchange_vecs packed the send segments on this stream)
+    const uint64_t items = a.total * a.nv;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((items + 1023) / 1024, 256));
+    k_peer_push<<<grid, 256, 0, h->stream>>>(a);
+    k_peer_wait<<<1, 64, 0, h->stream>>>(reinterpret_cast<const uint32_t *>(static_cast<char *>(cm->mbox) + off_flags()),
+                                         (uint32_t)n, (uint32_t)h->rank, epoch, h->ctl);
+    PeerUnpack u{};
+    const uint64_t nghost = h->ds.N - h->ds.Nown;
+    u.recv = reinterpret_cast<const float *>(static_cast<char *>(cm->mbox) + off_recv(n) + par * recv_bytes(nghost));
+    u.nghost = nghost;
+    u.ghost0 = h->ds.Nown;
+    u.nv = (uint32_t)vecs.size();
+    for (size_t v = 0; v < vecs.size(); ++v)
+        u.vec[v] = vecs[v];
+    u.gath = reinterpret_cast<const double *>(static_cast<char *>(cm->mbox) + off_gath(n) + par * gath_bytes(n));
+    u.ng = a.ng;
+    for (uint32_t q = 0; q < a.ng; ++q)
+    {
+        u.gcount[q] = a.gcount[q];
+        u.gbuf[q] = h->*(gathers.begin()[q].buf);
+    }
+    u.nranks = (uint32_t)n;
+    u.rank = (uint32_t)h->rank;
+    const uint64_t uitems = 3 * nghost * u.nv;
+    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uitems + 1023) / 1024, 256));
+    k_peer_unpack<<<ugrid, 256, 0, h->stream>>>(u);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(h, e, "peer exchange launch");
+}
+
+}  // namespace cwf
+
+using namespace cwf;
+
+extern "C" {
+
+int cwf_hip_comm_create_peer(int32_t nranks, int32_t rank, int device, cwf_hip_comm **out)
+{
+    if (!out)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    *out = nullptr;
+    if (nranks < 1 || nranks > kMaxPeers || rank < 0 || rank >= nranks)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "rank out of range", "peer communicators hold <= 16 ranks");
+    hipError_t he = hipSetDevice(device);
+    if (he != hipSuccess)
+        return hip_fail(nullptr, he, "hipSetDevice");
+    cwf_hip_comm *cm = new (std::nothrow) cwf_hip_comm();
+    if (!cm)
+        return set_error(nullptr, CWF_ERR_ALLOC, "host allocation failed");
+    cm->kind = 2;
+    cm->nranks = nranks;
+    cm->rank = rank;
+    cm->device = device;
+    *out = cm;
+    return 0;
+}
+
+int cwf_hip_comm_peer_handle(cwf_hip_comm *cm, uint8_t *handle)
+{
+    if (!cm || !handle || cm->kind != 2)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "not a peer communicator");
+    if (!cm->mbox)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "attach the rank's handle first");
+    (void)hipSetDevice(cm->device);
+    hipIpcMemHandle_t m;
+    const hipError_t e = hipIpcGetMemHandle(&m, cm->mbox);
+    if (e != hipSuccess)
+        return hip_fail(nullptr, e, "hipIpcGetMemHandle");
+    static_assert(sizeof m <= CWF_IPC_HANDLE_BYTES, "ipc handle size");
+    std::memset(handle, 0, CWF_IPC_HANDLE_BYTES);
+    std::memcpy(handle, &m, sizeof m);
+    return 0;
+}
+
+int cwf_hip_comm_peer_connect(cwf_hip_comm *cm, const uint8_t *handles)
+{
+    if (!cm || !handles || cm->kind != 2 || !cm->peer_member)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "attach the rank's handle to a peer communicator first");
+    cwf_hip_system *h = cm->peer_member;
+    (void)hipSetDevice(cm->device);
+    const int n = cm->nranks;
+    cm->peer_mbox.assign(n, nullptr);
+    cm->peer_nghost.assign(n, 0);
+    cm->peer_recv_off.assign(n, 0);
+    for (int p = 0; p < n; ++p)
+    {
+        if (p == cm->rank)
+            continue;
+        hipIpcMemHandle_t m;
+        std::memcpy(&m, handles + (size_t)p * CWF_IPC_HANDLE_BYTES, sizeof m);
+        void *ptr = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&ptr, m, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess)
+            return hip_fail(h, e, "hipIpcOpenMemHandle");
+        cm->peer_mbox[p] = ptr;
+        MboxHeader hd{};
+        HIPTRY(h, hipMemcpy(&hd, ptr, sizeof hd, hipMemcpyDeviceToHost));
+        if (hd.magic != kPeerMagic || hd.nranks != (uint64_t)n)
+            return set_error(h, CWF_ERR_COMM, "peer mailbox does not match this communicator",
+                             "peer=" + std::to_string(p));
+        cm->peer_nghost[p] = hd.nghost;
+        cm->peer_recv_off[p] = hd.recv_off[cm->rank];
+    }
+    // every neighbour expects exactly my send segment for it
+    for (size_t k = 0; k < h->nbr.size(); ++k)
+    {
+        const int q = h->nbr[k];
+        MboxHeader hd{};
+        HIPTRY(h, hipMemcpy(&hd, cm->peer_mbox[q], sizeof hd, hipMemcpyDeviceToHost));
+        if (hd.recv_off[cm->rank] == ~0ull || hd.recv_cnt[cm->rank] != h->send_off[k + 1] - h->send_off[k])
+            return set_error(h, CWF_ERR_COMM, "halo plans disagree",
+                             "rank=" + std::to_string(cm->rank) + "\npeer=" + std::to_string(q));
+    }
+    return 0;
+}
+
+// `steps` exchange steps of the single-launch iteration's shape (one 4-double slot all-gather, the r, w, s halos)
+// on h's stream, hipEvent-timed: the per-step latency the 8-GPU projection uses (every rank calls it)
+int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_step)
+{
+    if (!h || !us_per_step || steps < 1 || !h->sharded() || !h->comm)
+        return set_error(h, CWF_ERR_ARGUMENT, "an attached handle and steps >= 1");
+    (void)hipSetDevice(h->device);
+    hipEvent_t e0, e1;
+    HIPTRY(h, hipEventCreate(&e0));
+    HIPTRY(h, hipEventCreate(&e1));
+    std::vector<cwf_hip_system *> g{h};
+    std::vector<std::vector<float *>> vecs{{h->r, h->Ap, h->z}};
+    int st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);  // warm
+    if (!st && hipEventRecord(e0, h->stream) != hipSuccess)
+        st = set_error(h, CWF_ERR_HIP, "hipEventRecord");
+    for (int i = 0; i < steps && !st; ++i)
+        st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);
+    float ms = 0.f;
+    if (!st && hipEventRecord(e1, h->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess)
+        (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *us_per_step = 1e3 * (double)ms / steps;
+    return st;
+}
+
+}  // extern "C"

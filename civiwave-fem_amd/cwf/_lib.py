@@ -94,6 +94,7 @@ class FrameViewC(C.Structure):
 
 
 COMM_ID_BYTES = 128
+IPC_HANDLE_BYTES = 64  # CWF_IPC_HANDLE_BYTES
 
 _lib = None
 
@@ -161,6 +162,10 @@ def load() -> C.CDLL:
         "cwf_hip_comm_create_rccl": ([i32, i32, P, i32, P], i32),
         "cwf_hip_comm_create_local": ([i32, i32, P], i32),
         "cwf_hip_comm_destroy": ([P], None),
+        "cwf_hip_comm_create_peer": ([i32, i32, i32, P], i32),
+        "cwf_hip_comm_peer_handle": ([P, P], i32),
+        "cwf_hip_comm_peer_connect": ([P, P], i32),
+        "cwf_hip_comm_time_exchange": ([P, i32, P], i32),
         "cwf_hip_system_attach": ([P, P, i32, P], i32),
         "cwf_hip_solve_pcg_group": ([P, i32, P, P, P, P, i32, P], i32),
         "cwf_preprocess_tets": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),

@@ -186,6 +186,36 @@ class Comm:
         return cls(h, nranks, "rccl")
 
     @classmethod
+    def peer(cls, nranks: int, rank: int, device: int = 0) -> "Comm":
+        """PEER (peer.hip): one process per rank; after attach, exchange `handle()` between the processes and
+        `connect(handles)` with all of them in rank order."""
+        h = C.c_void_p()
+        if _lib.load().cwf_hip_comm_create_peer(nranks, rank, device, C.byref(h)):
+            raise RuntimeError(f"peer communicator: {_lib.last_error(None)}")
+        return cls(h, nranks, "peer")
+
+    def handle(self) -> bytes:
+        buf = (C.c_uint8 * _lib.IPC_HANDLE_BYTES)()
+        if _lib.load().cwf_hip_comm_peer_handle(self._h, buf):
+            raise RuntimeError(f"peer handle: {_lib.last_error(None)}")
+        return bytes(buf)
+
+    def connect(self, handles: list):
+        blob = b"".join(handles)
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        if _lib.load().cwf_hip_comm_peer_connect(self._h, buf):
+            raise RuntimeError(f"peer connect: {_lib.last_error(None)}")
+
+    @staticmethod
+    def time_exchange(system: MatrixFreeSystem, steps: int = 200) -> float:
+        """microseconds per exchange step of the single-launch iteration's shape (collective)"""
+        us = C.c_double()
+        h = system.handle()
+        if _lib.load().cwf_hip_comm_time_exchange(h, steps, C.byref(us)):
+            raise RuntimeError(f"time exchange: {_lib.last_error(h)}")
+        return us.value
+
+    @classmethod
     def local(cls, nranks: int, device: int = 0) -> "Comm":
         h = C.c_void_p()
         if _lib.load().cwf_hip_comm_create_local(nranks, device, C.byref(h)):

@@ -307,6 +307,21 @@ int cwf_hip_comm_create_rccl(int32_t nranks, int32_t rank, const uint8_t *id, in
 int cwf_hip_comm_create_local(int32_t nranks, int device, cwf_hip_comm **out);
 void cwf_hip_comm_destroy(cwf_hip_comm *comm); /* after every attached handle is destroyed */
 
+/* PEER: one process per rank, as RCCL, but the FAST exchange steps (the per-rank scalar all-gathers and the
+ * halos) are device-initiated stores into the peers' IPC-mapped mailboxes plus a flag per step (peer.hip; the
+ * "one-shot P2P" of SURVEY.md section 7 (iv)); PARITY's chunk-partial all-gathers are refused
+ * (CWF_ERR_UNSUPPORTED: use RCCL). Setup: create, cwf_hip_system_attach (allocates this rank's mailbox),
+ * cwf_hip_comm_peer_handle, exchange the handles between the processes (e.g. torch.distributed
+ * all_gather_object), cwf_hip_comm_peer_connect with every rank's handle in rank order. Replaces the RCCL
+ * group calls comm.cpp issues where pcg.cpp:170-207's dots would cross ranks. <= 16 ranks. */
+#define CWF_IPC_HANDLE_BYTES 64
+int cwf_hip_comm_create_peer(int32_t nranks, int32_t rank, int device, cwf_hip_comm **out);
+int cwf_hip_comm_peer_handle(cwf_hip_comm *comm, uint8_t *handle /* [CWF_IPC_HANDLE_BYTES] */);
+int cwf_hip_comm_peer_connect(cwf_hip_comm *comm, const uint8_t *handles /* [nranks * CWF_IPC_HANDLE_BYTES] */);
+/* `steps` exchange steps shaped like one single-launch PCG iteration's (a 4-double slot all-gather and three
+ * halos) on the attached handle's stream, hipEvent-timed: microseconds per step (collective: every rank calls) */
+int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_step);
+
 /* Make `h` (created from a shard's local desc with CWF_DESC_KEEP_NODE_ORDER) rank `rank` of `comm` with the
  * shard's halo plan. Afterwards solve_pcg / stepper_step are collective: scalars are all-gathered and folded
  * in rank order on every rank (identical control flow everywhere), ghost DOFs are refreshed by the halo

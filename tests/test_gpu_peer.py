@@ -1,0 +1,119 @@
+"""The PEER communicator (peer.hip): 2 and 3 processes on one GPU, each rank's mailbox IPC-mapped by the others.
+
+The exchange steps are device-initiated stores into the peers' mailboxes and a flag per step instead of RCCL
+groups; the kernels, fold orders and halo plans above them are the ones the LOCAL communicator runs, so:
+- the single-launch (Chronopoulos-Gear) iteration on slab sub-meshes (one exchange step per iteration: the rank
+  triples and the r, w, s halos) equals the LOCAL solve of the same decomposition bit for bit;
+- so does the two-kernel FAST iteration on a global-mesh node partition (two steps per iteration);
+- a PARITY solve over PEER is refused (its chunk-partial all-gathers stay on RCCL / LOCAL);
+- the exchange latency per step is measured (printed; DESIGN.md section 7 uses it). Two processes on one GPU
+  share its CUs, so this is the protocol's latency on one device, not an xGMI figure."""
+import multiprocessing as mp
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from cwf import _lib, pcg, scenarios, shard
+from helpers import assert_bitwise, oracle_system
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(spec, nranks):
+    import transport_worker
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    rdv = tempfile.mkdtemp(prefix="cwf_peer.")
+    procs = [ctx.Process(target=transport_worker.run_rank_peer, args=(k, nranks, rdv, spec, q)) for k in range(nranks)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(nranks):
+        rank, status, payload = q.get(timeout=240)
+        assert status == "ok", f"rank {rank}: {payload}"
+        out[rank] = payload
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def _local_slab(shape, nranks, tol, mi):
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=tol, max_iterations=mi)
+    sK, sM = glob.scalars()
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs = [], [], [], []
+    for r in range(nranks):
+        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, tol=tol)
+        src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
+        sh = shard.build_shard(src, begin, r, node_global)
+        s = sh.system(glob.materials, sK, sM)
+        comm.attach(s, sh)
+        systems.append(s)
+        shards.append(sh)
+        rhs.append(sh.local_dofs(case.static_rhs()))
+        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    t = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(mi, tol), xs).value()
+    x = np.zeros((glob.packing.node_count, 3), np.float32)
+    for sh, v in zip(shards, xs):
+        x[sh.node_global[: sh.owned_nodes].astype(np.int64)] = v.reshape(-1, 3)[: sh.owned_nodes]
+    comm.close()
+    return glob, t, x.reshape(-1)
+
+
+def _assemble(out, n):
+    x = np.zeros((n, 3), np.float32)
+    for d in out.values():
+        x[d["nodes"]] = d["x"].reshape(-1, 3)
+    return x.reshape(-1)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_peer_single_launch_slabs_equal_local(nranks):
+    shape = (13, 9, 4)
+    spec = dict(slab=shape, tol=1e-6, max_iterations=800)
+    out = _run(spec, nranks)
+    glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
+    x = _assemble(out, glob.packing.node_count)
+    for d in out.values():
+        assert d["kernel"].startswith("k_cg_lattice"), d["kernel"]
+        assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
+        assert d["parity_error"]  # refused (unaligned chunks or the FAST-only transport), never a hang
+    assert_bitwise(x, xl, "PEER single-launch x vs LOCAL")
+    ref = oracle_system(glob.packing, glob.materials, *glob.scalars()).solve_pcg(glob.static_rhs(), 800, 1e-6)
+    assert tl.converged
+    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    print(f"PEER exchange step, {nranks} processes on one GPU: "
+          + ", ".join(f"rank {k} {d['exchange_us']:.2f} us" for k, d in sorted(out.items())))
+
+
+def test_peer_two_kernel_iteration_equals_local():
+    nranks = 2
+    glob = scenarios.block_case(10, 6, 12, h=0.1, tol=1e-6, max_iterations=800)
+    P = glob.packing
+    sK, sM = glob.scalars()
+    ranges = shard.slab_ranges(P.node_count, nranks)
+    spec = dict(block=(10, 6, 12), tol=1e-6, max_iterations=800, ranges=[int(v) for v in ranges])
+    out = _run(spec, nranks)
+    comm = shard.Comm.local(nranks)
+    systems, shards, rhs, xs = [], [], [], []
+    for k in range(nranks):
+        src = pcg.MatrixFreeSystem.from_packing(P, glob.materials, sK, sM, mode=_lib.MODE_FAST)
+        sh = shard.build_shard(src, ranges, k)
+        s = sh.system(glob.materials, sK, sM)
+        comm.attach(s, sh)
+        systems.append(s)
+        shards.append(sh)
+        rhs.append(sh.local_dofs(glob.static_rhs()))
+        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
+    tl = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(800, 1e-6), xs).value()
+    xl = np.zeros((P.node_count, 3), np.float32)
+    for sh, v in zip(shards, xs):
+        xl[sh.node_global[: sh.owned_nodes].astype(np.int64)] = v.reshape(-1, 3)[: sh.owned_nodes]
+    comm.close()
+    for d in out.values():
+        assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
+    assert_bitwise(_assemble(out, P.node_count), xl.reshape(-1), "PEER two-kernel x vs LOCAL")

@@ -101,3 +101,68 @@ def run_rank(rank, nranks, uid, spec, queue):
         import traceback
 
         queue.put((rank, "error", f"{e!r}\n{traceback.format_exc()}"))
+
+
+def run_rank_peer(rank, nranks, rdv, spec, queue):
+    """One rank over the PEER communicator (peer.hip): the IPC handles of the ranks' mailboxes are exchanged through
+    files in the rendezvous directory `rdv`. spec["slab"] = (nx, ny, nz per rank): the bench's slab sub-meshes
+    (structured block: the single-launch iteration unless spec["env"] switches it off); else spec["ranges"] over
+    the global block. Returns the owned x, the telemetry, the exchange latency and the error of a PARITY solve."""
+    try:
+        import time
+
+        import numpy as np
+
+        for k, v in spec.get("env", {}).items():
+            os.environ[k] = v
+        from cwf import _lib, pcg, scenarios, shard
+
+        if spec.get("slab"):
+            shape = tuple(spec["slab"])
+            glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=spec["tol"],
+                                        max_iterations=spec["max_iterations"])
+            sK, sM = glob.scalars()
+            case, node_global, begin = scenarios.slab_case_shape(shape, nranks, rank, tol=spec["tol"])
+            src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
+            sh = shard.build_shard(src, begin, rank, node_global)
+            rhs = sh.local_dofs(case.static_rhs())
+        else:
+            glob = case_for(spec)
+            sK, sM = glob.scalars()
+            src = pcg.MatrixFreeSystem.from_packing(glob.packing, glob.materials, sK, sM, mode=_lib.MODE_FAST)
+            sh = shard.build_shard(src, np.asarray(spec["ranges"], np.uint64), rank)
+            rhs = sh.local_dofs(glob.static_rhs())
+        s = sh.system(glob.materials, sK, sM)
+        comm = shard.Comm.peer(nranks, rank, 0)
+        comm.attach(s, sh)
+        with open(os.path.join(rdv, f"rank{rank}.tmp"), "wb") as fh:
+            fh.write(comm.handle())
+        os.replace(os.path.join(rdv, f"rank{rank}.tmp"), os.path.join(rdv, f"rank{rank}.bin"))
+        t0 = time.time()
+        while not all(os.path.exists(os.path.join(rdv, f"rank{p}.bin")) for p in range(nranks)):
+            if time.time() - t0 > 120:
+                raise RuntimeError("rendezvous timed out")
+            time.sleep(0.05)
+        comm.connect([open(os.path.join(rdv, f"rank{p}.bin"), "rb").read() for p in range(nranks)])
+        kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
+        x = np.zeros(3 * sh.local_nodes, np.float32)
+        res = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]), pcg.PcgVectors(x))
+        if not res.has_value():
+            queue.put((rank, "error", str(res.error())))
+            return
+        t = res.value()
+        us = shard.Comm.time_exchange(s, spec.get("timing_steps", 200))
+        # PARITY over PEER is refused (its chunk-partial all-gathers need RCCL / LOCAL)
+        _lib.load().cwf_hip_system_set_mode(s.handle(), _lib.MODE_PARITY)
+        pres = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, spec["tol"]), pcg.PcgVectors(np.zeros_like(x)))
+        perr = None if pres.has_value() else pres.error().message
+        own = 3 * sh.owned_nodes
+        queue.put((rank, "ok", dict(telemetry=(t.iterations, t.converged, t.residual_norm), kernel=kern,
+                                    nodes=sh.node_global[: sh.owned_nodes].astype(np.int64), x=x[:own].copy(),
+                                    exchange_us=us, parity_error=perr)))
+        s.close()
+        comm.close()
+    except Exception as e:
+        import traceback
+
+        queue.put((rank, "error", f"{e!r}\n{traceback.format_exc()}"))
