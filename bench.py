@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-iterations", type=int, default=40)
     ap.add_argument("--no-general-roofline", action="store_true",
                     help="skip roofline_general (the fan-group tiles kernel on C3 with the lattice stencil off)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "peer"],
+                    help="N>1 exchange steps: RCCL groups, or the PEER communicator's device-initiated stores into "
+                         "IPC-mapped mailboxes (FAST only)")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the 'general' block (the same workload on the fan-group tiles, CWF_LATTICE=0)")
     ap.add_argument("--no-hbm-roofline", action="store_true",
@@ -325,10 +328,17 @@ def main():
         src = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=mode)  # host arrays only
         sh = shard.build_shard(src, begin, rank, node_global)
         system = sh.system(case.materials, 1.0, 0.0, device=device)
-        uid = [shard.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = shard.Comm.rccl(world, rank, uid[0], device)
-        comm.attach(system, sh)
+        if args.comm == "peer":  # device-initiated stores into IPC-mapped mailboxes (peer.hip)
+            comm = shard.Comm.peer(world, rank, device)
+            comm.attach(system, sh)
+            handles = [None] * world
+            dist.all_gather_object(handles, comm.handle())
+            comm.connect(handles)
+        else:
+            uid = [shard.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = shard.Comm.rccl(world, rank, uid[0], device)
+            comm.attach(system, sh)
 
         class _LocalPacking:  # the Stepper's view of the shard: local node order, local vectors
             external_force = sh.local_dofs(P.external_force)
@@ -464,7 +474,8 @@ def main():
                        ("hexes_per_gpu" if args.element == "hex8" else "tets_per_gpu"): local_tets,
                        "dofs": int(dofs_sum), "mode": args.mode,
                        "parallelism": (f"{'RCB' if unstructured else 'slab'} node-range shards x{world} "
-                                       f"(RCCL halo + all-gather, {'strong' if strong else 'weak'} scaling)")
+                                       f"({'PEER mailbox' if args.comm == 'peer' else 'RCCL'} halo + all-gather, "
+                                       f"{'strong' if strong else 'weak'} scaling)")
                        if world > 1 else "single"},
             "ranks": per_rank if world > 1 else None,
             "pcg_iterations": int(iters_sum),
