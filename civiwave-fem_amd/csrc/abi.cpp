@@ -1,6 +1,7 @@
-// abi.cpp -- C-ABI (include/cwf_hip.h) over the gfx950 kernels: handle lifetime, HBM upload,
-// apply_keff / block-Jacobi / dot / solve_pcg / Stepper orchestration. One HIP stream per
-// handle; the PCG loop is enqueued in batches and only the 104-B control block is read back.
+// abi.cpp -- C-ABI (include/cwf_hip.h) over the gfx950 kernels: handle lifetime (validation, HBM layout and
+// upload, the FAST tilings and the structured-block detection), mode / scalar / timing switches and the
+// measurement entry points. One HIP stream per handle. The PCG entry points are in abi_pcg.cpp, the Stepper in
+// abi_stepper.cpp, the communicators in comm.cpp and peer.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,42 +55,10 @@ uint32_t hex_tile_lanes(uint64_t hexes)
 
 using namespace cwf;
 
-#define HIPTRY(h, expr)                                                                                        \
-    do                                                                                                         \
-    {                                                                                                          \
-        hipError_t e__ = (expr);                                                                               \
-        if (e__ != hipSuccess)                                                                                 \
-            return hip_fail((h), e__, #expr);                                                                  \
-    } while (0)
+#include "abi_internal.hpp"
 
-namespace
+namespace cwf
 {
-
-template <class T> int dalloc(cwf_hip_system *h, T **p, size_t count)
-{
-    void *q = nullptr;
-    const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
-    hipError_t e = hipMalloc(&q, bytes);
-    if (e != hipSuccess)
-        return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer",
-                         "bytes=" + std::to_string(bytes));
-    h->owned.push_back(q);
-    h->bytes += bytes;
-    *p = static_cast<T *>(q);
-    return 0;
-}
-
-// the Dirichlet mask can ride in node_part_off's top bits when the offsets leave them free
-inline bool ht_off_mask_ok(const std::vector<uint32_t> &npo) { return npo.back() <= cwf::kPartOffBits; }
-
-template <class T> int upload(cwf_hip_system *h, T **dst, const T *src, size_t count)
-{
-    if (int st = dalloc(h, dst, count))
-        return st;
-    if (count)
-        HIPTRY(h, hipMemcpy(*dst, src, count * sizeof(T), hipMemcpyHostToDevice));
-    return 0;
-}
 
 bool iso_pattern(const double *D)
 {
@@ -298,213 +267,7 @@ uint32_t group_lanes(uint64_t E)
     return gn && atoi(gn) == 128 ? 128u : 256u;
 }
 
-std::string pcg_error_message(int code, int iter, std::string *ctx)
-{
-    if (code == CWF_ERR_DENOM_ZERO)
-    {
-        *ctx = "iteration=" + std::to_string(iter);
-        return "CG denominator approached zero";  // pcg.cpp:846-849
-    }
-    if (code == CWF_ERR_RHO_ZERO && iter < 0)
-    {
-        *ctx = "rho~0";
-        return "preconditioner produced near-zero rho";  // pcg.cpp:810-813
-    }
-    *ctx = "iteration=" + std::to_string(iter);
-    return "CG rho approached zero";  // pcg.cpp:889-892
-}
-
-// run solve_pcg on device buffers: rhs[i] and g[i]->x (holding the warm start) for every member of a
-// group -- one handle, or every rank of a sharded system driven from this process (LOCAL comm).
-int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
-                  const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
-{
-    cwf_hip_system *h = g[0];
-    if (set.max_iterations == 0)
-        return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
-    const bool sharded = h->sharded();
-    if (!sharded && g.size() != 1)
-        return set_error(h, CWF_ERR_ARGUMENT, "a group needs attached shards");
-    for (cwf_hip_system *m : g)
-        if (m->mode != h->mode)
-            return set_error(m, CWF_ERR_ARGUMENT, "every rank of a sharded solve runs in the same mode",
-                             "rank=" + std::to_string(m->rank));
-    for (cwf_hip_system *m : g)
-        if (m->hist_cap < set.max_iterations + 1)
-        {
-            if (m->hist)
-                (void)hipFree(m->hist);
-            m->hist = nullptr;
-            const uint64_t cap = std::max<uint64_t>(set.max_iterations + 1, 1024);
-            if (hipMalloc(reinterpret_cast<void **>(&m->hist), cap * sizeof(double)) != hipSuccess)
-                return set_error(m, CWF_ERR_ALLOC, "failed to grow matrix-free workspace buffers",
-                                 "history=" + std::to_string(cap));
-            m->hist_cap = cap;
-        }
-    hipStream_t st = h->stream;
-    if (!set.warm_start)
-        for (cwf_hip_system *m : g)
-            HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
-    const bool fast = h->mode == CWF_MODE_FAST;
-    bool cg = fast;  // one launch per iteration (structured blocks, every member)
-    for (cwf_hip_system *m : g)
-        cg = cg && fast_cg_enabled(m);
-    if (cg && sharded)
-    {
-        if (int e = sharded_cg_init(g, rhs, set.relative_tolerance))
-            return e;
-    }
-    else if (cg)
-        fast_cg_init(h, rhs[0], set.relative_tolerance, st);
-    else if (sharded)
-    {
-        if (int e = fast ? sharded_pcg_init(g, rhs, set.relative_tolerance)
-                         : sharded_parity_init(g, rhs, set.relative_tolerance))
-            return e;
-    }
-    else if (fast)
-        fast_pcg_init(h, rhs[0], set.relative_tolerance, st);
-    else
-        parity_pcg_init(h, rhs[0], set.relative_tolerance, st);
-    HIPTRY(h, hipGetLastError());
-    uint64_t enq = 0;
-    constexpr uint64_t kMaxBatch = 64;
-    uint64_t batch = set.check_interval > 0 ? std::min<uint64_t>((uint64_t)set.check_interval, kMaxBatch) : 4;
-    // Batches end in a control-block read-back (a host round trip with the GPU idle) and overshoot the
-    // converging iteration by up to a batch of no-op launches. Consecutive solves on one handle (warm-started
-    // Newmark steps) take similar iteration counts, so with no check interval set and the handle's last two
-    // solves within 25% of each other, the first batch runs up to 24 short of the smaller count and the
-    // doubling restarts from 4 there: C2 steps ~17 read-backs and ~50 no-op iterations -> ~4 and <= 8. A
-    // handle whose counts moved (its first solves, a static solve before Newmark steps, a changed tolerance)
-    // doubles from 4, so a solve that converges early never waits on a long queue of no-op launches. Every
-    // rank of a sharded solve has the same history (identical scalars), so their enqueued counts stay equal.
-    uint64_t first = batch;
-    const uint64_t lo = std::min(h->last_iters, h->prev_iters), hi = std::max(h->last_iters, h->prev_iters);
-    if (set.check_interval <= 0 && lo > 40 && 4 * hi <= 5 * lo)
-    {
-        first = std::min<uint64_t>(lo - 24, kMaxFirstBatch);
-        batch = 4;
-    }
-    if (h->timing && h->ev.size() < 2 * std::max(first, kMaxBatch))
-    {
-        const size_t had = h->ev.size();
-        h->ev.resize(2 * std::max(first, kMaxBatch));
-        for (size_t i = had; i < h->ev.size(); ++i)
-            HIPTRY(h, hipEventCreateWithFlags(&h->ev[i], hipEventDisableSystemFence));  // no L2 write-back per timed launch
-    }
-    uint64_t prev_enq = 0, prev_nb = 0;
-    for (;;)
-    {
-        // every member's control block is identical (rank-order folds); member 0's is polled
-        HIPTRY(h, hipMemcpyAsync(h->ctl_host, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
-        HIPTRY(h, hipStreamSynchronize(st));
-        if (h->timing && prev_nb)
-        {
-            // only launches that did work: iteration index < completed iterations
-            for (uint64_t i = 0; i < prev_nb; ++i)
-            {
-                if (prev_enq + i >= h->ctl_host->iterations)
-                    break;
-                if ((prev_enq + i) % (uint64_t)h->timing)
-                    continue;
-                float ms = 0.f;
-                if (hipEventElapsedTime(&ms, h->ev[2 * i], h->ev[2 * i + 1]) == hipSuccess)
-                {
-                    h->keff_ms += ms;
-                    ++h->keff_count;
-                }
-            }
-            prev_nb = 0;
-        }
-        if (!h->ctl_host->active || enq >= set.max_iterations)
-            break;
-        const uint64_t nb = std::min<uint64_t>(enq ? batch : first, set.max_iterations - enq);
-        for (uint64_t i = 0; i < nb; ++i)
-        {
-            const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
-            hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
-            if (cg && sharded)
-            {
-                if (int e = sharded_cg_iteration(g, (unsigned)(enq + i), e0, e1))
-                    return e;
-            }
-            else if (cg)
-                fast_cg_iteration(h, (unsigned)(enq + i), st, e0, e1);
-            else if (fast)
-            {
-                if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
-                    return e;
-            }
-            else if (sharded)
-            {
-                if (int e = sharded_parity_iteration(g, rhs, e0, e1))
-                    return e;
-            }
-            else
-                parity_pcg_iteration(h, rhs[0], st, e0, e1);
-        }
-        if (cg)
-            for (cwf_hip_system *m : g)
-                fast_cg_check(m, (unsigned)(enq + nb), m->stream);
-        else if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
-            for (cwf_hip_system *m : g)
-                fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
-        HIPTRY(h, hipGetLastError());
-        prev_enq = enq;
-        prev_nb = nb;
-        enq += nb;
-        if (set.check_interval <= 0)
-            batch = std::min<uint64_t>(batch * 2, kMaxBatch);
-    }
-    if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
-        for (size_t i = 0; i < g.size(); ++i)
-            fast_flush_x(g[i], rhs[i], g[i]->stream);
-    if (cg && (h->ctl_host->iterations & 1u))  // r_n lives in the second buffer for odd n
-        for (cwf_hip_system *m : g)
-            HIPTRY(m, hipMemcpyAsync(m->r, m->cg_r2, m->ds.D * sizeof(float), hipMemcpyDeviceToDevice, m->stream));
-    if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows
-    {
-        if (int e = comm_halo(g, &cwf_hip_system::x))
-            return e;
-        for (cwf_hip_system *m : g)
-            HIPTRY(m, hipStreamSynchronize(m->stream));
-    }
-    const Ctl &c = *h->ctl_host;
-    for (cwf_hip_system *m : g)
-    {
-        m->hist_count = c.iterations + 1;
-        m->prev_iters = m->last_iters;
-        m->last_iters = c.iterations;
-    }
-    if (tel)
-    {
-        tel->iterations = c.iterations;
-        tel->residual_norm = c.res;
-        tel->rhs_norm = c.rhs_norm_raw;
-        tel->alpha_last = c.alpha_last;
-        tel->beta_last = c.beta_last;
-        tel->converged = c.converged;
-        tel->reserved = 0;
-    }
-    if (c.error)
-    {
-        std::string ctx;
-        std::string msg = pcg_error_message(c.error, c.error_iter, &ctx);
-        for (size_t i = 1; i < g.size(); ++i)
-            set_error(g[i], c.error, msg, ctx);
-        return set_error(h, c.error, msg, ctx);
-    }
-    return 0;
-}
-
-int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
-{
-    if (h->comm && h->comm->kind == 0 && h->nranks > 1)
-        return set_error(h, CWF_ERR_UNSUPPORTED, "a LOCAL-communicator shard solves through cwf_hip_solve_pcg_group");
-    return run_pcg_group({h}, {rhs_dev}, set, tel);
-}
-
-}  // namespace
+}  // namespace cwf
 
 extern "C" {
 
@@ -1608,541 +1371,6 @@ int cwf_hip_derived_fields(cwf_hip_system *h, const float *u, uint64_t n, int u_
     derived_fields(h, uin, de, dn, h->stream);
     HIPTRY(h, hipGetLastError());
     HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_apply_keff(cwf_hip_system *h, const float *x, float *y, uint64_t n, int kind)
-{
-    if (int st = check_ready(h))
-        return st;
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "input/output span size mismatch",
-                         "input=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
-    const float *xin = nullptr;
-    if (int st = stage_vec(h, x, h->tmp, kind, 3, &xin))
-        return st;
-    float *yout = kind == CWF_PTR_DEVICE && !h->perm ? y : h->Ap;
-    if (h->mode == CWF_MODE_FAST)
-        fast_keff(h, xin, yout, true, nullptr, nullptr, h->stream);
-    else
-        parity_keff(h, xin, yout, true, nullptr, h->stream);
-    HIPTRY(h, hipGetLastError());
-    if (int st = vec_out(h, yout, y, kind, 3))
-        return st;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_build_block_jacobi_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int kind)
-{
-    if (int st = check_ready(h))
-        return st;
-    const uint64_t req = 9ull * h->ds.N;
-    if (n < req)
-        return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
-                         "required=" + std::to_string(req) + "\navailable=" + std::to_string(n));
-    float *dst = kind == CWF_PTR_DEVICE && !h->perm ? inv_out : h->inv;
-    if (dst == h->inv)
-        h->inv_fast = false;  // overwritten with the unsymmetrised reference inverse
-    if (h->ds.hex)
-        hex_block_jacobi(h, dst, h->stream);
-    else
-        parity_block_jacobi(h, dst, h->stream);
-    HIPTRY(h, hipGetLastError());
-    if (int st = vec_out(h, dst, inv_out, kind, 9))
-        return st;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_fast_block_inverse(cwf_hip_system *h, float *inv_out, uint64_t n, int kind, uint32_t *packed_out,
-                               uint64_t *fallback_nodes)
-{
-    if (int st = check_ready(h))
-        return st;
-    const uint64_t N = h->ds.N, req = 9ull * N;
-    if (n < req)
-        return set_error(h, CWF_ERR_SIZE, "block inverse span too small",
-                         "required=" + std::to_string(req) + "\navailable=" + std::to_string(n));
-    if (h->mode != CWF_MODE_FAST)
-        return set_error(h, CWF_ERR_ARGUMENT, "FAST-mode operator requested on a PARITY handle");
-    fast_block_inverse(h, h->stream);
-    HIPTRY(h, hipGetLastError());
-    if (int st = vec_out(h, h->inv, inv_out, kind, 9))
-        return st;
-    if (packed_out || fallback_nodes)
-    {
-        std::vector<uint32_t> w(4 * N);
-        if (N)
-            HIPTRY(h, hipMemcpyAsync(w.data(), h->inv6, 16 * N, hipMemcpyDeviceToHost, h->stream));
-        HIPTRY(h, hipStreamSynchronize(h->stream));
-        std::vector<uint32_t> perm;  // caller's node of internal node i
-        if (h->perm)
-        {
-            perm.resize(N);
-            HIPTRY(h, hipMemcpy(perm.data(), h->perm, 4 * N, hipMemcpyDeviceToHost));
-        }
-        std::vector<uint32_t> out(4 * N);
-        uint64_t nf = 0;
-        for (uint64_t i = 0; i < N; ++i)
-        {
-            const uint64_t c = h->perm ? perm[i] : i;
-            for (int k = 0; k < 4; ++k)
-                out[4 * c + k] = w[4 * i + k];
-            nf += (int32_t)w[4 * i] < 0;
-        }
-        if (packed_out)
-            std::memcpy(packed_out, out.data(), out.size() * sizeof(uint32_t));
-        if (fallback_nodes)
-            *fallback_nodes = nf;
-    }
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_pack_block_inverse(const float *v, uint32_t mask, uint32_t *w, float *d)
-{
-    if (!v || !w || !d)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
-    return cwf::pack_block_inverse(v, mask, w, d) ? 1 : 0;
-}
-
-int cwf_hip_dot(cwf_hip_system *h, const float *a, const float *b, uint64_t n, int kind, double *out,
-                double *partials)
-{
-    if (int st = check_ready(h))
-        return st;
-    if (!out)
-        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "dot product span size mismatch",
-                         "lhs=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
-    const float *da = nullptr, *db = nullptr;
-    if (int st = stage_in(h, a, h->tmp, n, kind, &da))
-        return st;
-    if (int st = stage_in(h, b, h->Ap, n, kind, &db))
-        return st;
-    double *res = h->scal;
-    uint32_t count;
-    if (h->mode == CWF_MODE_FAST)
-    {
-        count = fast_dot_blocks(h->ds.D);
-        fast_dot(da, db, nullptr, h->ds.D, h->part0, nullptr, h->stream);
-        fast_fold(h->part0, count, res, h->stream);
-    }
-    else
-    {
-        count = parity_chunk_count(h);
-        parity_dot_partials(h, da, db, nullptr, h->part0, nullptr, nullptr, h->stream);
-        parity_fold(h->part0, count, res, h->stream);
-    }
-    HIPTRY(h, hipGetLastError());
-    HIPTRY(h, hipMemcpyAsync(out, res, sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    if (partials)
-    {
-        const uint64_t total = h->reduction_partials;
-        const uint64_t ncopy = std::min<uint64_t>(count, total);
-        if (kind == CWF_PTR_DEVICE)
-        {
-            HIPTRY(h, hipMemcpyAsync(partials, h->part0, ncopy * sizeof(double), hipMemcpyDeviceToDevice,
-                                     h->stream));
-            if (total > ncopy)
-                HIPTRY(h, hipMemsetAsync(partials + ncopy, 0, (total - ncopy) * sizeof(double), h->stream));
-        }
-        else
-        {
-            HIPTRY(h, hipMemcpyAsync(partials, h->part0, ncopy * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-            HIPTRY(h, hipStreamSynchronize(h->stream));
-            for (uint64_t c = ncopy; c < total; ++c)
-                partials[c] = 0.0;
-        }
-    }
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_solve_pcg(cwf_hip_system *h, const float *rhs, const cwf_pcg_settings *settings, float *x_inout,
-                      float *residual_out, uint64_t n, int kind, cwf_pcg_telemetry *telemetry)
-{
-    if (int st = check_ready(h))
-        return st;
-    if (!rhs || !settings || !x_inout)
-        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
-    if (telemetry)
-        std::memset(telemetry, 0, sizeof *telemetry);
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "rhs span size mismatch",
-                         "rhs=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
-    if (settings->max_iterations == 0)
-        return set_error(h, CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
-    const float *drhs = nullptr;
-    if (int st = stage_vec(h, rhs, h->rhs, kind, 3, &drhs))
-        return st;
-    if (settings->warm_start)
-        if (int st = vec_in(h, x_inout, h->x, kind, 3))
-            return st;
-    int st = run_pcg(h, drhs, *settings, telemetry);
-    if (int e = vec_out(h, h->x, x_inout, kind, 3))
-        return e;
-    if (residual_out)
-        if (int e = vec_out(h, h->r, residual_out, kind, 3))
-            return e;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return st;
-}
-
-int cwf_hip_solve_pcg_group(cwf_hip_system *const *members, int32_t count, const float *const *rhs,
-                            const cwf_pcg_settings *settings, float *const *x_inout, float *const *residual_out,
-                            int kind, cwf_pcg_telemetry *telemetry)
-{
-    if (!members || count < 1 || !rhs || !settings || !x_inout)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
-    if (telemetry)
-        std::memset(telemetry, 0, sizeof *telemetry);
-    std::vector<cwf_hip_system *> g(members, members + count);
-    cwf_hip_comm *cm = g[0] ? g[0]->comm : nullptr;
-    for (int32_t i = 0; i < count; ++i)
-    {
-        if (int st = check_ready(g[i]))
-            return st;
-        if (!rhs[i] || !x_inout[i])
-            return set_error(g[i], CWF_ERR_ARGUMENT, "null pointer");
-        if (count > 1 && (!cm || cm->kind != 0 || g[i]->comm != cm || g[i]->rank != i || cm->nranks != count))
-            return set_error(g[i], CWF_ERR_ARGUMENT, "members must be every rank of one LOCAL communicator, in rank order",
-                             "member=" + std::to_string(i));
-    }
-    if (settings->max_iterations == 0)
-        return set_error(g[0], CWF_ERR_MAX_ITERATIONS, "max_iterations must be >= 1", "max_iterations=0");
-    std::vector<const float *> drhs(count);
-    for (int32_t i = 0; i < count; ++i)
-    {
-        cwf_hip_system *h = g[i];
-        if (int st = stage_in(h, rhs[i], h->rhs, h->ds.D, kind, &drhs[i]))
-            return st;
-        if (settings->warm_start)
-            HIPTRY(h, hipMemcpyAsync(h->x, x_inout[i], h->ds.D * sizeof(float),
-                                     kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                     h->stream));
-    }
-    int st = run_pcg_group(g, drhs, *settings, telemetry);
-    const hipMemcpyKind back = kind == CWF_PTR_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    for (int32_t i = 0; i < count; ++i)
-    {
-        cwf_hip_system *h = g[i];
-        HIPTRY(h, hipMemcpyAsync(x_inout[i], h->x, h->ds.D * sizeof(float), back, h->stream));
-        if (residual_out && residual_out[i])
-            HIPTRY(h, hipMemcpyAsync(residual_out[i], h->r, h->ds.D * sizeof(float), back, h->stream));
-        HIPTRY(h, hipStreamSynchronize(h->stream));
-    }
-    return st;
-}
-
-int cwf_hip_residual_history(cwf_hip_system *h, double *out, uint64_t capacity, uint64_t *count)
-{
-    if (int st = check_ready(h))
-        return st;
-    const uint64_t c = std::min(capacity, h->hist_count);
-    if (c && out)
-        HIPTRY(h, hipMemcpy(out, h->hist, c * sizeof(double), hipMemcpyDeviceToHost));
-    if (count)
-        *count = c;
-    return 0;
-}
-
-}  // extern "C"
-
-// ------------------------------------------------------------------------------------------
-// Stepper (newmark_stepper.cpp:1005-1379)
-// ------------------------------------------------------------------------------------------
-
-struct cwf_hip_stepper
-{
-    cwf_hip_system *sys = nullptr;
-    cwf_stepper_desc d{};
-    double dt = 1e-3, accumulated_time = 0.0, beta = 0.25, gamma = 0.5;
-    uint64_t frame_index = 0;
-    int warm_start = 1;
-    float *u = nullptr, *v = nullptr, *a = nullptr, *up = nullptr, *vp = nullptr, *f = nullptr, *bcv = nullptr,
-          *damp = nullptr, *kd = nullptr, *srhs = nullptr;
-    double *lbase = nullptr, *lpat = nullptr;  // cwf_hip_stepper_set_load_pattern: f64 [3N] each (internal order)
-    std::vector<void *> owned;
-};
-
-namespace
-{
-int st_alloc(cwf_hip_stepper *t, float **p, uint64_t n)
-{
-    void *q = nullptr;
-    if (hipMalloc(&q, std::max<uint64_t>(n, 4) * sizeof(float)) != hipSuccess)
-        return set_error(t->sys, CWF_ERR_ALLOC, "failed to allocate stepper buffers");
-    t->owned.push_back(q);
-    *p = static_cast<float *>(q);
-    return 0;
-}
-}  // namespace
-
-extern "C" {
-
-void cwf_hip_stepper_destroy(cwf_hip_stepper *t)
-{
-    if (!t)
-        return;
-    (void)hipSetDevice(t->sys->device);
-    (void)hipStreamSynchronize(t->sys->stream);
-    for (void *p : t->owned)
-        (void)hipFree(p);
-    delete t;
-}
-
-int cwf_hip_stepper_create(cwf_hip_system *h, const cwf_stepper_desc *desc, cwf_hip_stepper **out)
-{
-    if (int st = check_ready(h))
-        return st;
-    if (!desc || !out)
-        return set_error(h, CWF_ERR_ARGUMENT, "null pointer");
-    *out = nullptr;
-    auto *t = new (std::nothrow) cwf_hip_stepper();
-    if (!t)
-        return set_error(h, CWF_ERR_ALLOC, "host allocation failed");
-    t->sys = h;
-    t->d = *desc;
-    t->d.external_force = nullptr;
-    t->d.bc_value = nullptr;
-    t->dt = desc->initial_dt > 0.0 ? desc->initial_dt : 1.0e-3;  // :1020
-    t->warm_start = desc->warm_start;
-    const uint64_t D = h->ds.D;
-    for (float **p : {&t->u, &t->v, &t->a, &t->up, &t->vp, &t->f, &t->bcv, &t->damp, &t->kd, &t->srhs})
-        if (int st = st_alloc(t, p, D))
-        {
-            cwf_hip_stepper_destroy(t);
-            return st;
-        }
-    hipStream_t s = h->stream;
-    for (float *p : {t->u, t->v, t->a, t->up, t->vp, t->f, t->bcv})
-        (void)hipMemsetAsync(p, 0, D * sizeof(float), s);
-    if (desc->external_force)
-        (void)vec_in(h, desc->external_force, t->f, CWF_PTR_HOST, 3);
-    if (desc->bc_value)
-        (void)vec_in(h, desc->bc_value, t->bcv, CWF_PTR_HOST, 3);
-    (void)hipMemsetAsync(h->x, 0, D * sizeof(float), s);  // solver.x starts at 0 (pack.cpp:214)
-    hipError_t e = hipStreamSynchronize(s);
-    if (e != hipSuccess)
-    {
-        cwf_hip_stepper_destroy(t);
-        return hip_fail(h, e, "stepper create");
-    }
-    *out = t;
-    return 0;
-}
-
-int cwf_hip_stepper_step(cwf_hip_stepper *t, double sim_time, int paused, cwf_step_telemetry *tel)
-{
-    if (!t)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
-    cwf_hip_system *h = t->sys;
-    if (int st = check_ready(h))
-        return st;
-    hipStream_t s = h->stream;
-    const uint32_t N = h->ds.N, D = h->ds.D;
-    t->accumulated_time = sim_time;
-    // refresh_coefficients + update_matrix_free_scalars (:1316-1326)
-    const double b = t->beta, g = t->gamma, dt = t->dt;
-    double c6[6];
-    c6[0] = 1.0 / (b * dt * dt);
-    c6[1] = g / (b * dt);
-    c6[2] = 1.0 / (b * dt);
-    c6[3] = (1.0 / (2.0 * b)) - 1.0;
-    c6[4] = (g / b) - 1.0;
-    c6[5] = dt * ((g / (2.0 * b)) - 1.0);
-    const double inv_beta_dt2 = 1.0 / (b * dt * dt);
-    const double gamma_over_beta_dt = g / (b * dt);
-    const cwf::DevSys saved = h->ds;
-    h->ds.sK = 1.0 + c6[1] * t->d.rayleigh_beta;
-    h->ds.sM = c6[0] + c6[1] * t->d.rayleigh_alpha;
-    stepper_predictor(D, t->u, t->v, t->a, t->up, t->vp, dt, b, g, s);
-    stepper_assemble_rhs(N, h->ds.mass, t->u, t->v, t->a, t->f, t->srhs, t->damp, c6, t->d.rayleigh_alpha, s);
-    if (std::fabs(t->d.rayleigh_beta) > DBL_EPSILON)
-    {
-        cwf::DevSys stiff = h->ds;  // stiffness_only_system_ (:1051-1053)
-        stiff.sK = 1.0;
-        stiff.sM = 0.0;
-        if (h->mode == CWF_MODE_FAST)
-            fast_keff_ds(stiff, t->damp, t->kd, true, nullptr, nullptr, s);
-        else
-            parity_keff_ds(stiff, t->damp, t->kd, true, nullptr, s);
-        stepper_rhs_damping(D, t->srhs, t->kd, (float)t->d.rayleigh_beta, s);
-    }
-    stepper_clamp(N, h->ds.mask, t->bcv, t->u, t->srhs, s);
-    const double tol = paused ? t->d.pause_tolerance : t->d.runtime_tolerance;
-    cwf_pcg_settings ps{t->d.max_iterations, tol, t->warm_start, 0};
-    cwf_pcg_telemetry pt{};
-    int st = run_pcg(h, t->srhs, ps, &pt);
-    h->ds.sK = saved.sK;
-    h->ds.sM = saved.sM;
-    if (st)
-    {
-        std::string inner = h->err;
-        return set_error(h, st, "pcg solve failed", inner);  // :1130-1133
-    }
-    stepper_update(D, h->x, t->up, t->vp, t->u, t->v, t->a, (float)inv_beta_dt2, (float)gamma_over_beta_dt, s);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess)
-        e = hipStreamSynchronize(s);
-    if (e != hipSuccess)
-        return hip_fail(h, e, "stepper update");
-    cwf_step_telemetry T{};
-    T.simulation_time = sim_time;
-    T.time_step = t->dt;
-    T.applied_tolerance = tol;
-    T.paused_mode = paused ? 1 : 0;
-    T.pcg = pt;
-    // adapt_timestep (:1328-1367)
-    if (t->d.adaptive)
-    {
-        const double low = t->d.low_iteration_ratio * (double)t->d.max_iterations;
-        if ((double)pt.iterations <= low)
-        {
-            t->dt *= t->d.increase_factor;
-            T.dt_increased = 1;
-        }
-        else if (!pt.converged)
-        {
-            t->dt *= t->d.decrease_factor;
-            T.dt_decreased = 1;
-        }
-        if (t->d.min_dt > 0.0 && t->dt <= t->d.min_dt)
-        {
-            t->dt = t->d.min_dt;
-            T.dt_clamped_min = 1;
-        }
-        if (t->d.max_dt > 0.0 && t->dt >= t->d.max_dt)
-        {
-            t->dt = t->d.max_dt;
-            T.dt_clamped_max = 1;
-        }
-    }
-    ++t->frame_index;
-    t->accumulated_time = sim_time + t->dt;
-    if (tel)
-        *tel = T;
-    return 0;
-}
-
-int cwf_hip_stepper_get_state(cwf_hip_stepper *t, int which, float *out, uint64_t n, int kind)
-{
-    if (!t || !out)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
-    cwf_hip_system *h = t->sys;
-    if (int st = check_ready(h))
-        return st;
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "state span size mismatch");
-    const float *src = which == 0   ? t->u
-                       : which == 1 ? t->v
-                       : which == 2 ? t->a
-                       : which == 3 ? h->x
-                       : which == 4 ? t->f  // nodes.external_force (after set_load_scale / set_external_force)
-                                    : nullptr;
-    if (!src)
-        return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
-    if (int st = vec_out(h, src, out, kind, 3))
-        return st;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_stepper_set_state(cwf_hip_stepper *t, int which, const float *in, uint64_t n, int kind)
-{
-    if (!t || !in)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
-    cwf_hip_system *h = t->sys;
-    if (int st = check_ready(h))
-        return st;
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "state span size mismatch");
-    float *dst = which == 0 ? t->u : which == 1 ? t->v : which == 2 ? t->a : which == 3 ? h->x : nullptr;
-    if (!dst)
-        return set_error(h, CWF_ERR_ARGUMENT, "unknown state field");
-    if (int st = vec_in(h, in, dst, kind, 3))
-        return st;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_stepper_set_external_force(cwf_hip_stepper *t, const float *f, uint64_t n, int kind)
-{
-    if (!t || !f)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
-    cwf_hip_system *h = t->sys;
-    if (int st = check_ready(h))
-        return st;
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "external force span size mismatch");
-    if (int st = vec_in(h, f, t->f, kind, 3))
-        return st;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_stepper_set_load_pattern(cwf_hip_stepper *t, const double *base, const double *pattern, uint64_t n)
-{
-    if (!t || !base || !pattern)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
-    cwf_hip_system *h = t->sys;
-    if (int st = check_ready(h))
-        return st;
-    if (n != h->ds.D)
-        return set_error(h, CWF_ERR_SIZE, "load pattern span size mismatch",
-                         "input=" + std::to_string(n) + "\ndofs=" + std::to_string(h->ds.D));
-    if (!t->lbase)
-    {
-        void *q = nullptr;
-        if (hipMalloc(&q, std::max<uint64_t>(2 * n, 2) * sizeof(double)) != hipSuccess)
-            return set_error(h, CWF_ERR_ALLOC, "failed to allocate stepper buffers");
-        t->owned.push_back(q);
-        t->lbase = static_cast<double *>(q);
-        t->lpat = t->lbase + n;
-    }
-    // a node's 3 f64 = 6 floats: the node-order conversion moves them as 6-float records
-    if (int st = vec_in(h, reinterpret_cast<const float *>(base), reinterpret_cast<float *>(t->lbase), CWF_PTR_HOST, 6))
-        return st;
-    if (int st = vec_in(h, reinterpret_cast<const float *>(pattern), reinterpret_cast<float *>(t->lpat), CWF_PTR_HOST,
-                        6))
-        return st;
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    return 0;
-}
-
-int cwf_hip_stepper_set_load_scale(cwf_hip_stepper *t, double scale)
-{
-    if (!t)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
-    cwf_hip_system *h = t->sys;
-    if (int st = check_ready(h))
-        return st;
-    if (!t->lbase)
-        return set_error(h, CWF_ERR_ARGUMENT, "no load pattern set", "cwf_hip_stepper_set_load_pattern");
-    stepper_scaled_load(h->ds.D, t->lbase, t->lpat, scale, t->f, h->stream);  // ordered before the next step
-    HIPTRY(h, hipGetLastError());
-    return 0;
-}
-
-int cwf_hip_stepper_set_warm_start(cwf_hip_stepper *t, int enabled)
-{
-    if (!t)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
-    t->warm_start = enabled ? 1 : 0;
-    return 0;
-}
-
-int cwf_hip_stepper_time(const cwf_hip_stepper *t, double *current_time, double *time_step)
-{
-    if (!t)
-        return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
-    if (current_time)
-        *current_time = t->accumulated_time;
-    if (time_step)
-        *time_step = t->dt;
     return 0;
 }
 
