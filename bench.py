@@ -501,15 +501,20 @@ def main():
             # the same workload on the general operator (fan-group tiles), timed after the headline's region
             "general": general,
         }
-        if args.mode == "parity":
-            # the events bracket both PARITY K_eff passes: the element pass and the node fold that also forms
-            # the p . Ap chunk partials (rocprof lists them as two kernels; their averages add up to this)
-            result["roofline"]["kernels_bracketed"] = [kname, "k_keff_parity_fold<false, true>"]
         if args.mode == "parity" and keff_n.value:
-            # the element pass computes each tet's fp64 element math once: strain 72, stress 24 (isotropic D),
-            # V s_K 1, 4 corner forces x (18 + 3 scale) = 84, and the node fold adds 3 per incidence (12 per tet):
-            # 193 fp64 flops per tet (kernels_parity.hip). The fp64 vector peak is AMD's MI355X spec (78.6 TFLOP/s,
-            # not in the microarch guide); avg_launch_ms brackets the element pass and the node fold.
+            # PARITY's roofline is priced against the REFERENCE layout's compulsory bytes (72 B per tet + 32 B per
+            # node): the node-tile kernel's own compulsory bytes (the 64-B record, volume and incidence
+            # tiles per tet, x, y, mass, mask and CSR offsets per node) are reported beside it
+            result["roofline"]["layout_bytes_per_launch"] = alg_bytes
+            result["roofline"]["layout_frac"] = result["roofline"]["frac"]
+            result["roofline"]["achieved"] = ref_equiv
+            result["roofline"]["frac"] = ref_equiv / HBM_PEAK_GBS
+            result["roofline"]["algorithmic_bytes_per_launch"] = ref_bytes
+            result["roofline"]["bytes_basis"] = "reference layout (72 B/tet + 32 B/node)"
+            # each tet's fp64 element math once: strain 72, stress 24 (isotropic D), V s_K 1, 4 corner forces x
+            # (18 + 3 scale) = 84, and the node fold adds 3 per incidence (12 per tet): 193 fp64 flops per tet
+            # (kernels_parity.hip; halo tets are computed again by the neighbouring tile, not counted). The fp64
+            # vector peak is AMD's MI355X spec (78.6 TFLOP/s, not in the microarch guide).
             flops = 193.0 * local_tets
             result["roofline_fp64"] = {"bound": "valu_fp64", "achieved": flops / (avg_keff_ms * 1e-3) / 1e12,
                                        "peak": 78.6, "unit": "TFLOP/s",

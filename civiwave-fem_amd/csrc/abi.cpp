@@ -72,23 +72,22 @@ bool iso_pattern(const double *D)
     return true;
 }
 
-// the per-incidence fp64 force planes of the element-centric PARITY K_eff (3 x fslots doubles, ~96 B per tet),
-// allocated once a handle runs PARITY
 // Built on first use (a PARITY create or set_mode(PARITY)), from the node -> incidence CSR already on the device:
-// node n's k-th incidence (ascending element) goes to slot fblk[n / 64] + 64 k + n % 64 of the force planes, so a
-// wave of 64 consecutive nodes folds slot k of all its nodes with one coalesced load; ipos maps every (tet, corner)
-// to its slot. FAST handles never build it (16 B per tet, and its 2^32-slot limit is a PARITY limit only).
+// the node tiles of k_keff_parity_tile. Tile b holds nodes [256 b, 256 b + 256) (three whole 256-DOF reduction
+// chunks, so the p.Ap chunk partials stay fused), its incident tets in ascending element order, and for each of its
+// nodes' incidences the tet's index in that list. FAST handles never build it.
 int parity_incidence_slots(cwf_hip_system *h)
 {
     DevSys &s = h->ds;
-    const uint64_t N = s.N, E = s.E, nb = (N + 63) / 64;
-    std::vector<uint32_t> off, inc, ipos, fblk;
+    const uint64_t N = s.N, E = s.E, nt = (N + 255) / 256;
+    std::vector<uint32_t> off, inc, toff, tets, pinc;
     try
     {
         off.resize(N + 1);
         inc.resize(4 * E);
-        ipos.assign(4 * E, 0xFFFFFFFFu);
-        fblk.resize(nb + 1);
+        pinc.resize(4 * E);
+        toff.resize(nt + 1);
+        tets.reserve(3 * E);
     }
     catch (const std::bad_alloc &)
     {
@@ -96,45 +95,50 @@ int parity_incidence_slots(cwf_hip_system *h)
     }
     HIPTRY(h, hipMemcpy(off.data(), s.off, (N + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
     HIPTRY(h, hipMemcpy(inc.data(), s.inc, 4 * E * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    uint64_t slots = 0;
-    for (uint64_t b = 0; b < nb; ++b)
+    std::vector<uint32_t> loc;
+    for (uint64_t b = 0; b < nt; ++b)
     {
-        fblk[b] = (uint32_t)slots;
-        uint32_t kmax = 0;
-        for (uint64_t n = 64 * b; n < std::min<uint64_t>(N, 64 * b + 64); ++n)
-            kmax = std::max(kmax, off[n + 1] - off[n]);
-        slots += 64ull * kmax;
+        const uint64_t n0 = 256 * b, n1 = std::min<uint64_t>(N, n0 + 256);
+        toff[b] = (uint32_t)tets.size();
+        loc.clear();
+        for (uint32_t j = off[n0]; j < off[n1]; ++j)
+            loc.push_back(inc[j] >> 2);
+        std::sort(loc.begin(), loc.end());
+        loc.erase(std::unique(loc.begin(), loc.end()), loc.end());
+        for (uint32_t j = off[n0]; j < off[n1]; ++j)
+            pinc[j] = (uint32_t)(std::lower_bound(loc.begin(), loc.end(), inc[j] >> 2) - loc.begin()) << 2 |
+                      (inc[j] & 3u);
+        try
+        {
+            tets.insert(tets.end(), loc.begin(), loc.end());
+        }
+        catch (const std::bad_alloc &)
+        {
+            return set_error(h, CWF_ERR_ALLOC, "host allocation failed");
+        }
+        if (tets.size() >= (1ull << 32))
+            return set_error(h, CWF_ERR_UNSUPPORTED, "mesh too large for one PARITY handle (shard it)",
+                             "tile_tets=" + std::to_string(tets.size()));
     }
-    if (slots >= (1ull << 32))
-        return set_error(h, CWF_ERR_UNSUPPORTED, "mesh too large for one PARITY handle (shard it)",
-                         "force_slots=" + std::to_string(slots));
-    fblk[nb] = (uint32_t)slots;
-    for (uint64_t n = 0; n < N; ++n)
-        for (uint32_t j = off[n]; j < off[n + 1]; ++j)
-            ipos[inc[j]] = fblk[n / 64] + 64u * (j - off[n]) + (uint32_t)(n % 64);  // inc = element << 2 | corner
-    uint32_t *dp, *db;
-    if (int st = upload(h, &dp, ipos.data(), 4 * E))
+    toff[nt] = (uint32_t)tets.size();
+    uint32_t *dto, *dte, *dpi;
+    if (int st = upload(h, &dto, toff.data(), nt + 1))
         return st;
-    if (int st = upload(h, &db, fblk.data(), nb + 1))
+    if (int st = upload(h, &dte, tets.data(), tets.size()))
         return st;
-    s.ipos = dp;
-    s.fblk = db;
-    s.fslots = slots;
+    if (int st = upload(h, &dpi, pinc.data(), 4 * E))
+        return st;
+    s.ptile_off = dto;
+    s.ptile_tets = dte;
+    s.pinc = dpi;
     return 0;
 }
 
 int parity_force_buffer(cwf_hip_system *h)
 {
-    if (h->ds.pforce || h->ds.hex || !h->ds.E)
+    if (h->ds.ptile_off || h->ds.hex || !h->ds.E)
         return 0;
-    if (!h->ds.ipos)
-        if (int st = parity_incidence_slots(h))
-            return st;
-    double *f = nullptr;
-    if (int st = dalloc(h, &f, 3ull * h->ds.fslots))
-        return st;
-    h->ds.pforce = f;
-    return 0;
+    return parity_incidence_slots(h);
 }
 
 int check_ready(cwf_hip_system *h)
@@ -1291,9 +1295,9 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         *layout_bytes = 16ull * s.t.ntiles + E * (rec + (s.t.mat ? 4 : 0)) +
                         T * (8 + (s.t.geo ? 12 : 0) + (s.t.node_major ? 4 : 0) + 12) + N * (24 + 4 + 12);
     }
-    else  // PARITY element pass + node fold: per tet the 64-B record, vol, 4 incidence positions, the 4 fp64
-          // corner forces written and read back (2 x 96 B); per node CSR offset, x in, y out, mass, mask
-        *layout_bytes = E * (64 + 4 + 16 + 2 * 96 + (s.M > 1 ? 4 : 0)) + N * (4 + 12 + 12 + 4 + 4);
+    else  // PARITY node tiles (k_keff_parity_tile), compulsory: per tet the 64-B record, vol, its 4 incidence
+          // entries (pinc) and its tile-list entry (+ material); per node CSR offset, x in, y out, mass, mask
+        *layout_bytes = E * (64 + 4 + 16 + 4 + (s.M > 1 ? 4 : 0)) + N * (4 + 12 + 12 + 4 + 4);
     return 0;
 }
 
@@ -1303,7 +1307,7 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
         return nullptr;
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
-        return h->ds.iso ? "k_keff_parity_elem<true, false>" : "k_keff_parity_elem<false, false>";
+        return h->ds.iso ? "k_keff_parity_tile<true, false, true>" : "k_keff_parity_tile<false, false, true>";
     if (fast_cg_enabled(h))  // the launches without the lazy x update (three in four)
     {
         static thread_local char name[96];

@@ -241,13 +241,12 @@ struct DevSys
     const uint32_t *mask = nullptr;
     const uint32_t *off = nullptr;
     const uint32_t *inc = nullptr;
-    // element-centric PARITY K_eff (kernels_parity.hip): the force of node n's k-th incidence (ascending element)
-    // lives in slot fblk[n / 64] + 64 k + n % 64 of three fp64 planes pforce[c * fslots + slot] (allocated with
-    // PARITY mode); ipos[4e + a] = the slot of incidence (e, a)
-    const uint32_t *ipos = nullptr;
-    const uint32_t *fblk = nullptr;  // [ceil(N / 64) + 1]
-    uint64_t fslots = 0;
-    double *pforce = nullptr;
+    // node-tile PARITY K_eff (kernels_parity.hip k_keff_parity_tile; built at the first PARITY use): tile b = nodes
+    // [256 b, 256 b + 256); ptile_tets[ptile_off[b] ..] its incident tets, ascending; pinc[j] = (the tile-local index
+    // of incidence j's tet) << 2 | corner, for every incidence j of the node -> incidence CSR (off / inc order)
+    const uint32_t *ptile_off = nullptr;
+    const uint32_t *ptile_tets = nullptr;
+    const uint32_t *pinc = nullptr;
     double sK = 1.0;  // stiffness_scale
     double sM = 0.0;  // mass_factor
     int iso = 0;      // every material has the isotropic Voigt zero pattern

@@ -192,42 +192,6 @@ __device__ __forceinline__ void stage_dtab(const DevSys &s, double *dtab)
     }
 }
 
-// K_eff x (pcg.cpp:505-694), element-centric: one thread per tet computes its strain and stress once and its 4
-// corner forces, each the exact fp64 term the reference's scatter adds (pcg.cpp:643-661), and stores it at the
-// incidence's position in the node-major CSR (ipos). The node pass then folds each node's contiguous run in
-// ascending element order from +0.0: the reference's additions in the reference's order, so y is bit-identical.
-// Round 2's node-centric gather (one thread per node recomputing every incident tet, 4x the fp64 element work
-// and 4 reads of every tet record) took 293 us on C2 against 76 + 85 us for this pair (r03c / r03f profiles).
-template <bool ISO, bool SANITIZE>
-__global__ __launch_bounds__(kBlock) void k_keff_parity_elem(DevSys s, const float *__restrict__ x,
-                                                             const Ctl *__restrict__ ctl)
-{
-    __shared__ double dtab[kMaxLdsMaterials * 36];
-    if (ctl && !ctl->active)
-        return;
-    stage_dtab<ISO>(s, dtab);
-    __syncthreads();
-    const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
-    if (e >= s.E)
-        return;
-    Grad G;
-    load_erec(s.erec, e, G);
-    double gx[4], gy[4], gz[4], sig[6];
-    tet_stress<ISO, SANITIZE>(s, G, x, dtab, s.mat[e], gx, gy, gz, sig);
-    const double vol = (double)s.vol[e] * s.sK;  // pcg.cpp:642
-    const uint4 pos = reinterpret_cast<const uint4 *>(s.ipos)[e];
-    const uint32_t j[4] = {pos.x, pos.y, pos.z, pos.w};
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-    {
-        double f[3];
-        corner_force(gx[a], gy[a], gz[a], sig, vol, f);
-        s.pforce[j[a]] = f[0];
-        s.pforce[s.fslots + j[a]] = f[1];
-        s.pforce[2 * s.fslots + j[a]] = f[2];
-    }
-}
-
 // A 256-thread workgroup of consecutive nodes covers 768 DOFs = three whole 256-DOF reduction chunks (workgroup b:
 // chunks 3b .. 3b + 2), so the node kernels that produce a dot's operands also produce its chunk partials. Every
 // thread stages the fp64 products of its own DOFs in LDS (chunk k at row 257 k, against bank conflicts); a
@@ -246,11 +210,12 @@ __device__ __forceinline__ uint32_t chunk_slot(uint32_t d)  // LDS index of the 
 }
 
 template <int NV>
-__device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint32_t chunks, double *pab, double *pac)
+__device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint32_t chunks, double *pab, double *pac,
+                                                  uint32_t blk)
 {
     if (threadIdx.x >= 3u)
         return;
-    const uint32_t k = 3u * blockIdx.x + threadIdx.x;
+    const uint32_t k = 3u * blk + threadIdx.x;
     if (k >= chunks)
         return;
     const ChunkTerm<NV> *row = st + threadIdx.x * kChunkRow;
@@ -272,31 +237,83 @@ __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint3
         pac[k] = s1;
 }
 
-// node pass of the element-centric K_eff: the ascending-element fold of the node's incidence forces, then the
-// mass term, Dirichlet identity rows and the cast (pcg.cpp:653-691). DOT (the PCG loop): also the chunk partials of
-// x . y, the p . Ap of pcg.cpp:840 (wg_chunk_partials), so no separate dot pass reads p and Ap again.
-template <bool SANITIZE, bool DOT>
-__global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const float *__restrict__ x,
+// K_eff x (pcg.cpp:505-694) over node tiles: workgroup b owns nodes [256 b, 256 b + 256) (thread t node 256 b + t)
+// and walks the tile's incident tets in ascending element order, 256 at a time. In each batch thread t computes one
+// tet's strain and stress in fp64 (the reference's operand order) and the corner forces of its corners inside the
+// tile, each the exact fp64 term pcg.cpp:643-661 adds, into LDS; then every node thread adds its incidences that
+// fall in the batch, in ascending element order, to its fp64 accumulators (started at +0.0). Batches run in
+// element order, so each node's sum is the reference's left fold over its incident elements: y is bit-identical.
+// Then the mass term, the Dirichlet identity rows and the cast (pcg.cpp:664-691); DOT (the PCG loop): the chunk
+// partials of x . y (the p . Ap of pcg.cpp:840), three whole 256-DOF chunks per workgroup (wg_chunk_partials).
+// Halo tets (those with corners in two tiles) are computed once per tile that needs them (~2.4 tets per tet on a
+// Kuhn block); nothing but y leaves the workgroup. Round 3 stored every corner force to HBM (96 B per tet written
+// and read back by a node pass: 76 + 36 us on C2); round 2 gathered every incident tet per node (4x the element
+// work, 293 us).
+constexpr int kTileTets = 256;
+template <bool ISO, bool SANITIZE, bool DOT>
+__global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
                                                              float *__restrict__ y, const Ctl *__restrict__ ctl,
                                                              double *__restrict__ pdot, uint32_t nlim,
                                                              uint32_t chunks)
 {
+    __shared__ double dtab[kMaxLdsMaterials * 36];
+    __shared__ double fs[3][4 * kTileTets];  // [component][batch tet * 4 + corner]
     __shared__ double sxy[DOT ? 3 * kChunkRow : 1];
     if (ctl && !ctl->active)
         return;
-    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    stage_dtab<ISO>(s, dtab);
+    // XCD-aware tile order: consecutive tiles (which share halo tets) on one XCD
+    const uint32_t ntile = gridDim.x, xcd = blockIdx.x & 7u, per = ntile >> 3, rem = ntile & 7u;
+    const uint32_t tile = xcd * per + min(xcd, rem) + (blockIdx.x >> 3);
+    const uint32_t n0 = tile * kBlock, n = n0 + threadIdx.x;
+    const uint32_t t0 = s.ptile_off[tile], nt = s.ptile_off[tile + 1] - t0;
+    uint32_t j = 0, jend = 0;
+    if (n < s.N)
+    {
+        j = s.off[n];
+        jend = s.off[n + 1];
+    }
+    uint32_t q = j < jend ? s.pinc[j] : 0xFFFFFFFFu;  // the node's next incidence: tile-local tet << 2 | corner
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+    __syncthreads();  // dtab
+    for (uint32_t base = 0; base < nt; base += kTileTets)
+    {
+        if (base + threadIdx.x < nt)
+        {
+            const uint32_t e = s.ptile_tets[t0 + base + threadIdx.x];
+            Grad G;
+            load_erec(s.erec, e, G);
+            double gx[4], gy[4], gz[4], sig[6];
+            tet_stress<ISO, SANITIZE>(s, G, x, dtab, s.mat[e], gx, gy, gz, sig);
+            const double vol = (double)s.vol[e] * s.sK;  // pcg.cpp:642
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                if (G.c[a] - n0 < (uint32_t)kBlock)  // a corner of this tile
+                {
+                    double f[3];
+                    corner_force(gx[a], gy[a], gz[a], sig, vol, f);
+                    const uint32_t sl = 4u * threadIdx.x + (uint32_t)a;
+                    fs[0][sl] = f[0];
+                    fs[1][sl] = f[1];
+                    fs[2][sl] = f[2];
+                }
+        }
+        __syncthreads();
+        const uint32_t lim = (base + kTileTets) << 2;
+        while (q < lim)  // incidences are ascending in element order, so in tile-local tet order
+        {
+            const uint32_t sl = q - (base << 2);
+            acc0 += fs[0][sl];
+            acc1 += fs[1][sl];
+            acc2 += fs[2][sl];
+            ++j;
+            q = j < jend ? s.pinc[j] : 0xFFFFFFFFu;
+        }
+        __syncthreads();
+    }
     float yv[3] = {0.f, 0.f, 0.f}, xv[3] = {0.f, 0.f, 0.f};
     if (n < s.N)
     {
-        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-        const double *f = s.pforce + s.fblk[n / 64u] + (n % 64u);
-        const uint32_t cnt = s.off[n + 1] - s.off[n];
-        for (uint32_t k = 0; k < cnt; ++k)  // slot k of the node's wave block: one coalesced load per plane
-        {
-            acc0 += f[64ull * k];
-            acc1 += f[s.fslots + 64ull * k];
-            acc2 += f[2 * s.fslots + 64ull * k];
-        }
         const uint32_t mk = s.mask[n];
         const double m = (double)s.mass[n] * s.sM;
         const float x0 = x[3u * n + 0], x1 = x[3u * n + 1], x2 = x[3u * n + 2];
@@ -324,12 +341,13 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_fold(DevSys s, const flo
     }
     if constexpr (DOT)
     {
+        // the tile's chunks are 3 tile, 3 tile + 1, 3 tile + 2 (wg_chunk_partials reads blockIdx.x: pass the tile)
         const bool own = n < nlim;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
             sxy[chunk_slot(3u * threadIdx.x + k)] = own ? (double)xv[k] * (double)yv[k] : 0.0;
         __syncthreads();
-        wg_chunk_partials<1>(sxy, chunks, pdot, nullptr);
+        wg_chunk_partials<1>(sxy, chunks, pdot, nullptr, tile);
     }
 }
 
@@ -952,7 +970,7 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
         srz[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
     }
     __syncthreads();
-    wg_chunk_partials<2>(srz, chunks, prr, prz);
+    wg_chunk_partials<2>(srz, chunks, prr, prz, blockIdx.x);
 }
 
 // p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
@@ -985,24 +1003,24 @@ uint32_t parity_chunk_count(const cwf_hip_system *h)
     return (uint32_t)((h->ds.D + B - 1) / B);
 }
 
-// element-centric K_eff: the 4 corner forces of every tet once, then the ordered node fold (the handle holds the
-// incidence positions and the force buffer whenever it runs PARITY: abi.cpp parity_force_buffer)
+// the node-tile K_eff (the handle builds its tiles whenever it runs PARITY: abi.cpp parity_force_buffer)
+template <bool SAN, bool DOT>
+void launch_parity_tile(const DevSys &s, const float *x, float *y, const Ctl *ctl, double *pdot, uint32_t nlim,
+                        uint32_t chunks, hipStream_t st)
+{
+    const dim3 gn(grid_for(s.N, kBlock)), b(kBlock);
+    if (s.iso)
+        k_keff_parity_tile<true, SAN, DOT><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
+    else
+        k_keff_parity_tile<false, SAN, DOT><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
+}
+
 void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
 {
     if (s.N == 0)
         return;
-    const dim3 ge(grid_for(s.E, kBlock)), gn(grid_for(s.N, kBlock)), b(kBlock);
-    if (s.E)
-    {
-        if (s.iso)
-            sanitize ? k_keff_parity_elem<true, true><<<ge, b, 0, st>>>(s, x, ctl)
-                     : k_keff_parity_elem<true, false><<<ge, b, 0, st>>>(s, x, ctl);
-        else
-            sanitize ? k_keff_parity_elem<false, true><<<ge, b, 0, st>>>(s, x, ctl)
-                     : k_keff_parity_elem<false, false><<<ge, b, 0, st>>>(s, x, ctl);
-    }
-    sanitize ? k_keff_parity_fold<true, false><<<gn, b, 0, st>>>(s, x, y, ctl, nullptr, 0u, 0u)
-             : k_keff_parity_fold<false, false><<<gn, b, 0, st>>>(s, x, y, ctl, nullptr, 0u, 0u);
+    sanitize ? launch_parity_tile<true, false>(s, x, y, ctl, nullptr, 0u, 0u, st)
+             : launch_parity_tile<false, false>(s, x, y, ctl, nullptr, 0u, 0u, st);
 }
 
 // the PCG loop's K_eff p with the chunk partials of p . Ap over nodes [0, Nown) into pdot: fused into the node fold
@@ -1018,15 +1036,7 @@ void parity_keff_dot(const cwf_hip_system *h, const float *p, float *Ap, const C
     }
     if (s.N == 0)
         return;
-    const dim3 ge(grid_for(s.E, kBlock)), gn(grid_for(s.N, kBlock)), b(kBlock);
-    if (s.E)
-    {
-        if (s.iso)
-            k_keff_parity_elem<true, false><<<ge, b, 0, st>>>(s, p, ctl);
-        else
-            k_keff_parity_elem<false, false><<<ge, b, 0, st>>>(s, p, ctl);
-    }
-    k_keff_parity_fold<false, true><<<gn, b, 0, st>>>(s, p, Ap, ctl, pdot, s.Nown, grid_for(3u * s.Nown, 256u));
+    launch_parity_tile<false, true>(s, p, Ap, ctl, pdot, s.Nown, grid_for(3u * s.Nown, 256u), st);
 }
 
 void parity_keff(const cwf_hip_system *h, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
