@@ -1071,20 +1071,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         return bail(st);
     if (int st = dalloc(h, &h->inv6, 4 * N))
         return bail(st);
-    // the single-launch PCG of a structured block with the class preconditioner (spmv_tiles.hip: fast_cg_*)
-    const char *lcg = knob("CWF_LAT_CG");
-    if (h->mode == CWF_MODE_FAST && s.t.lat && s.t.lcls && s.t.lmu && !(lcg && lcg[0] == '0'))
-    {
-        for (float **v : {&h->cg_r2, &h->cg_w2, &h->cg_s0, &h->cg_s1})
-            if (int st = dalloc(h, v, D))
-                return bail(st);
-    }
     const uint64_t chunks = (D + d->reduction_block - 1) / d->reduction_block;
-    // the PARITY chunk partials, the FAST dot partials, and 4 doubles per workgroup of the FAST PCG kernels'
-    // shares (fold_publish: K_eff and single-launch grids in part0, the update pass's in part1)
     h->part_cap = std::max<uint64_t>(
-        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), 4ull * s.t.ntiles,
-         4ull * s.t.pipe_grid, 4ull * 2048, 1});
+        {chunks, (uint64_t)fast_block_count(h), (uint64_t)fast_dot_blocks(s.D), (uint64_t)s.t.ntiles,
+         (uint64_t)s.t.pipe_grid, 1});
     if (int st = dalloc(h, &h->part0, h->part_cap))
         return bail(st);
     if (int st = dalloc(h, &h->part1, h->part_cap))
@@ -1093,11 +1083,6 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         return bail(st);
     if (int st = dalloc(h, &h->ctl, 1))
         return bail(st);
-    if (int st = dalloc(h, &h->gsum, 4 * 32 * 4))
-        return bail(st);
-    if (int st = dalloc(h, &h->gcnt, 2 * 32 * 16))
-        return bail(st);
-    HIPTRY(h, hipMemset(h->gcnt, 0, 2 * 32 * 16 * sizeof(unsigned)));
     if (int st = dalloc(h, &h->scal, 8))
         return bail(st);
     // folded per-rank scalars (one rank until cwf_hip_system_attach): p.Ap, {r.r, r.z}, {rhs.rhs, r0.r0}, r0.z0
@@ -1274,12 +1259,6 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
-        if (fast_cg_enabled(h))  // the single-launch iteration: per owned node r, w, s, p_old read + the class
-        {                        // byte, p, s, r, w written; the shell's mass; the lazy x (x and three older
-                                 // directions read, x written) every x_lag-th launch, amortised over four
-            *layout_bytes = (uint64_t)s.Nown * (48 + 1 + 48) + 4ull * s.t.lnshell + (uint64_t)s.Nown * (12 + 36 + 12) / 4;
-            return 0;
-        }
         if (s.t.lat)  // per owned node: z and p_old read, the new p and the row value written; the mass read
         {             // (only the shell's when the strict interior's is one value, lmu)
             *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 12 + 12 + (s.t.lmu && s.t.lzr ? 1 : 0)) +
@@ -1308,13 +1287,6 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
         return h->ds.iso ? "k_keff_parity_tile<true, false, true>" : "k_keff_parity_tile<false, false, true>";
-    if (fast_cg_enabled(h))  // the launches without the lazy x update (three in four)
-    {
-        static thread_local char name[96];
-        snprintf(name, sizeof name, "k_cg_lattice<%s, %s, false>", t.lsym ? "true" : "false",
-                 t.lhex ? "LatHex" : "LatKuhn");
-        return name;
-    }
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {
         static thread_local char name[96];

@@ -1,6 +1,6 @@
 // abi_pcg.cpp -- the PCG entry points of the C-ABI (include/cwf_hip.h; pcg.hpp:161-227): apply_keff, the block
 // Jacobi inverse, dot, solve_pcg (single handle and LOCAL groups) and the residual history, over the device
-// PCG driver run_pcg_group (the FAST / PARITY / sharded / single-launch schedules, enqueued in batches with only
+// PCG driver run_pcg_group (the FAST / PARITY / sharded schedules, enqueued in batches with only
 // the control block read back).
 #include <cmath>
 #include <cstring>
@@ -59,17 +59,7 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (cwf_hip_system *m : g)
             HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
-    bool cg = fast;  // one launch per iteration (structured blocks, every member)
-    for (cwf_hip_system *m : g)
-        cg = cg && fast_cg_enabled(m);
-    if (cg && sharded)
-    {
-        if (int e = sharded_cg_init(g, rhs, set.relative_tolerance))
-            return e;
-    }
-    else if (cg)
-        fast_cg_init(h, rhs[0], set.relative_tolerance, st);
-    else if (sharded)
+    if (sharded)
     {
         if (int e = fast ? sharded_pcg_init(g, rhs, set.relative_tolerance)
                          : sharded_parity_init(g, rhs, set.relative_tolerance))
@@ -136,14 +126,7 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         {
             const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
             hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
-            if (cg && sharded)
-            {
-                if (int e = sharded_cg_iteration(g, (unsigned)(enq + i), e0, e1))
-                    return e;
-            }
-            else if (cg)
-                fast_cg_iteration(h, (unsigned)(enq + i), st, e0, e1);
-            else if (fast)
+            if (fast)
             {
                 if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
                     return e;
@@ -156,10 +139,7 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             else
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
-        if (cg)
-            for (cwf_hip_system *m : g)
-                fast_cg_check(m, (unsigned)(enq + nb), m->stream);
-        else if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
+        if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
             for (cwf_hip_system *m : g)
                 fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
         HIPTRY(h, hipGetLastError());
@@ -172,9 +152,6 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
         for (size_t i = 0; i < g.size(); ++i)
             fast_flush_x(g[i], rhs[i], g[i]->stream);
-    if (cg && (h->ctl_host->iterations & 1u))  // r_n lives in the second buffer for odd n
-        for (cwf_hip_system *m : g)
-            HIPTRY(m, hipMemcpyAsync(m->r, m->cg_r2, m->ds.D * sizeof(float), hipMemcpyDeviceToDevice, m->stream));
     if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows
     {
         if (int e = comm_halo(g, &cwf_hip_system::x))

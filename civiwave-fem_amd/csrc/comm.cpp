@@ -262,42 +262,6 @@ int sharded_pcg_init(const std::vector<cwf_hip_system *> &g, const std::vector<c
     return 0;
 }
 
-// The single-launch (Chronopoulos-Gear) iteration of structured-block shards (lattice_cg.inc): one exchange step
-// per iteration instead of two. Launch i needs, on its ghost planes, r_i, w_i and s_(i-1) (it recomputes u_(i+1)
-// there from them, as it does for every halo entry) and every rank's {r.r, r.u, w.u} of launch i - 1, so after
-// each launch a rank folds its group totals into its slot and one grouped step all-gathers the slots (4 f64 per
-// rank, folded in rank order by every rank: identical scalars everywhere) and sends the three halos.
-int sharded_cg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
-{
-    if (int st = sharded_pcg_init(g, rhs, rel_tol))  // r_0, norms, u_0 = z (+ its halo), rho, p_(-1)
-        return st;
-    for (cwf_hip_system *h : g)
-    {
-        const uint32_t Down = 3u * h->ds.Nown;
-        fast_keff(h, h->z, h->Ap, false, nullptr, nullptr, h->stream);  // w_0 on the owned rows
-        fast_dot(h->z, h->r, h->Ap, Down, h->part0, h->part1, h->stream);
-        HIPTRY(h, hipMemsetAsync(h->g_cg + 4 * h->rank, 0, 4 * sizeof(double), h->stream));
-        fold_pair(h->part0, h->part1, fast_dot_blocks(Down), h->g_cg + 4 * h->rank + 1, h->stream);  // gamma, delta
-    }
-    std::vector<std::vector<float *>> vecs;
-    for (cwf_hip_system *h : g)
-        vecs.push_back({fast_cg_vec(h, 'r', 0), fast_cg_vec(h, 'w', 0)});
-    return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);
-}
-
-int sharded_cg_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1)
-{
-    for (size_t i = 0; i < g.size(); ++i)
-    {
-        fast_cg_iteration(g[i], it, g[i]->stream, i ? nullptr : e0, i ? nullptr : e1);
-        fast_cg_fold_rank(g[i], it, g[i]->stream);
-    }
-    std::vector<std::vector<float *>> vecs;
-    for (cwf_hip_system *h : g)
-        vecs.push_back({fast_cg_vec(h, 'r', it + 1), fast_cg_vec(h, 'w', it + 1), fast_cg_vec(h, 's', it)});
-    return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);
-}
-
 // one FAST PCG iteration of every member (a single unsharded handle is the group {h} with one rank): two
 // exchange steps, p.Ap after the tiles kernel and {r.r, r.z} + the z halo (one RCCL group) after the update
 int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
@@ -586,50 +550,6 @@ void cwf_hip_comm_destroy(cwf_hip_comm *cm)
 
 }  // extern "C"
 
-namespace cwf
-{
-// The single-launch iteration on a structured-block shard forms u = M^-1 r on its ghost planes from each node's
-// class byte. A ghost plane is globally interior along z, but its local class says "surface" (the shard's mesh
-// stops one cell layer past its owned planes), and its local diagonal blocks and lumped mass are partial. So at
-// attach every ghost-plane node takes the class of its global position (z inside), whose block inverse then comes
-// from an owned representative node (complete rows) at the next block-Jacobi build. A shard whose classes have no
-// owned representative keeps the two-kernel iteration (cg_shard stays false).
-int attach_ghost_classes(cwf_hip_system *h)
-{
-    DevTiles &t = h->ds.t;
-    h->cg_shard = false;
-    if (!t.lcls || !t.lmu || !h->cg_r2 || h->mode != CWF_MODE_FAST)
-        return 0;
-    const uint64_t N = h->ds.N, Nown = h->ds.Nown, per = (uint64_t)t.lnx * t.lny;
-    std::vector<uint8_t> cls(N);
-    HIPTRY(h, hipMemcpy(cls.data(), t.lcls, N, hipMemcpyDeviceToHost));
-    for (uint32_t k = 0; k < t.lnz; ++k)
-    {
-        const uint64_t b = h->lat_plane[k];
-        if (b < Nown)
-            continue;
-        for (uint64_t q = 0; q < per && b + q < N; ++q)
-        {
-            const uint32_t c = cls[b + q], ty = c >> 3, tz = ty / 9;
-            cls[b + q] = (uint8_t)((ty - 9 * tz + 9) << 3 | (c & 7u));
-        }
-    }
-    std::vector<uint32_t> rep(kLatClasses, 0xFFFFFFFFu);
-    for (uint64_t n = 0; n < Nown; ++n)
-        if (rep[cls[n]] == 0xFFFFFFFFu)
-            rep[cls[n]] = (uint32_t)n;
-    for (uint64_t n = Nown; n < N; ++n)
-        if (rep[cls[n]] == 0xFFFFFFFFu)
-            return 0;  // a ghost class without an owned representative
-    HIPTRY(h, hipMemcpy(const_cast<uint8_t *>(t.lcls), cls.data(), N, hipMemcpyHostToDevice));
-    HIPTRY(h, hipMemcpy(const_cast<uint32_t *>(t.lrep), rep.data(), kLatClasses * sizeof(uint32_t),
-                        hipMemcpyHostToDevice));
-    h->inv_fast = false;  // rebuild the class inverses from the new representatives
-    h->cg_shard = true;
-    return 0;
-}
-}  // namespace cwf
-
 extern "C" {
 
 int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, const cwf_shard_info *plan)
@@ -673,14 +593,13 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         return 0;
     };
     void *p = nullptr;
-    if (int st = alloc(&p, 10 * (size_t)n * sizeof(double)))
+    if (int st = alloc(&p, 6 * (size_t)n * sizeof(double)))
         return st;
     h->g_pap = static_cast<double *>(p);
     h->g_rrz = h->g_pap + n;
     h->g_init = h->g_rrz + 2 * n;
     h->g_rz0 = h->g_init + 2 * n;
-    h->g_cg = h->g_rz0 + n;
-    HIPTRY(h, hipMemset(h->g_pap, 0, 10 * (size_t)n * sizeof(double)));
+    HIPTRY(h, hipMemset(h->g_pap, 0, 6 * (size_t)n * sizeof(double)));
     if (int st = alloc(&p, nsend * sizeof(uint32_t)))
         return st;
     h->send_idx = static_cast<uint32_t *>(p);
@@ -713,8 +632,6 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         t.lk1 = k0 < k1 ? k1 : 1;
         t.lzr = 0;  // the update pass stores z: the halo exchange carries z, and a ghost's class is a local one
         lattice_plan(t);
-        if (int st = attach_ghost_classes(h))
-            return st;
     }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
     h->owned_contiguous = true;  // PARITY shards fold chunk partials in global order (comm.cpp parity_setup)

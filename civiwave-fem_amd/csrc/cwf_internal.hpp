@@ -296,15 +296,6 @@ struct cwf_hip_system
     // Ap is scratch (apply_keff staging, PARITY's K p, the prologues' K x); FAST PCG never reads it
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
     float *p2 = nullptr, *p3 = nullptr, *p4 = nullptr;  // FAST: p_j lives in {p, p2, p3, p4}[(j + 1) % 4]
-    // single-launch (Chronopoulos-Gear) FAST PCG of a structured block (lattice_cg.inc): r_i in {r, cg_r2}[i % 2],
-    // w_i = K u_i in {Ap, cg_w2}[i % 2], s_i in {cg_s0, cg_s1}[i % 2]
-    float *cg_r2 = nullptr, *cg_w2 = nullptr, *cg_s0 = nullptr, *cg_s1 = nullptr;
-    // FAST PCG scalars folded by their producers (spmv_tiles.hip fold_publish): gsum = 4 sets of [32][4] group
-    // totals ([0] the update pass's {r.r, r.z}, [1] K_eff's p.Ap, [2] / [3] the single-launch iteration's
-    // {r.r, r.u, w.u} by iteration parity); gcnt = 2 sets of 32 arrival counters, 64 B apart ([0] update /
-    // single-launch, [1] K_eff); the per-workgroup shares go to part1 (update) and part0 (K_eff, single-launch)
-    double *gsum = nullptr;
-    unsigned *gcnt = nullptr;
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's
@@ -346,8 +337,6 @@ struct cwf_hip_system
     double *g_rrz = nullptr;   // [2 nranks]    {r.r, r.z}
     double *g_init = nullptr;  // [2 nranks]    {rhs.rhs, r0.r0}
     double *g_rz0 = nullptr;   // [nranks]      r0.z0
-    double *g_cg = nullptr;    // [4 nranks]    the single-launch iteration's {r.r, r.u, w.u, -} per rank
-    bool cg_shard = false;     // an attached structured-block shard whose ghost planes carry global node classes
     // sharded PARITY: every rank's 256-DOF chunk partials all-gathered into slot [r * pstride, (r+1) * pstride)
     // (zero-padded past the rank's own chunk count) and folded in that order on every rank = the global chunk
     // order of pcg.cpp:170-207, since the owned node ranges are ascending by rank and aligned to whole chunks
@@ -432,15 +421,7 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
 void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st);  // the lazy x terms still pending
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
-// single-launch (Chronopoulos-Gear) PCG of an unsharded structured block with the class preconditioner
-bool fast_cg_enabled(const cwf_hip_system *h);
-void fast_cg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
-void fast_cg_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
-void fast_cg_check(cwf_hip_system *h, unsigned it, hipStream_t st);
-void fast_cg_fold_rank(cwf_hip_system *h, unsigned it, hipStream_t st);  // this rank's triple -> g_cg[4 rank]
-float *fast_cg_vec(cwf_hip_system *h, char which, unsigned i);         // 'r' r_i, 'w' w_i, 's' s_i buffers
-int sharded_cg_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
-int sharded_cg_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1);
+
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
 unsigned fast_update_blocks(const DevSys &s, bool flush);  // grid of update pass (lazy-x iteration or not)
@@ -452,7 +433,7 @@ void fast_fold_pap(cwf_hip_system *h, hipStream_t st);  // local p.Ap shares -> 
 void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st);  // local r.r / r.z shares -> g_rrz[2 rank]
 void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st, float *dst = nullptr);  // dst: sendbuf
 void fast_block_inverse(cwf_hip_system *h, hipStream_t st);  // parity BJ, symmetrised + packed to inv6
-void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st, uint32_t stride = 1);
+void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st);
 void fast_init_scalars_strided(cwf_hip_system *h, const double *p_rhs, const double *p_rr, uint32_t count,
                                uint32_t stride, double rel_tol, hipStream_t st);
 void fast_rho_from(cwf_hip_system *h, const double *p_rz, uint32_t count, hipStream_t st);
@@ -464,7 +445,7 @@ struct Gather
 };
 int comm_exchange(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                   float *cwf_hip_system::*vec);
-constexpr size_t kMaxHaloVecs = 3;  // halo vectors of one exchange step (the single-launch iteration's r, w, s)
+constexpr size_t kMaxHaloVecs = 3;  // halo vectors of one exchange step
 constexpr int kMaxPeers = 16;       // ranks of a PEER communicator
 // peer.hip: the PEER communicator's mailbox (at attach), its exchange step, and its teardown
 int peer_attach(cwf_hip_system *h);

@@ -34,8 +34,6 @@ inline constexpr Knob kKnobs[] = {
                    "(default: the latter from 2M nodes)"},
     {"CWF_LAT_SHELL_LAST", "0|1: the lattice shell workgroups lead / follow the bricks (default: follow when the "
                            "grid fits one round of resident workgroups)"},
-    {"CWF_LAT_CG", "0: structured blocks run the two-kernel PCG iteration (k_keff_lattice + update pass) instead of "
-                   "the single-launch Chronopoulos-Gear iteration (lattice_cg.inc)"},
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},

@@ -382,8 +382,9 @@ int cwf_hip_comm_peer_connect(cwf_hip_comm *cm, const uint8_t *handles)
     return 0;
 }
 
-// `steps` exchange steps of the single-launch iteration's shape (one 4-double slot all-gather, the r, w, s halos)
-// on h's stream, hipEvent-timed: the per-step latency the 8-GPU projection uses (every rank calls it)
+// `steps` exchange steps shaped like the FAST iteration's second one (the {r.r, r.z} all-gather and the z halo;
+// the first, p.Ap, has no halo) on h's stream, hipEvent-timed: the per-step latency the 8-GPU projection uses
+// (every rank calls it)
 int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_step)
 {
     if (!h || !us_per_step || steps < 1 || !h->sharded() || !h->comm)
@@ -393,12 +394,12 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
     HIPTRY(h, hipEventCreate(&e0));
     HIPTRY(h, hipEventCreate(&e1));
     std::vector<cwf_hip_system *> g{h};
-    std::vector<std::vector<float *>> vecs{{h->r, h->Ap, h->z}};
-    int st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);  // warm
+    std::vector<std::vector<float *>> vecs{{h->z}};
+    int st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_rrz, 2}}, vecs);  // warm
     if (!st && hipEventRecord(e0, h->stream) != hipSuccess)
         st = set_error(h, CWF_ERR_HIP, "hipEventRecord");
     for (int i = 0; i < steps && !st; ++i)
-        st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_cg, 4}}, vecs);
+        st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_rrz, 2}}, vecs);
     float ms = 0.f;
     if (!st && hipEventRecord(e1, h->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess)
         (void)hipEventElapsedTime(&ms, e0, e1);

@@ -84,96 +84,6 @@ template <int NT> __device__ __forceinline__ double block_sum(double v, double *
     return t;
 }
 
-// NV (<= 3) NT-thread block sums in a fixed order, valid in every thread; red: 3 NT / 64 doubles
-template <int NT, int NV>
-__device__ __forceinline__ void block_sum_n(double (&v)[NV], double *red)
-{
-#pragma unroll
-    for (int q = 0; q < NV; ++q)
-        v[q] = wave_sum(v[q]);
-    if ((threadIdx.x & 63) == 0)
-#pragma unroll
-        for (int q = 0; q < NV; ++q)
-            red[NV * (threadIdx.x >> 6) + q] = v[q];
-    __syncthreads();
-    double t[NV];
-#pragma unroll
-    for (int q = 0; q < NV; ++q)
-        t[q] = 0.0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w)
-#pragma unroll
-        for (int q = 0; q < NV; ++q)
-            t[q] += red[NV * w + q];
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NV; ++q)
-        v[q] = t[q];
-}
-
-// ---- the PCG scalars' per-workgroup shares, folded once by their producer (no consumer refolds them) ----
-// Every workgroup leaves its block-summed share (<= 3 values) write-through at share[4 b ..] and takes a ticket on
-// its group's arrival counter (group = b mod kFoldGroups, one 64-B line per counter); the group's last arriver
-// folds the group's shares (workgroups g, g + 32, ... in that order: thread t takes every NT-th, then a fixed-order
-// block sum) with sc1 loads and stores the group total at gtot[4 g ..], then resets the counter. A consumer (the
-// next launch) folds the min(grid, 32) group totals in group order. The order is fixed throughout, so the scalars
-// do not depend on arrival order or workgroup placement: bitwise the same run to run. The hand-off is the
-// counter form of MI355X_MICROARCH.md's visibility table ("one lane of each storing workgroup, for all that
-// workgroup's stores, an agent-scope atomic add ... the last arriver told by the value its add returned": sc1
-// stores drained before the add, sc1 loads after it). Before, every consumer workgroup refolded up to 2,048
-// producer shares itself (C3 lattice: 95 MB of L2 reads per K_eff launch).
-constexpr unsigned kFoldGroups = 32, kCntStride = 16;
-struct FoldOut
-{
-    double *share;  // [grid][4]
-    double *gtot;   // [kFoldGroups][4]
-    unsigned *cnt;  // [kFoldGroups * kCntStride], zero between launches
-};
-inline unsigned fold_groups(unsigned grid) { return grid < kFoldGroups ? grid : kFoldGroups; }
-typedef unsigned long long fold_u64;
-
-template <int NT, int NV>
-__device__ __forceinline__ void fold_publish(const FoldOut &f, double (&v)[NV], double *red)
-{
-    block_sum_n<NT, NV>(v, red);
-    unsigned *lastf = reinterpret_cast<unsigned *>(red);  // red is free again after the block sum
-    const unsigned G = gridDim.x, b = blockIdx.x, g = b % kFoldGroups, ng = (G - g + kFoldGroups - 1) / kFoldGroups;
-    if (threadIdx.x == 0)
-    {
-        fold_u64 *sh = reinterpret_cast<fold_u64 *>(f.share + 4ull * b);
-#pragma unroll
-        for (int q = 0; q < NV; ++q)
-            __hip_atomic_store(sh + q, (fold_u64)__double_as_longlong(v[q]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old =
-            __hip_atomic_fetch_add(f.cnt + kCntStride * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *lastf = old + 1u == ng ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!*lastf)
-        return;
-    double w[NV];
-#pragma unroll
-    for (int q = 0; q < NV; ++q)
-        w[q] = 0.0;
-    for (unsigned j = threadIdx.x; j < ng; j += NT)
-    {
-        fold_u64 *sh = reinterpret_cast<fold_u64 *>(f.share + 4ull * (g + kFoldGroups * j));
-#pragma unroll
-        for (int q = 0; q < NV; ++q)
-            w[q] += __longlong_as_double((long long)__hip_atomic_load(sh + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();  // lastf (in red) read by every thread before the block sum reuses red
-    block_sum_n<NT, NV>(w, red);
-    if (threadIdx.x == 0)
-    {
-#pragma unroll
-        for (int q = 0; q < NV; ++q)
-            f.gtot[4 * g + q] = w[q];
-        __hip_atomic_store(f.cnt + kCntStride * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 template <int NT>
 __device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigned count, double *red,
                                            unsigned stride = 1)
@@ -481,9 +391,9 @@ struct PcgArgs
 {
     const float *z;           // z (PCG); x holds p_old
     Ctl *ctl;
-    FoldOut pap;              // out: the p.Ap shares, folded to group totals (fold_publish)
-    const double *prr, *prz;  // in: {r.r, r.z} of the previous update: its group totals (stride 4), or the
-    unsigned nupd;            //     all-gathered per-rank pairs of a sharded system (stride 2)
+    double *part_dot;         // out: per-tile p.Ap share
+    const double *prr, *prz;  // in: folded {r.r, r.z} of the previous update (per rank)
+    unsigned nupd;
     unsigned stride;
     unsigned it;
     double *hist;
@@ -793,8 +703,9 @@ __global__ __launch_bounds__(NT) void k_keff_tiles(DevSys s, const float *__rest
     }
     if constexpr (MODE == 1)
     {
-        double v[1] = {pap};
-        fold_publish<NT, 1>(pa.pap, v, red);
+        const double t = block_sum<NT>(pap, red);
+        if (threadIdx.x == 0)
+            pa.part_dot[blockIdx.x] = t;
     }
 }
 
@@ -1051,8 +962,9 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
     }
     if constexpr (MODE == 1)
     {
-        double v[1] = {pap};
-        fold_publish<NT, 1>(pa.pap, v, red);
+        const double tt = block_sum<NT>(pap, red);
+        if (threadIdx.x == 0)
+            pa.part_dot[blockIdx.x] = tt;
     }
 }
 
@@ -1426,8 +1338,9 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
     }
     if constexpr (MODE == 1)
     {
-        double v[1] = {pap};
-        fold_publish<NT, 1>(pa.pap, v, red);
+        const double tt = block_sum<NT>(pap, red);
+        if (threadIdx.x == 0)
+            pa.part_dot[blockIdx.x] = tt;
     }
 }
 
@@ -1446,11 +1359,11 @@ __global__ __launch_bounds__(256) void k_pcg_check(Ctl *ctl, const double *__res
 
 // one workgroup: out[0] = fold(a[0..n)), out[1] = fold(b[0..n)) (b may be NULL), fixed order
 __global__ __launch_bounds__(1024) void k_fold_pair(const double *__restrict__ a, const double *__restrict__ b,
-                                                    unsigned n, unsigned stride, double *__restrict__ out)
+                                                    unsigned n, double *__restrict__ out)
 {
     __shared__ double red[16];
-    const double ta = fold_all<1024>(a, n, red, stride);
-    const double tb = b ? fold_all<1024>(b, n, red, stride) : 0.0;
+    const double ta = fold_all<1024>(a, n, red);
+    const double tb = b ? fold_all<1024>(b, n, red) : 0.0;
     if (threadIdx.x == 0)
     {
         out[0] = ta;
@@ -1565,9 +1478,9 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     DevSys s, const float *__restrict__ rhs, const float *__restrict__ inv, const float *__restrict__ inv9,
     float *__restrict__ x, float *__restrict__ r, float *__restrict__ z, const float *__restrict__ pold,
     float *__restrict__ pnew, Ctl *__restrict__ ctl, const double *__restrict__ part_dot, unsigned ntp,
-    unsigned pstride, FoldOut rrz, unsigned it, int wt, PBufs pbuf, unsigned lag)
+    double *__restrict__ prr, double *__restrict__ prz, unsigned it, int wt, PBufs pbuf, unsigned lag)
 {
-    __shared__ double red[2 * (kUpdThreads / 64)];
+    __shared__ double red[kUpdThreads / 64];
     __shared__ uint4 cinv[LAT ? kLatClasses : 1];
     if (!ctl->active)
         return;
@@ -1661,7 +1574,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     if (base < s.Nown)
         load_nodes(base);
     // pcg.cpp:840-852: alpha = rho / (p . Ap)
-    const double denom = fold_all<kUpdThreads>(part_dot, ntp, red, pstride);
+    const double denom = fold_all<kUpdThreads>(part_dot, ntp, red);
     if (fabs(denom) < 1.0e-18)
     {
         if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1805,8 +1718,13 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         for (int k = 0; k < 3; ++k)
             pnew[3u * n + k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
     }
-    double sh2[2] = {rr, rz};
-    fold_publish<kUpdThreads, 2>(rrz, sh2, red);
+    const double t0 = block_sum<kUpdThreads>(rr, red);
+    const double t1 = block_sum<kUpdThreads>(rz, red);
+    if (threadIdx.x == 0)
+    {
+        prr[blockIdx.x] = t0;
+        prz[blockIdx.x] = t1;
+    }
 }
 
 inline unsigned grid_for(uint32_t n, uint32_t b) { return (n + b - 1) / b; }
@@ -1830,7 +1748,6 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 
 #include "hex8_tiles.inc"
 #include "lattice.inc"
-#include "lattice_cg.inc"
 
 // pipelined kernel: element forces + local CSR + per tile node {x y z v_x}{v_y v_z}
 inline size_t pipe_lds(const DevSys &s)
@@ -2085,9 +2002,6 @@ __global__ __launch_bounds__(256) void k_x_flush(DevSys s, const float *__restri
 // x / r / z of the update pass are stored write-through (store3; C2 +2.7% PCG it/s, C3 neutral)
 static bool update_write_through() { return true; }
 
-inline FoldOut fold_out_pap(cwf_hip_system *h) { return FoldOut{h->part0, h->gsum + 128, h->gcnt + 32 * kCntStride}; }
-inline FoldOut fold_out_rrz(cwf_hip_system *h) { return FoldOut{h->part1, h->gsum, h->gcnt}; }
-
 // iteration `it`: residual step of it-1's update (beta, convergence) + p_new + tile partials + p.Ap shares
 void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
@@ -2100,10 +2014,10 @@ void fast_tiles_pcg(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e
     // lzr: the lattice kernel forms z from r (pa.z carries r)
     const float *pz = s.t.lzr ? h->r : h->z;
     PcgArgs pa = fast_direct_fold(h)
-                     ? PcgArgs{pz, h->ctl, fold_out_pap(h), h->gsum, h->gsum + 1,
-                               fold_groups(fast_update_blocks(s, it && x_flush_iter(it - 1u))), 4u, it, h->hist, abl,
+                     ? PcgArgs{pz, h->ctl, h->part0, h->part1, h->part2,
+                               fast_update_blocks(s, it && x_flush_iter(it - 1u)), 1u, it, h->hist, abl,
                                fast_p_new(h, it)}
-                     : PcgArgs{pz, h->ctl, fold_out_pap(h), h->g_rrz, h->g_rrz + 1,
+                     : PcgArgs{pz, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1,
                                (unsigned)h->nranks, 2u, it, h->hist, abl, fast_p_new(h, it)};
     if (s.iso)
         launch_tiles<true, false, 1>(s, fast_p_old(h, it), pa, tile_threads(), st, e0, e1);
@@ -2122,8 +2036,8 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
                          : (xf ? k_pcg_update_tiles<1, true, false> : k_pcg_update_tiles<1, false, false>);
     k<<<fast_update_blocks(s, xf), kUpdThreads, 0, st>>>(
         s, rhs, h->inv6, h->inv, h->x, h->r, h->z, fast_p_old(h, it), fast_p_new(h, it), h->ctl,
-        direct ? h->gsum + 128 : h->g_pap, direct ? fold_groups(fast_tile_blocks(s)) : (unsigned)h->nranks,
-        direct ? 4u : 1u, fold_out_rrz(h), it, update_write_through(), fast_p_bufs(h), x_lag());
+        direct ? h->part0 : h->g_pap, direct ? fast_tile_blocks(s) : (unsigned)h->nranks, h->part1, h->part2, it,
+        update_write_through(), fast_p_bufs(h), x_lag());
 }
 
 void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st)
@@ -2135,112 +2049,11 @@ void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st)
     k_x_flush<<<g, 256, 0, st>>>(s, rhs, h->x, h->ctl, fast_p_bufs(h), x_lag());
 }
 
-// ---- single-launch (Chronopoulos-Gear) PCG of a structured block, lattice_cg.inc ----
-// the handle allocated the Chronopoulos-Gear buffers at create (abi.cpp; CWF_LAT_CG=0 there keeps the two-kernel
-// iteration, k_keff_lattice + k_pcg_update_tiles)
-bool fast_cg_enabled(const cwf_hip_system *h)
-{
-    const DevTiles &t = h->ds.t;
-    return h->mode == CWF_MODE_FAST && (!h->sharded() || h->cg_shard) && t.lat && t.lcls && t.lmu &&
-           h->cg_r2 != nullptr;
-}
-
-float *fast_cg_vec(cwf_hip_system *h, char which, unsigned i)
-{
-    float *R[2] = {h->r, h->cg_r2}, *W[2] = {h->Ap, h->cg_w2}, *S[2] = {h->cg_s0, h->cg_s1};
-    return (which == 'r' ? R : which == 'w' ? W : S)[i & 1u];
-}
-
-// solve_pcg prologue (pcg.cpp:744-828) plus the Chronopoulos-Gear start: w_0 = K u_0, gamma_0 = r_0.u_0,
-// delta_0 = w_0.u_0 (group total 0 of parity 0), the arrival counters zeroed
-void fast_cg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st)
-{
-    const DevSys &s = h->ds;
-    const uint32_t nbD = fast_dot_blocks(s.D);
-    fast_block_inverse(h, st);
-    fast_keff(h, h->x, h->Ap, true, nullptr, nullptr, st);
-    launch_init_residual(h, rhs, st);
-    fast_dot(rhs, rhs, nullptr, s.D, h->part0, nullptr, st);
-    fast_dot(h->r, h->r, nullptr, s.D, h->part1, nullptr, st);
-    fast_init_scalars_strided(h, h->part0, h->part1, nbD, 1u, rel_tol, st);
-    launch_precond(h, h->ctl, st);  // u_0 -> z
-    launch_p_init(h, st);           // the p_(-1) of launch 0 (times beta_0 = 0)
-    fast_keff(h, h->z, h->Ap, false, nullptr, nullptr, st);  // w_0
-    fast_dot(h->z, h->r, h->Ap, s.D, h->part0, h->part1, st);
-    k_cg_init<<<1, 256, 0, st>>>(h->ctl, h->part0, h->part1, nbD, h->gsum + 2 * 128);
-}
-
-static CgArgs cg_args(cwf_hip_system *h, unsigned it)
-{
-    CgArgs a{};
-    a.ctl = h->ctl;
-    a.rin = fast_cg_vec(h, 'r', it);
-    a.rout = fast_cg_vec(h, 'r', it + 1u);
-    a.win = fast_cg_vec(h, 'w', it);
-    a.wout = fast_cg_vec(h, 'w', it + 1u);
-    a.sin = it ? fast_cg_vec(h, 's', it - 1u) : nullptr;
-    a.sout = fast_cg_vec(h, 's', it);
-    a.pold = fast_p_old(h, it);
-    a.pnew = fast_p_new(h, it);
-    a.x = h->x;
-    a.pb = fast_p_bufs(h);
-    a.lag = x_lag();
-    // a shard folds the all-gathered per-rank triples (rank order), a single handle its own group totals
-    a.gin = h->sharded() ? h->g_cg : h->gsum + 128u * (2u + (it & 1u));
-    a.ngin = h->sharded() ? (unsigned)h->nranks : it ? fold_groups(h->ds.t.lnwork) : kFoldGroups;
-    a.fo = FoldOut{h->part0, h->gsum + 128u * (2u + ((it + 1u) & 1u)), h->gcnt};
-    a.it = it;
-    a.hist = h->hist;
-    return a;
-}
-
-template <bool SYM, class E, bool XF>
-static void cg_launch(cwf_hip_system *h, const CgArgs &a, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
-{
-    const DevSys &s = h->ds;
-    const auto k = k_cg_lattice<SYM, E, XF>;
-    if (e0 && e1)
-        hipExtLaunchKernelGGL(k, dim3(s.t.lnwork), dim3(kLatNT), 0, st, e0, e1, 0, s, a, s.t.lcoef, s.t.lplane);
-    else
-        k<<<s.t.lnwork, kLatNT, 0, st>>>(s, a, s.t.lcoef, s.t.lplane);
-}
-
-template <class E>
-static void cg_launch_e(cwf_hip_system *h, const CgArgs &a, bool xf, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
-{
-    if (h->ds.t.lsym)
-        xf ? cg_launch<true, E, true>(h, a, st, e0, e1) : cg_launch<true, E, false>(h, a, st, e0, e1);
-    else
-        xf ? cg_launch<false, E, true>(h, a, st, e0, e1) : cg_launch<false, E, false>(h, a, st, e0, e1);
-}
-
-void fast_cg_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
-{
-    const CgArgs a = cg_args(h, it);
-    const bool xf = x_flush_iter(it);
-    if (h->ds.t.lhex)
-        cg_launch_e<LatHex>(h, a, xf, st, e0, e1);
-    else
-        cg_launch_e<LatKuhn>(h, a, xf, st, e0, e1);
-}
-
-void fast_cg_check(cwf_hip_system *h, unsigned it, hipStream_t st)
-{
-    k_cg_check<<<1, 64, 0, st>>>(cg_args(h, it));
-}
-
-// a shard's {r.r, r.u, w.u} of launch `it` (its group totals, folded in group order) into its all-gather slot
-void fast_cg_fold_rank(cwf_hip_system *h, unsigned it, hipStream_t st)
-{
-    k_fold_triple<<<1, 64, 0, st>>>(h->ctl, h->gsum + 128u * (2u + ((it + 1u) & 1u)), fold_groups(h->ds.t.lnwork),
-                                    h->g_cg + 4 * h->rank);
-}
-
 // diagnostic: `reps` PCG-mode tiles launches with side-effect-free preambles (ablation bits | 32)
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    PcgArgs pa{s.t.lzr ? h->r : h->z, h->ctl, fold_out_pap(h), h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
+    PcgArgs pa{s.t.lzr ? h->r : h->z, h->ctl, h->part0, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, 1u,
                h->hist, abl | 32u};
     for (int i = 0; i < reps; ++i)
         launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
@@ -2249,9 +2062,8 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
     if (fast_direct_fold(h))
-        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->gsum, h->gsum + 1,
-                                       fold_groups(fast_update_blocks(h->ds, it && x_flush_iter(it - 1u))), 4u, it,
-                                       h->hist);
+        k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->part1, h->part2,
+                                       fast_update_blocks(h->ds, it && x_flush_iter(it - 1u)), 1u, it, h->hist);
     else
         k_pcg_check<<<1, 256, 0, st>>>(h->ctl, h->g_rrz, h->g_rrz + 1, (unsigned)h->nranks, 2u, it, h->hist);
 }
@@ -2273,29 +2085,28 @@ void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
         k_lat_class_inverse<<<1, 256, 0, st>>>(h->ds.t.lrep, h->inv6, h->inv, h->ds.t.lcinv6, h->ds.t.lcinv9);
 }
 
-void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st, uint32_t stride)
+void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st)
 {
-    k_fold_pair<<<1, 1024, 0, st>>>(a, b, n, stride, out);
+    k_fold_pair<<<1, 1024, 0, st>>>(a, b, n, out);
 }
 
-// a single (unsharded) handle skips the per-rank fold kernels: every consumer workgroup folds the producer's
-// <= 32 group totals itself (fold_publish), two launches fewer per iteration (C2 +11% PCG it/s against fold
-// kernels, same-box A/B, round 2)
+// a single (unsharded) handle skips the per-rank fold kernels: every consumer workgroup refolds the
+// producer's per-workgroup shares itself (<= 2048 doubles, L2-served), two launches fewer per iteration
+// (C2 +11% PCG it/s against fold kernels, same-box A/B, round 2)
 bool fast_direct_fold(const cwf_hip_system *h) { return !h->sharded(); }
 
 void fast_fold_pap(cwf_hip_system *h, hipStream_t st)
 {
     if (fast_direct_fold(h))
         return;
-    fold_pair(h->gsum + 128, nullptr, fold_groups(fast_tile_blocks(h->ds)), h->g_pap + h->rank, st, 4u);
+    fold_pair(h->part0, nullptr, fast_tile_blocks(h->ds), h->g_pap + h->rank, st);
 }
 
 void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
     if (fast_direct_fold(h))
         return;
-    fold_pair(h->gsum, h->gsum + 1, fold_groups(fast_update_blocks(h->ds, x_flush_iter(it))), h->g_rrz + 2 * h->rank,
-              st, 4u);
+    fold_pair(h->part1, h->part2, fast_update_blocks(h->ds, x_flush_iter(it)), h->g_rrz + 2 * h->rank, st);
 }
 
 void halo_pack(cwf_hip_system *h, const float *v, hipStream_t st, float *dst)

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("CWF_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libcwf_hip.so")  # env: A/B builds
+DEFAULT_LIB = os.path.join(PKG_ROOT, "lib", "libcwf_hip.so")
+LIB_PATH = os.environ.get("CWF_LIB_PATH") or DEFAULT_LIB  # env: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "cwf_hip.h")
 
 PTR_HOST, PTR_DEVICE = 0, 1
@@ -195,6 +196,8 @@ def load() -> C.CDLL:
         "cwf_scenario_destroy": ([P], None),
     }
     for name, (args, res) in sig.items():
+        if LIB_PATH != DEFAULT_LIB and not hasattr(L, name):
+            continue  # an older build under same-box A/B (CWF_LIB_PATH) may lack newer entry points
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -318,8 +318,9 @@ void cwf_hip_comm_destroy(cwf_hip_comm *comm); /* after every attached handle is
 int cwf_hip_comm_create_peer(int32_t nranks, int32_t rank, int device, cwf_hip_comm **out);
 int cwf_hip_comm_peer_handle(cwf_hip_comm *comm, uint8_t *handle /* [CWF_IPC_HANDLE_BYTES] */);
 int cwf_hip_comm_peer_connect(cwf_hip_comm *comm, const uint8_t *handles /* [nranks * CWF_IPC_HANDLE_BYTES] */);
-/* `steps` exchange steps shaped like one single-launch PCG iteration's (a 4-double slot all-gather and three
- * halos) on the attached handle's stream, hipEvent-timed: microseconds per step (collective: every rank calls) */
+/* `steps` exchange steps shaped like the FAST PCG iteration's second one (the {r.r, r.z} all-gather and the z
+ * halo) on the attached handle's stream, hipEvent-timed: microseconds per step (collective: every rank calls);
+ * any communicator kind */
 int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_step);
 
 /* Make `h` (created from a shard's local desc with CWF_DESC_KEEP_NODE_ORDER) rank `rank` of `comm` with the

@@ -7,10 +7,7 @@ solves at tol 1e-6 within 1e-4 (relative) of the oracle's solution and its itera
 detection (and its refusal of a jittered mesh), bricks cut by the block's faces in every direction, partial
 Dirichlet masks, Rayleigh scalars, a randomly permuted node order (renumbered to the lattice order and back at
 the boundary), Newmark steps, the fan-group path on the same mesh (CWF_LATTICE=0), and slab shards (a shard's
-local order: owned planes, then ghost planes) through the LOCAL communicator. An unsharded block with the class
-preconditioner runs PCG as one launch per iteration (the Chronopoulos-Gear recurrences, lattice_cg.inc): checked
-against the oracle and against the two-kernel iteration (CWF_LAT_CG=0), for run-to-run determinism, work-item
-lengths and shell order, lazy-x batches and Newmark steps."""
+local order: owned planes, then ghost planes) through the LOCAL communicator."""
 import numpy as np
 import pytest
 
@@ -63,11 +60,8 @@ def permuted_block(nx, ny, nz, h=0.1, **kw):
     return scenarios.Case(f"perm{nx}x{ny}x{nz}", mesh, cfg, pack.build_packed_buffers(mesh, cfg))
 
 
-LATTICE = ("k_keff_lattice", "k_cg_lattice")
-
-
 def test_lattice_detected(case):
-    assert _kernel(_system(case)).startswith(LATTICE)
+    assert _kernel(_system(case)).startswith("k_keff_lattice")
 
 
 def test_jittered_mesh_is_not_a_lattice():
@@ -100,7 +94,7 @@ def test_lattice_work_item_lengths(L, shell, monkeypatch):
 def test_lattice_permuted_node_order():
     case = permuted_block(9, 7, 6, tol=1e-6, max_iterations=800)
     s = _system(case)
-    assert _kernel(s).startswith(LATTICE)
+    assert _kernel(s).startswith("k_keff_lattice")
     assert _apply_err(case, s) <= 2e-5
     o = oracle_system(case.packing, case.materials, *case.scalars())
     rhs = case.static_rhs()
@@ -130,8 +124,7 @@ def test_lattice_pcg_variants_solve(variant, monkeypatch):
     k): the strict interior's one lumped mass as a kernel argument with z = M^-1 r formed from r and the node
     class in the K_eff pass and no z stored by the update pass (CWF_LAT_ZR=1, the default from 2M nodes), or with z
     stored by the update pass (CWF_LAT_ZR=0, the default below), and the per-node mass through LDS
-    (CWF_LAT_MASS=0, which also stores z). The two-kernel iteration (CWF_LAT_CG=0; shards run it)."""
-    monkeypatch.setenv("CWF_LAT_CG", "0")
+    (CWF_LAT_MASS=0, which also stores z)."""
     monkeypatch.setenv("CWF_LAT_ZR", "1" if variant == "z-from-r" else "0")
     if variant == "per-node-mass":
         monkeypatch.setenv("CWF_LAT_MASS", "0")
@@ -178,7 +171,7 @@ def test_lattice_slab_shards(nranks):
     P = glob.packing
     sK, sM = glob.scalars()
     single = _system(glob)
-    assert _kernel(single).startswith(LATTICE)
+    assert _kernel(single).startswith("k_keff_lattice")
     rng = np.random.Generator(np.random.PCG64(7))
     x = rng.uniform(-1, 1, P.dof_count).astype(np.float32)
     y1 = np.zeros_like(x)
@@ -215,153 +208,24 @@ def test_lattice_slab_shards(nranks):
     assert abs(tel.iterations - n_ref) <= max(3, n_ref // 10)
 
 
-def _solve(s, rhs, mi, tol=1e-6):
-    x = np.zeros_like(rhs)
-    r = np.zeros_like(rhs)
-    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(mi, tol), pcg.PcgVectors(x, r)).value()
-    return t, x, r
-
-
-def test_cg_lattice_solve_close(case):
-    """The single-launch iteration (the default here) solves to the oracle's solution at the oracle's iteration count
-    +-10%, and the returned residual is the solve's: |r| is the telemetry's residual norm."""
-    s = _system(case)
-    assert _kernel(s).startswith("k_cg_lattice")
-    o = oracle_system(case.packing, case.materials, *case.scalars())
-    rhs = case.static_rhs()
-    mi = case.cfg.solver.max_iterations
-    t, x, r = _solve(s, rhs, mi)
-    ref = o.solve_pcg(rhs, mi, 1e-6)
-    assert t.converged and ref["telemetry"].converged
-    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
-    assert abs(t.iterations - ref["telemetry"].iterations) <= max(3, ref["telemetry"].iterations // 10)
-    assert abs(np.linalg.norm(r.astype(np.float64)) - t.residual_norm) <= 1e-5 * t.residual_norm
-
-
-def test_cg_matches_two_kernel_iteration(monkeypatch):
-    """Chronopoulos-Gear and the standard recurrences produce the same Krylov iterates in exact arithmetic: same
-    solution (1e-5), iteration counts within 3%, on a block with bricks cut in every direction."""
-    case = scenarios.block_case(40, 19, 9, h=0.1, tol=1e-6, max_iterations=1500)
-    rhs = case.static_rhs()
-    out = {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("CWF_LAT_CG", v)
-        s = _system(case)
-        assert _kernel(s).startswith("k_cg_lattice" if v == "1" else "k_keff_lattice")
-        out[v] = _solve(s, rhs, 1500)
-        assert out[v][0].converged
-    n0 = out["0"][0].iterations
-    assert abs(out["1"][0].iterations - n0) <= max(2, n0 * 3 // 100)
-    assert np.linalg.norm(out["1"][1] - out["0"][1]) <= 1e-5 * np.linalg.norm(out["0"][1])
-
-
-def test_cg_run_to_run_deterministic():
-    """Every reduction is folded in a fixed order (per-workgroup triples, ticketed group totals in ascending
-    workgroup order, eight group totals in group order): two solves give the same bits."""
+@pytest.mark.parametrize("mesh", ["lattice", "fan-groups"])
+def test_fast_solve_run_to_run_deterministic(mesh, monkeypatch):
+    """Every FAST reduction is folded in a fixed order (per-workgroup shares, then the consumer's fixed-order
+    fold; no atomics): two solves on one handle and one on a fresh handle give the same bits."""
+    if mesh == "fan-groups":
+        monkeypatch.setenv("CWF_LATTICE", "0")
     case = scenarios.block_case(33, 9, 5, h=0.1, tol=1e-6, max_iterations=800)
     rhs = case.static_rhs()
+
+    def solve(s):
+        x = np.zeros_like(rhs)
+        r = np.zeros_like(rhs)
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(800, 1e-6), pcg.PcgVectors(x, r)).value()
+        return t, x, r
+
     s = _system(case)
-    runs = [_solve(s, rhs, 800), _solve(s, rhs, 800), _solve(_system(case), rhs, 800)]
+    runs = [solve(s), solve(s), solve(_system(case))]
     for t, x, r in runs[1:]:
         assert t.iterations == runs[0][0].iterations and t.residual_norm == runs[0][0].residual_norm
         assert np.array_equal(x.view(np.uint32), runs[0][1].view(np.uint32))
         assert np.array_equal(r.view(np.uint32), runs[0][2].view(np.uint32))
-
-
-@pytest.mark.parametrize("shell", ["lead", "follow"])
-@pytest.mark.parametrize("L", ["2", "3", "64"])
-def test_cg_work_item_lengths(L, shell, monkeypatch):
-    """The single-launch iteration over chunk boundaries inside the block, one chunk over all planes, and the shell
-    workgroups before or after the bricks: the solution and iteration count of the default plan."""
-    case = scenarios.block_case(40, 17, 9, h=0.1, tol=1e-6, max_iterations=1500)
-    rhs = case.static_rhs()
-    t0, x0, _ = _solve(_system(case), rhs, 1500)
-    monkeypatch.setenv("CWF_LAT_L", L)
-    monkeypatch.setenv("CWF_LAT_SHELL_LAST", "1" if shell == "follow" else "0")
-    s = _system(case)
-    assert _kernel(s).startswith("k_cg_lattice")
-    t, x, _ = _solve(s, rhs, 1500)
-    assert t.converged
-    assert abs(t.iterations - t0.iterations) <= 2
-    assert np.linalg.norm(x - x0) <= 1e-5 * np.linalg.norm(x0)
-
-
-def test_cg_batches_and_warm_start():
-    """Check intervals of 1, 3 and 64 iterations (the batch-end residual step, k_cg_check, then the next launch
-    repeating it) give the same bits, and a warm-started second solve (x from the first) converges at once."""
-    case = scenarios.block_case(12, 8, 7, h=0.1, tol=1e-6, max_iterations=800)
-    rhs = case.static_rhs()
-    s = _system(case)
-    res = []
-    for ci in (1, 3, 64):
-        x = np.zeros_like(rhs)
-        r = np.zeros_like(rhs)
-        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(800, 1e-6, False), pcg.PcgVectors(x, r), check_interval=ci).value()
-        assert t.converged
-        res.append((t, x))
-    for t, x in res[1:]:
-        assert t.iterations == res[0][0].iterations
-        assert np.array_equal(x.view(np.uint32), res[0][1].view(np.uint32))
-    x = res[0][1].copy()
-    t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(800, 1e-6, True), pcg.PcgVectors(x, np.zeros_like(rhs))).value()
-    assert t.converged and t.iterations <= 2
-
-
-def test_cg_stepper_steps():
-    """Newmark steps (Rayleigh beta_R != 0: the damping product runs the apply kernel between solves) on the
-    single-launch iteration against PARITY."""
-    case = scenarios.block_case(10, 5, 6, h=0.1, xi=0.05, w=(10.0, 100.0), tol=1e-6, max_iterations=1500)
-    P = case.packing
-    ref = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_PARITY)
-    fast = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST)
-    for k in range(3):
-        tr = ref.step(0.01 * k).value()
-        tf = fast.step(0.01 * k).value()
-        assert tf.pcg.converged and tr.pcg.converged
-        assert abs(tf.pcg.iterations - tr.pcg.iterations) <= max(3, tr.pcg.iterations // 10)
-    for what in (Stepper.DISPLACEMENT, Stepper.VELOCITY):
-        ur, uf = ref.get_state(what), fast.get_state(what)
-        assert np.linalg.norm(uf - ur) <= 1e-4 * np.linalg.norm(ur)
-
-
-def _slab_solve(shape, nranks, mi=800):
-    """FAST solve of a Kuhn block cut into `nranks` slab sub-meshes (LOCAL communicator, one process)."""
-    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=1e-6, max_iterations=mi)
-    sK, sM = glob.scalars()
-    comm = shard.Comm.local(nranks)
-    systems, shards, rhs, xs, kerns = [], [], [], [], []
-    for r in range(nranks):
-        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, tol=1e-6)
-        src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
-        sh = shard.build_shard(src, begin, r, node_global)
-        s = sh.system(glob.materials, sK, sM)
-        comm.attach(s, sh)
-        kerns.append(_kernel(s))
-        systems.append(s)
-        shards.append(sh)
-        rhs.append(sh.local_dofs(case.static_rhs()))
-        xs.append(np.zeros(3 * sh.local_nodes, np.float32))
-    tel = shard.solve_pcg_group(systems, rhs, pcg.PcgSettings(mi, 1e-6), xs).value()
-    xg = np.zeros((glob.packing.node_count, 3), np.float32)
-    for sh, xl in zip(shards, xs):
-        xg[sh.node_global[: sh.owned_nodes].astype(np.int64)] = xl.reshape(-1, 3)[: sh.owned_nodes]
-    comm.close()
-    return glob, tel, xg.reshape(-1), kerns
-
-
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_cg_slab_shards(nranks, monkeypatch):
-    """Structured-block shards run the single-launch iteration too (one exchange step per iteration: the rank's
-    {r.r, r.u, w.u} all-gathered and the r, w, s halos; ghost planes take the class of their global position): the
-    oracle's solution, and the two-kernel sharded iteration's (CWF_LAT_CG=0) iteration count within 3%."""
-    shape = (13, 9, 4)
-    glob, tel, x, kerns = _slab_solve(shape, nranks)
-    assert all(k.startswith("k_cg_lattice") for k in kerns), kerns
-    ref = oracle_system(glob.packing, glob.materials, *glob.scalars()).solve_pcg(glob.static_rhs(), 800, 1e-6)
-    assert tel.converged
-    assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
-    monkeypatch.setenv("CWF_LAT_CG", "0")
-    _, tel0, x0, kerns0 = _slab_solve(shape, nranks)
-    assert all(k.startswith("k_keff_lattice") for k in kerns0), kerns0
-    assert abs(tel.iterations - tel0.iterations) <= max(2, tel0.iterations * 3 // 100)
-    assert np.linalg.norm(x - x0) <= 1e-5 * np.linalg.norm(x0)

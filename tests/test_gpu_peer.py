@@ -2,9 +2,9 @@
 
 The exchange steps are device-initiated stores into the peers' mailboxes and a flag per step instead of RCCL
 groups; the kernels, fold orders and halo plans above them are the ones the LOCAL communicator runs, so:
-- the single-launch (Chronopoulos-Gear) iteration on slab sub-meshes (one exchange step per iteration: the rank
-  triples and the r, w, s halos) equals the LOCAL solve of the same decomposition bit for bit;
-- so does the two-kernel FAST iteration on a global-mesh node partition (two steps per iteration);
+- the FAST iteration on structured slab sub-meshes (the lattice stencil; two exchange steps per iteration: p.Ap,
+  then {r.r, r.z} with the z halo) equals the LOCAL solve of the same decomposition bit for bit;
+- so does the FAST iteration on a global-mesh node partition (the fan-group tiles);
 - a PARITY solve over PEER is refused (its chunk-partial all-gathers stay on RCCL / LOCAL);
 - the exchange latency per step is measured (printed; DESIGN.md section 7 uses it). Two processes on one GPU
   share its CUs, so this is the protocol's latency on one device, not an xGMI figure."""
@@ -72,17 +72,17 @@ def _assemble(out, n):
 
 
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_peer_single_launch_slabs_equal_local(nranks):
+def test_peer_lattice_slabs_equal_local(nranks):
     shape = (13, 9, 4)
     spec = dict(slab=shape, tol=1e-6, max_iterations=800)
     out = _run(spec, nranks)
     glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
     x = _assemble(out, glob.packing.node_count)
     for d in out.values():
-        assert d["kernel"].startswith("k_cg_lattice"), d["kernel"]
+        assert d["kernel"].startswith("k_keff_lattice"), d["kernel"]
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
         assert d["parity_error"]  # refused (unaligned chunks or the FAST-only transport), never a hang
-    assert_bitwise(x, xl, "PEER single-launch x vs LOCAL")
+    assert_bitwise(x, xl, "PEER lattice slabs x vs LOCAL")
     ref = oracle_system(glob.packing, glob.materials, *glob.scalars()).solve_pcg(glob.static_rhs(), 800, 1e-6)
     assert tl.converged
     assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
@@ -90,7 +90,7 @@ def test_peer_single_launch_slabs_equal_local(nranks):
           + ", ".join(f"rank {k} {d['exchange_us']:.2f} us" for k, d in sorted(out.items())))
 
 
-def test_peer_two_kernel_iteration_equals_local():
+def test_peer_global_partition_equals_local():
     nranks = 2
     glob = scenarios.block_case(10, 6, 12, h=0.1, tol=1e-6, max_iterations=800)
     P = glob.packing
@@ -116,4 +116,4 @@ def test_peer_two_kernel_iteration_equals_local():
     comm.close()
     for d in out.values():
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
-    assert_bitwise(_assemble(out, P.node_count), xl.reshape(-1), "PEER two-kernel x vs LOCAL")
+    assert_bitwise(_assemble(out, P.node_count), xl.reshape(-1), "PEER global partition x vs LOCAL")

@@ -106,7 +106,7 @@ def run_rank(rank, nranks, uid, spec, queue):
 def run_rank_peer(rank, nranks, rdv, spec, queue):
     """One rank over the PEER communicator (peer.hip): the IPC handles of the ranks' mailboxes are exchanged through
     files in the rendezvous directory `rdv`. spec["slab"] = (nx, ny, nz per rank): the bench's slab sub-meshes
-    (structured block: the single-launch iteration unless spec["env"] switches it off); else spec["ranges"] over
+    (structured block: the lattice stencil); else spec["ranges"] over
     the global block. Returns the owned x, the telemetry, the exchange latency and the error of a PARITY solve."""
     try:
         import time
@@ -146,7 +146,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         comm.connect([open(os.path.join(rdv, f"rank{p}.bin"), "rb").read() for p in range(nranks)])
         kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
         x = np.zeros(3 * sh.local_nodes, np.float32)
-        res = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]), pcg.PcgVectors(x))
+        res = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]), pcg.PcgVectors(x, None))
         if not res.has_value():
             queue.put((rank, "error", str(res.error())))
             return
@@ -154,7 +154,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         us = shard.Comm.time_exchange(s, spec.get("timing_steps", 200))
         # PARITY over PEER is refused (its chunk-partial all-gathers need RCCL / LOCAL)
         _lib.load().cwf_hip_system_set_mode(s.handle(), _lib.MODE_PARITY)
-        pres = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, spec["tol"]), pcg.PcgVectors(np.zeros_like(x)))
+        pres = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, spec["tol"]), pcg.PcgVectors(np.zeros_like(x), None))
         perr = None if pres.has_value() else pres.error().message
         own = 3 * sh.owned_nodes
         queue.put((rank, "ok", dict(telemetry=(t.iterations, t.converged, t.residual_norm), kernel=kern,
