@@ -153,7 +153,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         t = res.value()
         us = shard.Comm.time_exchange(s, spec.get("timing_steps", 200))
         # PARITY over PEER is refused (its chunk-partial all-gathers need RCCL / LOCAL)
-        _lib.load().cwf_hip_system_set_mode(s.handle(), _lib.MODE_PARITY)
+        s.mode = _lib.MODE_PARITY  # (the handle takes the system's mode at every call)
         pres = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, spec["tol"]), pcg.PcgVectors(np.zeros_like(x), None))
         perr = None if pres.has_value() else pres.error().message
         own = 3 * sh.owned_nodes
