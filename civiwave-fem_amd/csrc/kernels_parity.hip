@@ -107,24 +107,53 @@ __device__ __forceinline__ void corner_force(double ax, double ay, double az, co
     f[2] = fz * vol;
 }
 
-// strain / stress of tet e from its record and the (optionally sanitised) corner values (pcg.cpp:574-640):
-// gradients g{x,y,z}[4] in fp64, stress sig[6]
+// a tet's operands: its record (corner ids, f32 gradients), the f32 corner values and (SANITIZE) the corners'
+// Dirichlet masks, its volume and material. Gathered first so a pipelined kernel can have them in flight while it
+// works on the previous tet (k_keff_parity_tile).
+template <bool SANITIZE>
+struct TetIn
+{
+    Grad G;
+    float u[12];
+    uint32_t mk[SANITIZE ? 4 : 1];
+    float vol;
+    uint32_t mat;
+};
+
+// the loads of the corner values (needs G.c) and of the volume and material
+template <bool SANITIZE>
+__device__ __forceinline__ void tet_gather(const DevSys &s, const float *__restrict__ x, uint32_t e, TetIn<SANITIZE> &t)
+{
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t m = t.G.c[q];
+        const float *xp = x + 3u * m;
+        t.u[3 * q + 0] = xp[0];
+        t.u[3 * q + 1] = xp[1];
+        t.u[3 * q + 2] = xp[2];
+        if constexpr (SANITIZE)
+            t.mk[q] = s.mask[m];
+    }
+    t.vol = s.vol[e];
+    t.mat = s.mat[e];
+}
+
+// strain / stress of a tet from its operands (pcg.cpp:574-640): gradients g{x,y,z}[4] in fp64, stress sig[6]
 template <bool ISO, bool SANITIZE>
-__device__ __forceinline__ void tet_stress(const DevSys &s, const Grad &G, const float *__restrict__ x,
-                                           const double *dtab, uint32_t mi, double gx[4], double gy[4], double gz[4],
-                                           double sig[6])
+__device__ __forceinline__ void tet_stress_in(const DevSys &s, const TetIn<SANITIZE> &t, const double *dtab,
+                                              double gx[4], double gy[4], double gz[4], double sig[6])
 {
     constexpr int kTab = ISO ? 12 : 36;
+    const uint32_t mi = t.mat;
     double u[12];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
     {
-        const uint32_t m = G.c[q];
-        const float *xp = x + 3u * m;
-        double u0 = (double)xp[0], u1 = (double)xp[1], u2 = (double)xp[2];
+        double u0 = (double)t.u[3 * q + 0], u1 = (double)t.u[3 * q + 1], u2 = (double)t.u[3 * q + 2];
         if constexpr (SANITIZE)
         {
-            const uint32_t mk = s.mask[m];
+            const uint32_t mk = t.mk[q];
             if (mk & 1u)
                 u0 = 0.0;
             if (mk & 2u)
@@ -139,9 +168,9 @@ __device__ __forceinline__ void tet_stress(const DevSys &s, const Grad &G, const
 #pragma unroll
     for (int q = 0; q < 4; ++q)
     {
-        gx[q] = (double)G.g[3 * q + 0];
-        gy[q] = (double)G.g[3 * q + 1];
-        gz[q] = (double)G.g[3 * q + 2];
+        gx[q] = (double)t.G.g[3 * q + 0];
+        gy[q] = (double)t.G.g[3 * q + 1];
+        gz[q] = (double)t.G.g[3 * q + 2];
     }
     double eps[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -162,14 +191,14 @@ __device__ __forceinline__ void tet_stress(const DevSys &s, const Grad &G, const
     else
     {
         double tab[36];
-        for (int t = 0; t < kTab; ++t)
+        for (int t2 = 0; t2 < kTab; ++t2)
         {
             uint32_t src;
             if constexpr (ISO)
-                src = t < 9 ? (t / 3) * 6 + (t % 3) : (t - 6) * 7;
+                src = t2 < 9 ? (t2 / 3) * 6 + (t2 % 3) : (t2 - 6) * 7;
             else
-                src = t;
-            tab[t] = s.dmat[36u * mi + src];
+                src = t2;
+            tab[t2] = s.dmat[36u * mi + src];
         }
         stress_fp64<ISO>(tab, eps, sig);
     }
@@ -250,6 +279,7 @@ __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint3
 // and read back by a node pass: 76 + 36 us on C2); round 2 gathered every incident tet per node (4x the element
 // work, 293 us).
 constexpr int kTileTets = 256;
+constexpr int kIncAhead = 4;  // a node's next incidence entries held in registers
 template <bool ISO, bool SANITIZE, bool DOT>
 __global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
                                                              float *__restrict__ y, const Ctl *__restrict__ ctl,
@@ -273,43 +303,86 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const flo
         j = s.off[n];
         jend = s.off[n + 1];
     }
-    uint32_t q = j < jend ? s.pinc[j] : 0xFFFFFFFFu;  // the node's next incidence: tile-local tet << 2 | corner
+    // the node's next kIncAhead incidence entries (tile-local tet << 2 | corner; ~0 past its last), refilled after
+    // each batch's fold so their loads are in flight during the next batch's element work
+    uint32_t qa[kIncAhead];
+#pragma unroll
+    for (int i = 0; i < kIncAhead; ++i)
+        qa[i] = j + i < jend ? s.pinc[j + i] : 0xFFFFFFFFu;
+    // software pipeline over batches: batch b's operands were gathered during batch b - 1; the next batch's record
+    // is issued before this batch's math and its corner gathers before the fold
+    const uint32_t tid = threadIdx.x;
+    TetIn<SANITIZE> cur;
+    uint32_t e_cur = tid < nt ? s.ptile_tets[t0 + tid] : 0u;
+    if (tid < nt)
+    {
+        load_erec(s.erec, e_cur, cur.G);
+        tet_gather<SANITIZE>(s, x, e_cur, cur);
+    }
+    uint32_t e_nxt = kTileTets + tid < nt ? s.ptile_tets[t0 + kTileTets + tid] : 0u;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     __syncthreads();  // dtab
     for (uint32_t base = 0; base < nt; base += kTileTets)
     {
-        if (base + threadIdx.x < nt)
+        const bool has_nxt = base + kTileTets + tid < nt;
+        TetIn<SANITIZE> nxt;
+        if (has_nxt)
+            load_erec(s.erec, e_nxt, nxt.G);
+        const uint32_t e_nn = base + 2 * kTileTets + tid < nt ? s.ptile_tets[t0 + base + 2 * kTileTets + tid] : 0u;
+        if (base + tid < nt)
         {
-            const uint32_t e = s.ptile_tets[t0 + base + threadIdx.x];
-            Grad G;
-            load_erec(s.erec, e, G);
             double gx[4], gy[4], gz[4], sig[6];
-            tet_stress<ISO, SANITIZE>(s, G, x, dtab, s.mat[e], gx, gy, gz, sig);
-            const double vol = (double)s.vol[e] * s.sK;  // pcg.cpp:642
+            tet_stress_in<ISO, SANITIZE>(s, cur, dtab, gx, gy, gz, sig);
+            const double vol = (double)cur.vol * s.sK;  // pcg.cpp:642
 #pragma unroll
             for (int a = 0; a < 4; ++a)
-                if (G.c[a] - n0 < (uint32_t)kBlock)  // a corner of this tile
+                if (cur.G.c[a] - n0 < (uint32_t)kBlock)  // a corner of this tile
                 {
                     double f[3];
                     corner_force(gx[a], gy[a], gz[a], sig, vol, f);
-                    const uint32_t sl = 4u * threadIdx.x + (uint32_t)a;
+                    const uint32_t sl = 4u * tid + (uint32_t)a;
                     fs[0][sl] = f[0];
                     fs[1][sl] = f[1];
                     fs[2][sl] = f[2];
                 }
         }
+        if (has_nxt)
+            tet_gather<SANITIZE>(s, x, e_nxt, nxt);
         __syncthreads();
+        // incidences are ascending in element order, so in tile-local tet order: the node's entries below lim are
+        // this batch's, consumed in order
         const uint32_t lim = (base + kTileTets) << 2;
-        while (q < lim)  // incidences are ascending in element order, so in tile-local tet order
+        int used = 0;
+#pragma unroll
+        for (int i = 0; i < kIncAhead; ++i)
+            if (qa[i] < lim && used == i)
+            {
+                const uint32_t sl = qa[i] - (base << 2);
+                acc0 += fs[0][sl];
+                acc1 += fs[1][sl];
+                acc2 += fs[2][sl];
+                ++used;
+            }
+        j += (uint32_t)used;
+        if (used == kIncAhead)  // more in this batch than the register window holds (rare): straight from memory
         {
-            const uint32_t sl = q - (base << 2);
-            acc0 += fs[0][sl];
-            acc1 += fs[1][sl];
-            acc2 += fs[2][sl];
-            ++j;
-            q = j < jend ? s.pinc[j] : 0xFFFFFFFFu;
+            uint32_t q = j < jend ? s.pinc[j] : 0xFFFFFFFFu;
+            while (q < lim)
+            {
+                const uint32_t sl = q - (base << 2);
+                acc0 += fs[0][sl];
+                acc1 += fs[1][sl];
+                acc2 += fs[2][sl];
+                ++j;
+                q = j < jend ? s.pinc[j] : 0xFFFFFFFFu;
+            }
         }
+#pragma unroll
+        for (int i = 0; i < kIncAhead; ++i)
+            qa[i] = j + i < jend ? s.pinc[j + i] : 0xFFFFFFFFu;
         __syncthreads();
+        cur = nxt;
+        e_nxt = e_nn;
     }
     float yv[3] = {0.f, 0.f, 0.f}, xv[3] = {0.f, 0.f, 0.f};
     if (n < s.N)
@@ -341,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const flo
     }
     if constexpr (DOT)
     {
-        // the tile's chunks are 3 tile, 3 tile + 1, 3 tile + 2 (wg_chunk_partials reads blockIdx.x: pass the tile)
+        // the tile's chunks are 3 tile, 3 tile + 1, 3 tile + 2
         const bool own = n < nlim;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
