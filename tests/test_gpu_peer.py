@@ -74,7 +74,7 @@ def _assemble(out, n):
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_peer_lattice_slabs_equal_local(nranks):
     shape = (13, 9, 4)
-    spec = dict(slab=shape, tol=1e-6, max_iterations=800)
+    spec = dict(slab=shape, tol=1e-6, max_iterations=800, timing_steps=1000)
     out = _run(spec, nranks)
     glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
     x = _assemble(out, glob.packing.node_count)
