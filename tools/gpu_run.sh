@@ -16,6 +16,8 @@
 #   sq:NAME[:ARGS]          the SQ counter pass of the same (tools/profile.sh SQ_PMC=1)
 #   calib                   FETCH_SIZE / WRITE_SIZE against known byte counts (tools/pmc_calib, built in-tree
 #                           beforehand) -> <TAG>_calib.json
+#   peer                    the PEER communicator's tests with their exchange-latency prints (2 / 3 processes on
+#                           this GPU) -> <TAG>/peer.log
 # e.g. bash tools/gpu_run.sh r04c tests:tests/test_gpu_lattice.py bench:c2 bench:c3:--config,c3,--steps,3 \
 #        ab:c2cg:CWF_LAT_CG=0 prof:c3:--config,c3,--steps,2,--warmup,1,--no-cpu-baseline
 set -o pipefail
@@ -77,6 +79,10 @@ for step in "$@"; do
        timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $C/write -o write -- $R/tools/pmc_calib > /dev/null) || exit 4
       python3 tools/pmc_calib.py $C > $O/calib.txt && cp $C/calib.json $O/calib.json && cat $O/calib.txt || exit 4
       rm -rf $C ;;
+    peer)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_peer.py -m gpu -s -q --timeout 280 --timeout-method thread \
+        > $O/peer.log 2>&1 || { tail -30 $O/peer.log; exit 5; }
+      grep -E "PEER exchange|passed|failed" $O/peer.log ;;
     *) echo "unknown step $step"; exit 64 ;;
   esac
 done
