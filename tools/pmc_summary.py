@@ -24,6 +24,13 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def norm(k):
+    """'cwf::k<1, cwf::LatKuhn>' and 'k<1, LatKuhn>' alike: namespaces off the name and its template arguments."""
+    k = k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].replace(" ", "")
+    base, _, args = k.partition("<")
+    return base.split("::")[-1] + "<" + ",".join(x.split("::")[-1] for x in args.rstrip(">").split(",")) + ">"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -50,7 +57,7 @@ def main():
                           hbm_bytes_per_launch=(rd + wr) if rd is not None and wr is not None else None,
                           hbm_gbs=bw)
     if a.json:
-        sel = {k: v for k, v in out.items() if not a.kernel or any(s in k for s in a.kernel)}
+        sel = {k: v for k, v in out.items() if not a.kernel or any(s in k or norm(s) == norm(k) for s in a.kernel)}
         total = sum(v["hbm_bytes_per_launch"] or 0 for v in sel.values())
         json.dump(dict(kernels=sel, hbm_bytes_per_launch=total,
                        note="FETCH_SIZE x2 x1024 + WRITE_SIZE x1024 per launch, summed over the selected "
