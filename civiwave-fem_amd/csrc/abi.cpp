@@ -686,6 +686,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.lk0 = 0;
         t.lk1 = lat.nz;
         t.lplane = dpl;
+        t.lpstride = lat.nx * lat.ny;
+        for (uint32_t k = 0; k < lat.nz; ++k)
+            if (lat.plane[k] != k * t.lpstride)
+                t.lpstride = 0;
         t.lcoef = dcf;
         t.lsym = lat.sym ? 1 : 0;
         t.lhex = lat.hex ? 1 : 0;
@@ -751,6 +755,10 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     return bail(st);
                 if (int st = dalloc(h, &dci9, 9 * kLatClasses))
                     return bail(st);
+                float4 *dcz;
+                if (int st = dalloc(h, &dcz, 2 * kLatClasses))
+                    return bail(st);
+                HIPTRY(h, hipMemset(dcz, 0, 2 * kLatClasses * sizeof(float4)));
                 // classes without a node keep zero inverses (k_lat_class_inverse fills only represented ones; halo
                 // lanes of the z-from-r and single-launch passes may read any class)
                 HIPTRY(h, hipMemset(dci6, 0, kLatClasses * sizeof(uint4)));
@@ -759,6 +767,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                 t.lrep = drep;
                 t.lcinv6 = dci6;
                 t.lcinv9 = dci9;
+                t.lcz = dcz;
             }
         }
         h->lat_plane.swap(lat.plane);

@@ -129,12 +129,12 @@ int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_
     const size_t nv = vecs.empty() ? 0 : vecs[0].size();
     if (nv > kMaxHaloVecs)
         return set_error(h0, CWF_ERR_ARGUMENT, "too many halo vectors in one exchange");
+    const bool gather = h0->nranks > 1;
+    if (h0->comm && h0->comm->kind == 2)  // PEER: one launch that gathers its send rows from the vectors itself
+        return (gather || nv) ? peer_exchange(h0, gathers, vecs.empty() ? std::vector<float *>{} : vecs[0]) : 0;
     for (size_t i = 0; i < g.size(); ++i)  // vector j's send segment at sendbuf + 3 nsend j
         for (size_t j = 0; j < nv; ++j)
             halo_pack(g[i], vecs[i][j], g[i]->stream, g[i]->sendbuf + 3 * g[i]->nsend * j);
-    const bool gather = h0->nranks > 1;
-    if (h0->comm && h0->comm->kind == 2)
-        return (gather || nv) ? peer_exchange(h0, gathers, vecs.empty() ? std::vector<float *>{} : vecs[0]) : 0;
     if (h0->comm && h0->comm->kind == 1)
     {
         if (!gather && !nv)

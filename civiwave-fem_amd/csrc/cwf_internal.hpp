@@ -96,6 +96,8 @@ struct DevTiles
                                          // stores no z, the K_eff pass forms it from r and the node's class
     float lmass = 0.f;
     const uint32_t *lplane = nullptr;    // [lnz] storage index of node (0, 0, k)
+    uint32_t lpstride = 0;               // plane[k] == k lpstride for every k (the kernels then skip the plane[] load
+                                         // in front of every plane's first gather); 0: read plane[]
     const float *lcoef = nullptr;        // [kLatCoef] stencil, cell-pair and face blocks (unscaled by s_K)
     int lsym = 0;                        // S_(-d) == S_d: the paired-direction instantiation
     int lhex = 0;                        // native hex8 cells: the 27-point instantiation
@@ -106,6 +108,8 @@ struct DevTiles
     const uint32_t *lrep = nullptr;  // [kLatClasses], 0xFFFFFFFF: no node of the class
     uint4 *lcinv6 = nullptr;         // [kLatClasses]
     float *lcinv9 = nullptr;         // [9 kLatClasses]
+    float4 *lcz = nullptr;           // [2 kLatClasses] the same inverse unpacked, {a00 a01 a02 a11} {a12 a22 0 0}:
+                                     // loaded unconditionally in the K_eff prologue (lattice.inc, ZR)
 };
 // lattice work items for planes [lk0, lk1) (lattice.cpp): sets lnbx, lnby, lL, lnwork, ntiles
 void lattice_plan(DevTiles &t);

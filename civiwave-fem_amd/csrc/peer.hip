@@ -1,17 +1,21 @@
 // peer.hip -- the PEER communicator: device-initiated exchange steps over IPC-mapped mailboxes (SURVEY.md 8e,
 // VERDICT r3 item 4). One process per rank, as RCCL; an exchange step (the all-gathers of per-rank scalar slots
-// and the halos of up to three vectors, comm_exchange_vecs) is three launches on the rank's stream instead of an
-// RCCL group:
+// and the halos of up to three vectors, comm_exchange_vecs) is ONE launch on the rank's stream instead of an RCCL
+// group, k_peer_step, in three phases:
 //
-//   k_peer_push    every workgroup stores its share of the packed send segments straight into the neighbours'
-//                  mailboxes (remote stores over xGMI; the same device's memory under IPC on one GPU) and
-//                  workgroup 0 this rank's scalar slots into every peer's; each workgroup releases at system
-//                  scope and takes a ticket; the last one stores the step's epoch into every peer's flag for
-//                  this rank (system-scope atomic store);
-//   k_peer_wait    one wave polls this rank's flags, one lane per peer, until every peer has reached the epoch
-//                  (bounded: a peer that never arrives ends the solve with CWF_ERR_COMM instead of a hang), then
-//                  acquires at system scope;
-//   k_peer_unpack  the received ghost rows and scalar slots into their vectors / slots (system-scope loads).
+//   push    every workgroup gathers its share of the send rows straight from the vectors (send_idx: no pack pass)
+//           and stores them into the neighbours' mailboxes (remote stores over xGMI; the same device's memory under
+//           IPC on one GPU), workgroup 0 this rank's scalar slots into every peer's; each workgroup releases at
+//           system scope and takes a ticket; the last one stores the step's epoch into every peer's flag for this
+//           rank (system-scope atomic store);
+//   wait    every workgroup polls this rank's flags, one lane per peer, until every peer has reached the epoch
+//           (bounded: a peer that never arrives ends the solve with CWF_ERR_COMM instead of a hang), then acquires
+//           at system scope;
+//   unpack  its share of the received ghost rows and scalar slots into their vectors / slots (system-scope loads).
+//
+// Workgroups wait for peers, not for each other, and the grid is small (<= 128 workgroups of 256 threads, resident
+// together), so every workgroup reaches its ticket. Round 4's first form was three launches (push, wait, unpack)
+// after the pack pass: 13.7 us per step between two processes on one GPU (profiles/r04ev_peer.log).
 //
 // A mailbox (one hipMalloc per rank, exported with hipIpcGetMemHandle) is a header with the rank's receive layout
 // (where each neighbour's ghosts go, read once by the peers at connect), one 64-B flag line per peer, and two
@@ -57,35 +61,50 @@ inline size_t gath_bytes(int n) { return (size_t)kMaxPeerGathers * n * kSlot * s
 inline size_t off_recv(int n) { return align256(off_gath(n) + 2 * gath_bytes(n)); }
 inline size_t recv_bytes(uint64_t nghost) { return kMaxHaloVecs * 3 * nghost * sizeof(float); }  // one parity
 
-struct PeerPush
+struct PeerStep
 {
-    const float *send;  // [nv][3 nsend] packed segments
-    uint64_t nsend;
+    // push
+    const float *vec[kMaxHaloVecs];  // the halo vectors (node-interleaved, 3 floats per node)
+    const uint32_t *send_idx;        // [nsend] owned local node ids, neighbour k's at src_off[k] ..
     uint32_t nv, nnbr;
-    float *dst[kMaxPeers];       // per neighbour k: its receive area (this parity), my ghosts' first float
+    float *dst[kMaxPeers];            // per neighbour k: its receive area (this parity), my ghosts' first float
     uint64_t dst_vstride[kMaxPeers];  // floats between vectors there (3 nghost of the neighbour)
     uint64_t src_off[kMaxPeers], cnt[kMaxPeers];  // my send segment for k (nodes)
-    uint64_t total;              // sum over k of 3 cnt
+    uint64_t total;                   // sum over k of cnt (nodes)
     uint32_t ng, gcount[kMaxPeerGathers];
     const double *gsrc[kMaxPeerGathers];  // my slot of gather q
-    double *gdst[kMaxPeers];     // per rank p: p's gather area (this parity), my slot of gather 0
-    uint32_t *flag[kMaxPeers];   // per rank p: p's flag line for my rank
+    double *gdst[kMaxPeers];          // per rank p: p's gather area (this parity), my slot of gather 0
+    uint32_t *flag[kMaxPeers];        // per rank p: p's flag line for my rank
     uint32_t nranks, rank, epoch;
     uint32_t *cnt_ticket;
+    // wait
+    const uint32_t *flags;  // my mailbox's flag lines
+    Ctl *ctl;
+    // unpack
+    const float *recv;        // this parity's receive area
+    uint64_t nghost, ghost0;  // ghosts are local nodes ghost0 .. ghost0 + nghost
+    float *out[kMaxHaloVecs];
+    const double *gath;  // this parity's gather area
+    double *gbuf[kMaxPeerGathers];
 };
 
-__global__ __launch_bounds__(256) void k_peer_push(PeerPush a)
+__global__ __launch_bounds__(256) void k_peer_step(PeerStep a)
 {
-    // halo rows: item t of the flattened (neighbour, vector, float) space, workgroup-strided
+    // (1) push: node item t of the flattened (vector, neighbour, node) space, workgroup-strided
     const uint64_t items = a.total * a.nv;
     for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < items; t += (uint64_t)gridDim.x * 256)
     {
         uint64_t r = t % a.total;
         const uint32_t v = (uint32_t)(t / a.total);
         uint32_t k = 0;
-        while (k + 1 < a.nnbr && r >= 3 * a.cnt[k])
-            r -= 3 * a.cnt[k++];
-        a.dst[k][a.dst_vstride[k] * v + r] = a.send[3 * (a.nsend * v + a.src_off[k]) + r];
+        while (k + 1 < a.nnbr && r >= a.cnt[k])
+            r -= a.cnt[k++];
+        const float *src = a.vec[v] + 3ull * a.send_idx[a.src_off[k] + r];
+        float *d = a.dst[k] + a.dst_vstride[k] * v + 3 * r;
+        const float x0 = src[0], x1 = src[1], x2 = src[2];
+        d[0] = x0;
+        d[1] = x1;
+        d[2] = x2;
     }
     if (blockIdx.x == 0 && threadIdx.x < a.nranks * kMaxPeerGathers * kSlot)
     {
@@ -110,66 +129,57 @@ __global__ __launch_bounds__(256) void k_peer_push(PeerPush a)
             __hip_atomic_store(a.cnt_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-}
-
-// one wave; lane p polls this rank's flag line of peer p
-__global__ __launch_bounds__(64) void k_peer_wait(const uint32_t *flags, uint32_t nranks, uint32_t rank, uint32_t epoch,
-                                                  Ctl *ctl)
-{
-    const uint32_t p = threadIdx.x;
-    bool ok = true;
-    if (p < nranks && p != rank)
+    // (2) wait: wave 0, lane p polls peer p's flag line
+    __shared__ int ok_s;
+    if (threadIdx.x < 64)
     {
-        const uint32_t *f = flags + (kFlagLine / 4) * p;
-        uint32_t spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch)
+        const uint32_t p = threadIdx.x;
+        bool ok = true;
+        if (p < a.nranks && p != a.rank)
         {
-            __builtin_amdgcn_s_sleep(8);
-            if (++spins > (1u << 24))  // ~seconds: the peer is gone
+            const uint32_t *f = a.flags + (kFlagLine / 4) * p;
+            uint32_t spins = 0;
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch)
             {
-                ok = false;
-                break;
+                __builtin_amdgcn_s_sleep(4);
+                if (++spins > (1u << 24))  // ~seconds: the peer is gone
+                {
+                    ok = false;
+                    break;
+                }
             }
         }
+        const bool all = __all(ok);
+        if (threadIdx.x == 0)
+            ok_s = all ? 1 : 0;
     }
-    if (!__all(ok) && threadIdx.x == 0)
+    __syncthreads();
+    if (!ok_s)
     {
-        ctl->error = CWF_ERR_COMM;
-        ctl->error_iter = (int)epoch;
-        ctl->active = 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+        {
+            a.ctl->error = CWF_ERR_COMM;
+            a.ctl->error_iter = (int)a.epoch;
+            a.ctl->active = 0;
+        }
+        return;
     }
     __threadfence_system();
-}
-
-struct PeerUnpack
-{
-    const float *recv;  // this parity's receive area
-    uint64_t nghost, ghost0;  // ghosts are local nodes ghost0 .. ghost0 + nghost
-    uint32_t nv;
-    float *vec[kMaxHaloVecs];
-    const double *gath;  // this parity's gather area
-    uint32_t ng, gcount[kMaxPeerGathers], nranks, rank;
-    double *gbuf[kMaxPeerGathers];
-};
-
-__global__ __launch_bounds__(256) void k_peer_unpack(PeerUnpack a)
-{
+    // (3) unpack
     const uint64_t per = 3 * a.nghost;
     for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < per * a.nv; t += (uint64_t)gridDim.x * 256)
     {
         const uint32_t v = (uint32_t)(t / per);
         const uint64_t i = t % per;
-        a.vec[v][3 * a.ghost0 + i] =
-            __hip_atomic_load(a.recv + per * v + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        a.out[v][3 * a.ghost0 + i] = __hip_atomic_load(a.recv + per * v + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (blockIdx.x == 0 && threadIdx.x < a.nranks * kMaxPeerGathers * kSlot)
     {
         const uint32_t p = threadIdx.x / (kMaxPeerGathers * kSlot), q = (threadIdx.x / kSlot) % kMaxPeerGathers,
                        j = threadIdx.x % kSlot;
         if (p != a.rank && q < a.ng && j < a.gcount[q])
-            a.gbuf[q][(size_t)p * a.gcount[q] + j] =
-                __hip_atomic_load(a.gath + ((size_t)q * a.nranks + p) * kSlot + j, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_SYSTEM);
+            a.gbuf[q][(size_t)p * a.gcount[q] + j] = __hip_atomic_load(a.gath + ((size_t)q * a.nranks + p) * kSlot + j,
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -233,10 +243,11 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
                              "PARITY's chunk-partial all-gathers need RCCL or LOCAL");
     const uint32_t epoch = ++cm->epoch;
     const uint32_t par = epoch & 1u;
-    PeerPush a{};
-    a.send = h->sendbuf;
-    a.nsend = h->nsend;
+    PeerStep a{};
+    a.send_idx = h->send_idx;
     a.nv = (uint32_t)vecs.size();
+    for (size_t v = 0; v < vecs.size(); ++v)
+        a.vec[v] = a.out[v] = vecs[v];
     a.nnbr = (uint32_t)h->nbr.size();
     for (uint32_t k = 0; k < a.nnbr; ++k)
     {
@@ -247,13 +258,14 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
         a.dst_vstride[k] = 3 * qg;
         a.src_off[k] = h->send_off[k];
         a.cnt[k] = h->send_off[k + 1] - h->send_off[k];
-        a.total += 3 * a.cnt[k];
+        a.total += a.cnt[k];
     }
     a.ng = 0;
     for (const Gather &q : gathers)
     {
         a.gcount[a.ng] = (uint32_t)q.count;
         a.gsrc[a.ng] = h->*(q.buf) + (size_t)h->rank * q.count;
+        a.gbuf[a.ng] = h->*(q.buf);
         ++a.ng;
     }
     for (int p = 0; p < n; ++p)
@@ -266,32 +278,17 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
     a.rank = (uint32_t)h->rank;
     a.epoch = epoch;
     a.cnt_ticket = cm->ticket;
-    // (comm_exchange_vecs packed the send segments on this stream)
-    const uint64_t items = a.total * a.nv;
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((items + 1023) / 1024, 256));
-    k_peer_push<<<grid, 256, 0, h->stream>>>(a);
-    k_peer_wait<<<1, 64, 0, h->stream>>>(reinterpret_cast<const uint32_t *>(static_cast<char *>(cm->mbox) + off_flags()),
-                                         (uint32_t)n, (uint32_t)h->rank, epoch, h->ctl);
-    PeerUnpack u{};
+    a.flags = reinterpret_cast<const uint32_t *>(static_cast<char *>(cm->mbox) + off_flags());
+    a.ctl = h->ctl;
     const uint64_t nghost = h->ds.N - h->ds.Nown;
-    u.recv = reinterpret_cast<const float *>(static_cast<char *>(cm->mbox) + off_recv(n) + par * recv_bytes(nghost));
-    u.nghost = nghost;
-    u.ghost0 = h->ds.Nown;
-    u.nv = (uint32_t)vecs.size();
-    for (size_t v = 0; v < vecs.size(); ++v)
-        u.vec[v] = vecs[v];
-    u.gath = reinterpret_cast<const double *>(static_cast<char *>(cm->mbox) + off_gath(n) + par * gath_bytes(n));
-    u.ng = a.ng;
-    for (uint32_t q = 0; q < a.ng; ++q)
-    {
-        u.gcount[q] = a.gcount[q];
-        u.gbuf[q] = h->*(gathers.begin()[q].buf);
-    }
-    u.nranks = (uint32_t)n;
-    u.rank = (uint32_t)h->rank;
-    const uint64_t uitems = 3 * nghost * u.nv;
-    const unsigned ugrid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uitems + 1023) / 1024, 256));
-    k_peer_unpack<<<ugrid, 256, 0, h->stream>>>(u);
+    a.recv = reinterpret_cast<const float *>(static_cast<char *>(cm->mbox) + off_recv(n) + par * recv_bytes(nghost));
+    a.nghost = nghost;
+    a.ghost0 = h->ds.Nown;
+    a.gath = reinterpret_cast<const double *>(static_cast<char *>(cm->mbox) + off_gath(n) + par * gath_bytes(n));
+    // one workgroup per 256 pushed nodes or 1024 unpacked floats, <= 128 (all resident: every one reaches its ticket)
+    const uint64_t work = std::max<uint64_t>((a.total * a.nv + 255) / 256, (3 * nghost * a.nv + 1023) / 1024);
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(work, 128));
+    k_peer_step<<<grid, 256, 0, h->stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(h, e, "peer exchange launch");
 }

@@ -38,12 +38,31 @@ constexpr int kMaxM = 16;
 #endif
 constexpr int kUpdThreads = CWF_UPD_THREADS;  // update-pass workgroup size (its per-workgroup shares are refolded by every consumer workgroup)
 constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
+// fp64 lane exchange through DPP (both halves): CTRL is a GFX9 dpp_ctrl
+template <int CTRL> __device__ __forceinline__ double dpp_f64(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int lane)
+{
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                            __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+// Wave sum in a fixed order, the same value in every lane (all 64 lanes active). Inside each 16-lane row a butterfly
+// through DPP: quad_perm xor 1, xor 2, then row_half_mirror and row_mirror, which act as xor 4 and xor 8 on values
+// already uniform over quads / half-rows; each lane adds the same two operands (a + b == b + a bitwise), so every
+// lane of a row holds the same row sum. Then ((row0 + row1) + row2) + row3 from readlanes. The ds_bpermute butterfly
+// it replaces (__shfl_xor, six LDS-routed rounds of two 32-bit permutes) sat on the critical path of every consumer
+// prologue's scalar fold and every producer's share.
 __device__ __forceinline__ double wave_sum(double v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_f64<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += dpp_f64<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+    v += dpp_f64<0x140>(v);  // row_mirror
+    return ((lane_f64(v, 0) + lane_f64(v, 16)) + lane_f64(v, 32)) + lane_f64(v, 48);
 }
 
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
@@ -82,6 +101,29 @@ template <int NT> __device__ __forceinline__ double block_sum(double v, double *
         t += red[w];
     __syncthreads();
     return t;
+}
+
+// the pair {a, b} in one pass (one LDS round, two barriers); red: 2 NT / 64 doubles
+template <int NT> __device__ __forceinline__ void block_sum2(double a, double b, double *red, double &ta, double &tb)
+{
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if ((threadIdx.x & 63) == 0)
+    {
+        red[2 * (threadIdx.x >> 6)] = a;
+        red[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    double x = 0.0, y = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w)
+    {
+        x += red[2 * w];
+        y += red[2 * w + 1];
+    }
+    __syncthreads();
+    ta = x;
+    tb = y;
 }
 
 template <int NT>
@@ -156,25 +198,58 @@ __device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const d
     tb = b;
 }
 
+// Control-block words as vector (buffer) loads. A consumer prologue issues them with its gathers and the scalar
+// fold's loads, and they return with those: one memory round trip. As scalar loads they cost one of their own, in
+// front of the fold's loads (every s_waitcnt lgkmcnt(0) for a kernel argument the fold needs waits for them) or
+// after the fold (where their value is used).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ctl_rsrc(const Ctl *c)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<Ctl *>(c), 0, (int)sizeof(Ctl), 0x00020000);
+}
+__device__ __forceinline__ double ctl_f64(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0),
+                   hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4u, 0, 0);
+    return __hiloint2double((int)hi, (int)lo);
+}
+// what residual_step reads of the control block for iteration it >= 1
+struct CtlPre
+{
+    int active;
+    double rho_old, tol;  // rho2[(it - 1) & 1], tol
+};
+__device__ __forceinline__ CtlPre ctl_prefetch(const Ctl *ctl, unsigned it)
+{
+    const __amdgpu_buffer_rsrc_t rs = ctl_rsrc(ctl);
+    CtlPre p;
+    p.active = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)offsetof(Ctl, active), 0, 0);
+    p.rho_old = ctl_f64(rs, (uint32_t)(offsetof(Ctl, rho2) + 8u * ((it - 1u) & 1u)));
+    p.tol = ctl_f64(rs, (uint32_t)offsetof(Ctl, tol));
+    return p;
+}
+
 // pcg.cpp:862-895 for iteration `it` >= 1 from the update kernel's r.r / r.z shares (stride 1), or
 // from the all-gathered per-rank {r.r, r.z} pairs of a sharded system (stride 2, rank order).
-// Returns false when the solve is over (converged or rho breakdown); *beta_out = beta for this iteration.
+// Returns false when the solve is over (converged or rho breakdown); *beta_out = beta for this iteration. pre: the
+// control words prefetched by the caller (ctl_prefetch); then !pre->active (tested after the fold) also returns false.
 template <int NT>
 __device__ __forceinline__ bool residual_step(Ctl *ctl, const double *__restrict__ prr, const double *__restrict__ prz,
                                               unsigned nparts, unsigned stride, unsigned it,
                                               double *__restrict__ hist, double *red, float *beta_out,
-                                              bool dry = false)
+                                              bool dry = false, const CtlPre *pre = nullptr)
 {
     if (it == 0)
     {
         *beta_out = 0.f;
-        return true;
+        return pre ? pre->active != 0 : true;
     }
     double rr, rz;
     fold_all2<NT>(prr, prz, nparts, red, stride, rr, rz);
+    if (pre && !pre->active)
+        return false;
     const double res = sqrt(rr);
-    const double rho_old = ctl->rho2[(it - 1) & 1u];
-    const bool conv = res <= ctl->tol;
+    const double rho_old = pre ? pre->rho_old : ctl->rho2[(it - 1) & 1u];
+    const bool conv = res <= (pre ? pre->tol : ctl->tol);
     const bool err = !conv && fabs(rho_old) < 1.0e-18;
     const double beta = (conv || err) ? 0.0 : rz / rho_old;
     if (dry)  // diagnostic timing: full work, no side effects
@@ -1401,16 +1476,39 @@ __global__ __launch_bounds__(256) void k_sym_inverse(uint32_t N, const uint32_t 
 // of each class (every node of a class has the same diagonal blocks and mass: lattice.cpp)
 __global__ __launch_bounds__(256) void k_lat_class_inverse(const uint32_t *__restrict__ rep,
                                                            const float *__restrict__ inv6, const float *__restrict__ inv9,
-                                                           uint4 *__restrict__ cinv6, float *__restrict__ cinv9)
+                                                           uint4 *__restrict__ cinv6, float *__restrict__ cinv9,
+                                                           float4 *__restrict__ cz)
 {
     for (uint32_t c = threadIdx.x; c < kLatClasses; c += 256)
     {
         const uint32_t n = rep[c];
         if (n == 0xFFFFFFFFu)
             continue;
-        cinv6[c] = reinterpret_cast<const uint4 *>(inv6)[n];
+        const uint4 iw = reinterpret_cast<const uint4 *>(inv6)[n];
+        float a9[9];
         for (int q = 0; q < 9; ++q)
-            cinv9[9 * c + q] = inv9[9ull * n + q];
+            a9[q] = inv9[9ull * n + q];
+        cinv6[c] = iw;
+        for (int q = 0; q < 9; ++q)
+            cinv9[9 * c + q] = a9[q];
+        // the operator k_pcg_update_tiles applies (its unpack, or the flagged block's fp32 copy)
+        float bv[6];
+        if ((int)iw.x >= 0)
+            unpack_block_inverse(iw.y, iw.z, iw.w, __uint_as_float(iw.x), bv);
+        else
+        {
+            bv[0] = a9[0];
+            bv[1] = a9[1];
+            bv[2] = a9[2];
+            bv[3] = a9[4];
+            bv[4] = a9[5];
+            bv[5] = a9[8];
+        }
+        if (cz)
+        {
+            cz[2 * c] = float4{bv[0], bv[1], bv[2], bv[3]};
+            cz[2 * c + 1] = float4{bv[4], bv[5], 0.f, 0.f};
+        }
     }
 }
 
@@ -1480,18 +1578,12 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     float *__restrict__ pnew, Ctl *__restrict__ ctl, const double *__restrict__ part_dot, unsigned ntp,
     double *__restrict__ prr, double *__restrict__ prz, unsigned it, int wt, PBufs pbuf, unsigned lag)
 {
-    __shared__ double red[kUpdThreads / 64];
+    __shared__ double red[2 * (kUpdThreads / 64)];
     __shared__ uint4 cinv[LAT ? kLatClasses : 1];
-    if (!ctl->active)
-        return;
     const DevTiles &T = s.t;
-    if constexpr (LAT)  // structured block: the packed block inverse of each (boundary class, mask), lattice.cpp
-    {
-        for (uint32_t c = threadIdx.x; c < kLatClasses; c += kUpdThreads)
-            cinv[c] = T.lcinv6[c];
-        __syncthreads();
-    }
-    const float beta = (float)ctl->beta;  // this iteration's (the tiles kernel's residual step wrote it)
+    const __amdgpu_buffer_rsrc_t rctl = ctl_rsrc(ctl);
+    // this iteration's beta (the K_eff kernel's residual step wrote it), as a vector load like every control word here
+    const float beta = (float)ctl_f64(rctl, (uint32_t)offsetof(Ctl, beta));
     const float sM = (float)s.sM;
     const __amdgpu_buffer_rsrc_t rpart = whole_rsrc(T.part);
     // XF: this iteration applies the lazy x update (a separate instantiation, so the three iterations in four
@@ -1573,8 +1665,30 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     };
     if (base < s.Nown)
         load_nodes(base);
+    // LAT (structured block): the packed block inverse of each (boundary class, mask), lattice.cpp; thread c loads
+    // class c's with the node loads in flight (one prologue round trip for the nodes, the class table, the control
+    // block and the p.Ap shares, instead of three)
+    static_assert(!LAT || kLatClasses <= kUpdThreads, "one class per thread");
+    uint4 cw = {0u, 0u, 0u, 0u};
+    if constexpr (LAT)
+        cw = T.lcinv6[min((uint32_t)threadIdx.x, kLatClasses - 1u)];
+    // control words (ctl_rsrc): the flag, rho and the lazy-x alphas, in flight with the node loads and the fold's
+    const int active = (int)__builtin_amdgcn_raw_buffer_load_b32(rctl, (uint32_t)offsetof(Ctl, active), 0, 0);
+    const double rho = ctl_f64(rctl, (uint32_t)(offsetof(Ctl, rho2) + 8u * (it & 1u)));
+    double ah[kXLag];
+#pragma unroll
+    for (unsigned j = 0; j < kXLag; ++j)
+        ah[j] = xflush ? ctl_f64(rctl, (uint32_t)(offsetof(Ctl, alpha_h) + 8u * j)) : 0.0;
     // pcg.cpp:840-852: alpha = rho / (p . Ap)
     const double denom = fold_all<kUpdThreads>(part_dot, ntp, red);
+    if (!active)
+        return;
+    if constexpr (LAT)
+    {
+        if (threadIdx.x < kLatClasses)
+            cinv[threadIdx.x] = cw;
+        __syncthreads();
+    }
     if (fabs(denom) < 1.0e-18)
     {
         if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1586,7 +1700,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         }
         return;
     }
-    const double alpha_d = ctl->rho2[it & 1u] / denom;
+    const double alpha_d = rho / denom;
     if (blockIdx.x == 0 && threadIdx.x == 0)
     {
         ctl->denom = denom;
@@ -1599,7 +1713,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     for (unsigned j = 0; j < kXLag; ++j)
     {
         const unsigned ij = it + 1u - lag + j;
-        aj[j] = j < lag ? (float)(ij == it ? alpha_d : ctl->alpha_h[ij % kXLag]) : 0.f;
+        aj[j] = j < lag ? (float)(ij == it ? alpha_d : ah[ij % kXLag]) : 0.f;
     }
     const float alpha = (float)alpha_d;
     double rr = 0.0, rz = 0.0;
@@ -1718,8 +1832,8 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
         for (int k = 0; k < 3; ++k)
             pnew[3u * n + k] = fmaf(beta, pold[3u * n + k], z[3u * n + k]);
     }
-    const double t0 = block_sum<kUpdThreads>(rr, red);
-    const double t1 = block_sum<kUpdThreads>(rz, red);
+    double t0, t1;
+    block_sum2<kUpdThreads>(rr, rz, red, t0, t1);
     if (threadIdx.x == 0)
     {
         prr[blockIdx.x] = t0;
@@ -2082,7 +2196,8 @@ void fast_block_inverse(cwf_hip_system *h, hipStream_t st)
     if (h->ds.N)
         k_sym_inverse<<<grid_for(h->ds.N, 256), 256, 0, st>>>(h->ds.N, h->ds.mask, h->inv, h->inv6);
     if (h->ds.t.lcls)  // structured block: one representative node per (boundary class, mask)
-        k_lat_class_inverse<<<1, 256, 0, st>>>(h->ds.t.lrep, h->inv6, h->inv, h->ds.t.lcinv6, h->ds.t.lcinv9);
+        k_lat_class_inverse<<<1, 256, 0, st>>>(h->ds.t.lrep, h->inv6, h->inv, h->ds.t.lcinv6, h->ds.t.lcinv9,
+                                               h->ds.t.lcz);
 }
 
 void fold_pair(const double *a, const double *b, uint32_t n, double *out, hipStream_t st)
