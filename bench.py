@@ -55,9 +55,10 @@ def parse():
     ap.add_argument("--cpu-iterations", type=int, default=40)
     ap.add_argument("--no-general-roofline", action="store_true",
                     help="skip roofline_general (the fan-group tiles kernel on C3 with the lattice stencil off)")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "peer"],
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "peer", "auto"],
                     help="N>1 exchange steps: RCCL groups, or the PEER communicator's device-initiated stores into "
-                         "IPC-mapped mailboxes (FAST only)")
+                         "IPC-mapped mailboxes (FAST only); auto: PEER when every rank maps every peer and a trial "
+                         "exchange completes on all of them, else RCCL")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the 'general' block (the same workload on the fan-group tiles, CWF_LATTICE=0)")
     ap.add_argument("--no-hbm-roofline", action="store_true",
@@ -328,17 +329,43 @@ def main():
         src = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=mode)  # host arrays only
         sh = shard.build_shard(src, begin, rank, node_global)
         system = sh.system(case.materials, 1.0, 0.0, device=device)
-        if args.comm == "peer":  # device-initiated stores into IPC-mapped mailboxes (peer.hip)
-            comm = shard.Comm.peer(world, rank, device)
-            comm.attach(system, sh)
+        comm_kind = args.comm
+        if comm_kind in ("peer", "auto"):  # device-initiated stores into IPC-mapped mailboxes (peer.hip)
+            err = None
+            try:
+                comm = shard.Comm.peer(world, rank, device)
+                comm.attach(system, sh)
+            except Exception as e:  # noqa: BLE001 - reported, and agreed on below
+                err = e
             handles = [None] * world
-            dist.all_gather_object(handles, comm.handle())
-            comm.connect(handles)
-        else:
+            dist.all_gather_object(handles, None if err else comm.handle())
+            if err is None and all(hd is not None for hd in handles):
+                try:
+                    comm.connect(handles)
+                    shard.Comm.time_exchange(system, 8)  # a peer that never arrives fails here (bounded wait)
+                except Exception as e:  # noqa: BLE001
+                    err = e
+            ok = [None] * world
+            dist.all_gather_object(ok, err is None and all(hd is not None for hd in handles))
+            if not all(ok):
+                if comm_kind == "peer":
+                    raise SystemExit(f"rank {rank}: PEER communicator unavailable: {err}")
+                if rank == 0:
+                    print(f"# --comm auto: PEER unavailable on some rank ({err}); using RCCL", file=sys.stderr)
+                if comm is not None:
+                    comm.close()
+                comm = None
+                system.close()
+                system = sh.system(case.materials, 1.0, 0.0, device=device)
+                comm_kind = "rccl"
+            else:
+                comm_kind = "peer"
+        if comm_kind == "rccl":
             uid = [shard.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             comm = shard.Comm.rccl(world, rank, uid[0], device)
             comm.attach(system, sh)
+        args.comm = comm_kind
 
         class _LocalPacking:  # the Stepper's view of the shard: local node order, local vectors
             external_force = sh.local_dofs(P.external_force)

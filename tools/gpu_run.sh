@@ -16,6 +16,9 @@
 #   sq:NAME[:ARGS]          the SQ counter pass of the same (tools/profile.sh SQ_PMC=1)
 #   calib                   FETCH_SIZE / WRITE_SIZE against known byte counts (tools/pmc_calib, built in-tree
 #                           beforehand) -> <TAG>_calib.json
+#   n2:NAME[:ARGS]          bench.py --gpus 2 under torch.distributed.run, both ranks on this GPU (a rehearsal of the
+#                           driver's N>1 flow: the PEER communicator maps the other process's mailbox on the same
+#                           device) -> <TAG>_n2_NAME.json
 #   peer                    the PEER communicator's tests with their exchange-latency prints (2 / 3 processes on
 #                           this GPU) -> <TAG>/peer.log
 # e.g. bash tools/gpu_run.sh r04c tests:tests/test_gpu_lattice.py bench:c2 bench:c3:--config,c3,--steps,3 \
@@ -83,6 +86,10 @@ for step in "$@"; do
       timeout -k 10 300 python -u -m pytest tests/test_gpu_peer.py -m gpu -s -q --timeout 280 --timeout-method thread \
         > $O/peer.log 2>&1 || { tail -30 $O/peer.log; exit 5; }
       grep -E "PEER exchange|passed|failed" $O/peer.log ;;
+    n2)
+      timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29517 bench.py --gpus 2 $(sp "$b") > $O/n2_$a.log 2>&1 || { echo "FAIL n2_$a"; tail -20 $O/n2_$a.log; exit 2; }
+      grep '^{"metric"' $O/n2_$a.log > $O/n2_$a.json && line $O/n2_$a.log n2_$a ;;
     *) echo "unknown step $step"; exit 64 ;;
   esac
 done
