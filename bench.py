@@ -14,9 +14,11 @@ bounded single-thread CPU baseline (the oracle restatement of the reference's so
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): weak scaling, one process per
 GPU. The global block stacks N copies of the per-GPU workload along z; rank r owns a contiguous range
 of node planes, builds only its slab sub-mesh (+ one ghost cell layer) and solves as one shard of the
-global system: RCCL all-gathers of the PCG scalars (p.Ap, r.r / r.z, 8-16 B per rank) and one halo of
-z per iteration over xGMI (csrc/comm.cpp). value = sum over ranks of owned DOFs x PCG iterations /
-max-over-ranks wall time.
+global system: all-gathers of the PCG scalars (p.Ap, r.r / r.z, 8-16 B per rank) and one halo of z per
+iteration over xGMI, by default through the PEER communicator (csrc/peer.hip: one launch per exchange step,
+device stores into the neighbours' IPC-mapped mailboxes), with RCCL groups (csrc/comm.cpp) when any rank
+cannot map its peers (--comm auto; --comm rccl / peer to force one). value = sum over ranks of owned DOFs x
+PCG iterations / max-over-ranks wall time.
 """
 from __future__ import annotations
 
@@ -55,7 +57,7 @@ def parse():
     ap.add_argument("--cpu-iterations", type=int, default=40)
     ap.add_argument("--no-general-roofline", action="store_true",
                     help="skip roofline_general (the fan-group tiles kernel on C3 with the lattice stencil off)")
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "peer", "auto"],
+    ap.add_argument("--comm", default="auto", choices=["rccl", "peer", "auto"],
                     help="N>1 exchange steps: RCCL groups, or the PEER communicator's device-initiated stores into "
                          "IPC-mapped mailboxes (FAST only); auto: PEER when every rank maps every peer and a trial "
                          "exchange completes on all of them, else RCCL")
@@ -286,7 +288,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo", init_method="env://")  # bookkeeping only; the data path is RCCL
+        dist.init_process_group("gloo", init_method="env://")  # bookkeeping only; the data path is PEER / RCCL
     import numpy as np
 
     from cwf import _lib, pcg, scenarios, shard
