@@ -269,6 +269,17 @@ int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::
 {
     for (size_t i = 0; i < g.size(); ++i)  // member 0's launch carries the timing events
         fast_tiles_pcg(g[i], it, g[i]->stream, i ? nullptr : e0, i ? nullptr : e1);
+    // PEER (one member per process): the exchange step folds the rank's shares itself, one launch fewer per step
+    cwf_hip_system *h0 = g[0];
+    if (h0->comm && h0->comm->kind == 2 && h0->nranks > 1)
+    {
+        const PeerFold fpap{h0->part0, nullptr, fast_tile_blocks(h0->ds)};
+        if (int st = peer_exchange(h0, {Gather{&cwf_hip_system::g_pap, 1}}, {}, &fpap))
+            return st;
+        fast_update_pcg(h0, rhs[0], it, h0->stream);
+        const PeerFold frrz{h0->part1, h0->part2, fast_rrz_shares(h0->ds, it)};
+        return peer_exchange(h0, {Gather{&cwf_hip_system::g_rrz, 2}}, {h0->z}, &frrz);
+    }
     for (cwf_hip_system *h : g)
         fast_fold_pap(h, h->stream);
     if (int st = comm_allgather(g, &cwf_hip_system::g_pap, 1))

@@ -428,7 +428,8 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
 
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
-unsigned fast_update_blocks(const DevSys &s, bool flush);  // grid of update pass (lazy-x iteration or not)
+unsigned fast_update_blocks(const DevSys &s, bool flush);
+unsigned fast_rrz_shares(const DevSys &s, unsigned it);  // the {r.r, r.z} shares iteration it's update pass writes  // grid of update pass (lazy-x iteration or not)
 // sharded FAST PCG (comm.cpp orchestrates, spmv_tiles.hip / kernels_fast.hip launch)
 // post.hip: derived fields (derived_fields.cpp:139-211) -> f32 [13 E] / [13 N] (either may be NULL)
 void derived_fields(cwf_hip_system *h, const float *u, float *elem_out, float *node_out, hipStream_t st);
@@ -453,7 +454,15 @@ constexpr size_t kMaxHaloVecs = 3;  // halo vectors of one exchange step
 constexpr int kMaxPeers = 16;       // ranks of a PEER communicator
 // peer.hip: the PEER communicator's mailbox (at attach), its exchange step, and its teardown
 int peer_attach(cwf_hip_system *h);
-int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs);
+// fold (optional): the rank's own slot of gather 0 is computed in the step from this rank's per-workgroup shares
+// (k_fold_pair's order), in place of a fold launch before it
+struct PeerFold
+{
+    const double *a, *b;  // shares of slot 0 and (b) slot 1
+    uint32_t n;
+};
+int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs,
+                  const PeerFold *fold = nullptr);
 void peer_release(cwf_hip_comm *cm);
 int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                        const std::vector<std::vector<float *>> &vecs);

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "cwf_internal.hpp"
+#include "reduce.hpp"
 
 #define HIPTRY(h, expr)                                                                                        \
     do                                                                                                         \
@@ -47,6 +48,7 @@ namespace
 constexpr uint64_t kPeerMagic = 0x43574650454552ull;  // "CWFPEER"
 constexpr size_t kHdrBytes = 4096, kFlagLine = 64, kSlot = 4;  // kSlot doubles per rank and gather
 constexpr int kMaxPeerGathers = 2;
+constexpr int kPeerThreads = 1024;  // the fold of a rank's shares is k_fold_pair's 1024-thread fold_all
 
 struct MboxHeader  // at offset 0 of every mailbox
 {
@@ -86,13 +88,34 @@ struct PeerStep
     float *out[kMaxHaloVecs];
     const double *gath;  // this parity's gather area
     double *gbuf[kMaxPeerGathers];
+    // fold (fn > 0): gather 0's own slot(s) from the rank's shares fa / fb, folded by workgroup 0
+    const double *fa, *fb;
+    uint32_t fn;
 };
 
-__global__ __launch_bounds__(256) void k_peer_step(PeerStep a)
+__global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
 {
+    constexpr uint32_t NT = kPeerThreads;
+    // (0) workgroup 0: this rank's scalars, folded as k_fold_pair folds them, kept for the push and stored locally
+    __shared__ double red[NT / 64], gv[kSlot];
+    if (blockIdx.x == 0 && a.fn)
+    {
+        const double ta = fold_all<NT>(a.fa, a.fn, red);
+        const double tb = a.fb ? fold_all<NT>(a.fb, a.fn, red) : 0.0;
+        if (threadIdx.x == 0)
+        {
+            gv[0] = ta;
+            gv[1] = tb;
+            double *own = const_cast<double *>(a.gsrc[0]);
+            own[0] = ta;
+            if (a.fb)
+                own[1] = tb;
+        }
+        __syncthreads();
+    }
     // (1) push: node item t of the flattened (vector, neighbour, node) space, workgroup-strided
     const uint64_t items = a.total * a.nv;
-    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < items; t += (uint64_t)gridDim.x * 256)
+    for (uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x; t < items; t += (uint64_t)gridDim.x * NT)
     {
         uint64_t r = t % a.total;
         const uint32_t v = (uint32_t)(t / a.total);
@@ -111,7 +134,7 @@ __global__ __launch_bounds__(256) void k_peer_step(PeerStep a)
         const uint32_t p = threadIdx.x / (kMaxPeerGathers * kSlot), q = (threadIdx.x / kSlot) % kMaxPeerGathers,
                        j = threadIdx.x % kSlot;
         if (p != a.rank && q < a.ng && j < a.gcount[q])
-            a.gdst[p][(size_t)q * a.nranks * kSlot + j] = a.gsrc[q][j];
+            a.gdst[p][(size_t)q * a.nranks * kSlot + j] = q == 0 && a.fn ? gv[j] : a.gsrc[q][j];
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -167,7 +190,7 @@ __global__ __launch_bounds__(256) void k_peer_step(PeerStep a)
     __threadfence_system();
     // (3) unpack
     const uint64_t per = 3 * a.nghost;
-    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < per * a.nv; t += (uint64_t)gridDim.x * 256)
+    for (uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x; t < per * a.nv; t += (uint64_t)gridDim.x * NT)
     {
         const uint32_t v = (uint32_t)(t / per);
         const uint64_t i = t % per;
@@ -229,7 +252,8 @@ void peer_release(cwf_hip_comm *cm)
     cm->ticket = nullptr;
 }
 
-int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs)
+int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs,
+                  const PeerFold *fold)
 {
     cwf_hip_comm *cm = h->comm;
     const int n = cm->nranks;
@@ -241,6 +265,7 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
         if (q.count > kSlot)
             return set_error(h, CWF_ERR_UNSUPPORTED, "the peer communicator carries the FAST schedule only",
                              "PARITY's chunk-partial all-gathers need RCCL or LOCAL");
+    constexpr uint64_t NTP = kPeerThreads;
     const uint32_t epoch = ++cm->epoch;
     const uint32_t par = epoch & 1u;
     PeerStep a{};
@@ -285,10 +310,17 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
     a.nghost = nghost;
     a.ghost0 = h->ds.Nown;
     a.gath = reinterpret_cast<const double *>(static_cast<char *>(cm->mbox) + off_gath(n) + par * gath_bytes(n));
-    // one workgroup per 256 pushed nodes or 1024 unpacked floats, <= 128 (all resident: every one reaches its ticket)
-    const uint64_t work = std::max<uint64_t>((a.total * a.nv + 255) / 256, (3 * nghost * a.nv + 1023) / 1024);
-    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(work, 128));
-    k_peer_step<<<grid, 256, 0, h->stream>>>(a);
+    if (fold && a.ng)
+    {
+        a.fa = fold->a;
+        a.fb = fold->b;
+        a.fn = fold->n;
+    }
+    // one workgroup per 1024 pushed nodes or 4096 unpacked floats, <= 64 (all resident: every one reaches its
+    // ticket)
+    const uint64_t work = std::max<uint64_t>((a.total * a.nv + NTP - 1) / NTP, (3 * nghost * a.nv + 4 * NTP - 1) / (4 * NTP));
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(work, 64));
+    k_peer_step<<<grid, kPeerThreads, 0, h->stream>>>(a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(h, e, "peer exchange launch");
 }
@@ -392,11 +424,19 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
     HIPTRY(h, hipEventCreate(&e1));
     std::vector<cwf_hip_system *> g{h};
     std::vector<std::vector<float *>> vecs{{h->z}};
-    int st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_rrz, 2}}, vecs);  // warm
+    // as the iteration runs it: with the fold of the update pass's shares (PEER folds them in the step itself)
+    const PeerFold fold{h->part1, h->part2, fast_rrz_shares(h->ds, 0)};
+    const auto step = [&]() {
+        if (h->comm->kind == 2)
+            return peer_exchange(h, {Gather{&cwf_hip_system::g_rrz, 2}}, {h->z}, &fold);
+        fast_fold_rrz(h, 0, h->stream);
+        return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_rrz, 2}}, vecs);
+    };
+    int st = step();  // warm
     if (!st && hipEventRecord(e0, h->stream) != hipSuccess)
         st = set_error(h, CWF_ERR_HIP, "hipEventRecord");
     for (int i = 0; i < steps && !st; ++i)
-        st = comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_rrz, 2}}, vecs);
+        st = step();
     float ms = 0.f;
     if (!st && hipEventRecord(e1, h->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess)
         (void)hipEventElapsedTime(&ms, e0, e1);

@@ -27,6 +27,7 @@
 
 #include "blockinv_pack.hpp"
 #include "cwf_internal.hpp"
+#include "reduce.hpp"
 
 namespace cwf
 {
@@ -38,33 +39,6 @@ constexpr int kMaxM = 16;
 #endif
 constexpr int kUpdThreads = CWF_UPD_THREADS;  // update-pass workgroup size (its per-workgroup shares are refolded by every consumer workgroup)
 constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
-// fp64 lane exchange through DPP (both halves): CTRL is a GFX9 dpp_ctrl
-template <int CTRL> __device__ __forceinline__ double dpp_f64(double v)
-{
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double lane_f64(double v, int lane)
-{
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
-                            __builtin_amdgcn_readlane(__double2loint(v), lane));
-}
-// Wave sum in a fixed order, the same value in every lane (all 64 lanes active). Inside each 16-lane row a butterfly
-// through DPP: quad_perm xor 1, xor 2, then row_half_mirror and row_mirror, which act as xor 4 and xor 8 on values
-// already uniform over quads / half-rows; each lane adds the same two operands (a + b == b + a bitwise), so every
-// lane of a row holds the same row sum. Then ((row0 + row1) + row2) + row3 from readlanes. The ds_bpermute butterfly
-// it replaces (__shfl_xor, six LDS-routed rounds of two 32-bit permutes) sat on the critical path of every consumer
-// prologue's scalar fold and every producer's share.
-__device__ __forceinline__ double wave_sum(double v)
-{
-    v += dpp_f64<0xB1>(v);   // quad_perm [1, 0, 3, 2]
-    v += dpp_f64<0x4E>(v);   // quad_perm [2, 3, 0, 1]
-    v += dpp_f64<0x141>(v);  // row_half_mirror
-    v += dpp_f64<0x140>(v);  // row_mirror
-    return ((lane_f64(v, 0) + lane_f64(v, 16)) + lane_f64(v, 32)) + lane_f64(v, 48);
-}
-
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 
 // buffer descriptor over a whole allocation (base pointer wave-uniform: a kernel argument)
@@ -86,116 +60,6 @@ __device__ __forceinline__ void store3(float *base, __amdgpu_buffer_rsrc_t rs, u
         __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 16);
     else
         __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 0);
-}
-
-// NT-thread block sum in a fixed order; result valid in every thread. red: NT/64 doubles.
-template <int NT> __device__ __forceinline__ double block_sum(double v, double *red)
-{
-    v = wave_sum(v);
-    if ((threadIdx.x & 63) == 0)
-        red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w)
-        t += red[w];
-    __syncthreads();
-    return t;
-}
-
-// the pair {a, b} in one pass (one LDS round, two barriers); red: 2 NT / 64 doubles
-template <int NT> __device__ __forceinline__ void block_sum2(double a, double b, double *red, double &ta, double &tb)
-{
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if ((threadIdx.x & 63) == 0)
-    {
-        red[2 * (threadIdx.x >> 6)] = a;
-        red[2 * (threadIdx.x >> 6) + 1] = b;
-    }
-    __syncthreads();
-    double x = 0.0, y = 0.0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w)
-    {
-        x += red[2 * w];
-        y += red[2 * w + 1];
-    }
-    __syncthreads();
-    ta = x;
-    tb = y;
-}
-
-template <int NT>
-__device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigned count, double *red,
-                                           unsigned stride = 1)
-{
-    // thread t sums p[t], p[t + NT], ... in that order; 8 loads are issued before their adds so a long
-    // fold costs count / (8 NT) memory round trips instead of count / NT
-    double v = 0.0;
-    unsigned i = threadIdx.x;
-    for (; i + 7u * NT < count; i += 8u * NT)
-    {
-        double q[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            q[u] = p[(size_t)(i + u * NT) * stride];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            v += q[u];
-    }
-    for (; i < count; i += NT)
-        v += p[(size_t)i * stride];
-    return block_sum<NT>(v, red);
-}
-
-// the two folds of fold_all in one pass: every load of both arrays in flight together, one block reduction of
-// the pair (red: 2 NT / 64 doubles); fixed order, so every workgroup gets the same pair
-template <int NT>
-__device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const double *__restrict__ pb, unsigned count,
-                                          double *red, unsigned stride, double &ta, double &tb)
-{
-    double va = 0.0, vb = 0.0;
-    unsigned i = threadIdx.x;
-    for (; i + 3u * NT < count; i += 4u * NT)
-    {
-        double qa[4], qb[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-        {
-            qa[u] = pa[(size_t)(i + u * NT) * stride];
-            qb[u] = pb[(size_t)(i + u * NT) * stride];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-        {
-            va += qa[u];
-            vb += qb[u];
-        }
-    }
-    for (; i < count; i += NT)
-    {
-        va += pa[(size_t)i * stride];
-        vb += pb[(size_t)i * stride];
-    }
-    va = wave_sum(va);
-    vb = wave_sum(vb);
-    if ((threadIdx.x & 63) == 0)
-    {
-        red[2 * (threadIdx.x >> 6)] = va;
-        red[2 * (threadIdx.x >> 6) + 1] = vb;
-    }
-    __syncthreads();
-    double a = 0.0, b = 0.0;
-#pragma unroll
-    for (int w = 0; w < NT / 64; ++w)
-    {
-        a += red[2 * w];
-        b += red[2 * w + 1];
-    }
-    __syncthreads();
-    ta = a;
-    tb = b;
 }
 
 // Control-block words as vector (buffer) loads. A consumer prologue issues them with its gathers and the scalar
@@ -2216,6 +2080,8 @@ void fast_fold_pap(cwf_hip_system *h, hipStream_t st)
         return;
     fold_pair(h->part0, nullptr, fast_tile_blocks(h->ds), h->g_pap + h->rank, st);
 }
+
+unsigned fast_rrz_shares(const DevSys &s, unsigned it) { return fast_update_blocks(s, x_flush_iter(it)); }
 
 void fast_fold_rrz(cwf_hip_system *h, unsigned it, hipStream_t st)
 {
