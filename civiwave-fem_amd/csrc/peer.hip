@@ -4,10 +4,11 @@
 // group, k_peer_step, in three phases:
 //
 //   push    every workgroup gathers its share of the send rows straight from the vectors (send_idx: no pack pass)
-//           and stores them into the neighbours' mailboxes (remote stores over xGMI; the same device's memory under
-//           IPC on one GPU), workgroup 0 this rank's scalar slots into every peer's; each workgroup releases at
-//           system scope and takes a ticket; the last one stores the step's epoch into every peer's flag for this
-//           rank (system-scope atomic store);
+//           and stores them into the neighbours' mailboxes (write-through system-scope stores: over xGMI to the
+//           neighbour's HBM; the same device's memory under IPC on one GPU), workgroup 0 this rank's scalar slots
+//           (folded from the rank's shares in the step, PeerFold) into every peer's; each workgroup waits for its
+//           stores and takes a ticket; the last one releases at system scope and stores the step's epoch into
+//           every peer's flag for this rank (system-scope atomic store);
 //   wait    every workgroup polls this rank's flags, one lane per peer, until every peer has reached the epoch
 //           (bounded: a peer that never arrives ends the solve with CWF_ERR_COMM instead of a hang), then acquires
 //           at system scope;
@@ -125,27 +126,29 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
         const float *src = a.vec[v] + 3ull * a.send_idx[a.src_off[k] + r];
         float *d = a.dst[k] + a.dst_vstride[k] * v + 3 * r;
         const float x0 = src[0], x1 = src[1], x2 = src[2];
-        d[0] = x0;
-        d[1] = x1;
-        d[2] = x2;
+        // write-through (system scope): nothing is left dirty in this XCD's L2, so no workgroup needs an L2
+        // write-back fence before its ticket
+        __hip_atomic_store(d + 0, x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(d + 1, x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(d + 2, x2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (blockIdx.x == 0 && threadIdx.x < a.nranks * kMaxPeerGathers * kSlot)
     {
         const uint32_t p = threadIdx.x / (kMaxPeerGathers * kSlot), q = (threadIdx.x / kSlot) % kMaxPeerGathers,
                        j = threadIdx.x % kSlot;
         if (p != a.rank && q < a.ng && j < a.gcount[q])
-            a.gdst[p][(size_t)q * a.nranks * kSlot + j] = q == 0 && a.fn ? gv[j] : a.gsrc[q][j];
+            __hip_atomic_store(a.gdst[p] + (size_t)q * a.nranks * kSlot + j, q == 0 && a.fn ? gv[j] : a.gsrc[q][j],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    // every storing wave waits for its write-through stores, then one lane takes the workgroup's ticket
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
     {
-        __threadfence_system();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t old = __hip_atomic_fetch_add(a.cnt_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1 == gridDim.x)
         {
-            __threadfence_system();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
             for (uint32_t p = 0; p < a.nranks; ++p)
                 if (p != a.rank)
                     __hip_atomic_store(a.flag[p], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
         }
         return;
     }
-    __threadfence_system();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: an invalidate only (no L2 write-back)
     // (3) unpack
     const uint64_t per = 3 * a.nghost;
     for (uint64_t t = (uint64_t)blockIdx.x * NT + threadIdx.x; t < per * a.nv; t += (uint64_t)gridDim.x * NT)

@@ -1544,7 +1544,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_pcg_update_tiles(
     for (unsigned j = 0; j < kXLag; ++j)
         ah[j] = xflush ? ctl_f64(rctl, (uint32_t)(offsetof(Ctl, alpha_h) + 8u * j)) : 0.0;
     // pcg.cpp:840-852: alpha = rho / (p . Ap)
-    const double denom = fold_all<kUpdThreads>(part_dot, ntp, red);
+    const double denom = fold_all<kUpdThreads, 12>(part_dot, ntp, red);  // <= 3,072 K_eff shares in one trip
     if (!active)
         return;
     if constexpr (LAT)
