@@ -111,23 +111,23 @@ __device__ __forceinline__ double fold_all(const double *__restrict__ p, unsigne
 
 // the two folds of fold_all in one pass: every load of both arrays in flight together, one block reduction of
 // the pair (red: 2 NT / 64 doubles); fixed order, so every workgroup gets the same pair
-template <int NT>
+template <int NT, int B = 4>
 __device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const double *__restrict__ pb, unsigned count,
                                           double *red, unsigned stride, double &ta, double &tb)
 {
     double va = 0.0, vb = 0.0;
     unsigned i = threadIdx.x;
-    for (; i + 3u * NT < count; i += 4u * NT)
+    for (; i + (B - 1u) * NT < count; i += B * NT)
     {
-        double qa[4], qb[4];
+        double qa[B], qb[B];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < B; ++u)
         {
             qa[u] = pa[(size_t)(i + u * NT) * stride];
             qb[u] = pb[(size_t)(i + u * NT) * stride];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < B; ++u)
         {
             va += qa[u];
             vb += qb[u];
@@ -136,16 +136,16 @@ __device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const d
     if (i < count)  // the partial batch, as in fold_all
     {
         const unsigned w0 = i - (threadIdx.x & 63u), nb = (count - w0 + NT - 1u) / NT;
-        double qa[4], qb[4];
+        double qa[B], qb[B];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < B; ++u)
         {
             const size_t k = (size_t)min(i + u * NT, count - 1u) * stride;
             qa[u] = (unsigned)u < nb ? pa[k] : 0.0;
             qb[u] = (unsigned)u < nb ? pb[k] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < B; ++u)
         {
             va += i + u * NT < count ? qa[u] : 0.0;
             vb += i + u * NT < count ? qb[u] : 0.0;

@@ -96,7 +96,7 @@ __device__ __forceinline__ CtlPre ctl_prefetch(const Ctl *ctl, unsigned it)
 // from the all-gathered per-rank {r.r, r.z} pairs of a sharded system (stride 2, rank order).
 // Returns false when the solve is over (converged or rho breakdown); *beta_out = beta for this iteration. pre: the
 // control words prefetched by the caller (ctl_prefetch); then !pre->active (tested after the fold) also returns false.
-template <int NT>
+template <int NT, int B = 4>
 __device__ __forceinline__ bool residual_step(Ctl *ctl, const double *__restrict__ prr, const double *__restrict__ prz,
                                               unsigned nparts, unsigned stride, unsigned it,
                                               double *__restrict__ hist, double *red, float *beta_out,
@@ -108,7 +108,7 @@ __device__ __forceinline__ bool residual_step(Ctl *ctl, const double *__restrict
         return pre ? pre->active != 0 : true;
     }
     double rr, rz;
-    fold_all2<NT>(prr, prz, nparts, red, stride, rr, rz);
+    fold_all2<NT, B>(prr, prz, nparts, red, stride, rr, rz);
     if (pre && !pre->active)
         return false;
     const double res = sqrt(rr);
@@ -1192,7 +1192,7 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
     float beta = 0.f;
     if constexpr (MODE == 1)
     {
-        if (!residual_step<NT>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta, pa.abl & 32u))
+        if (!residual_step<NT, 8>(pa.ctl, pa.prr, pa.prz, pa.nupd, pa.stride, pa.it, pa.hist, red, &beta, pa.abl & 32u))
             return;
     }
     const float sK6 = (float)(s.sK / 6.0), sM = (float)s.sM;
