@@ -1299,8 +1299,9 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {
         static thread_local char name[96];
-        snprintf(name, sizeof name, "k_keff_lattice<1, false, %s, %s, %s, %s>", t.lsym ? "true" : "false",
-                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lmu && t.lzr ? "true" : "false");
+        snprintf(name, sizeof name, "k_keff_lattice<1, false, %s, %s, %s, %s, %s>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lmu && t.lzr ? "true" : "false",
+                 t.lpstride ? "true" : "false");
         return name;
     }
     if (t.grp)  // the PCG-mode instantiation, as rocprofv3 names it (so a profile of another one is not taken)
