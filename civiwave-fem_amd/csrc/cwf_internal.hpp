@@ -91,7 +91,10 @@ struct DevTiles
     // columns of the strict interior i, j in [1, n - 1) times lL planes of [lkI0, lkI1)); lnwork = all of them
     uint32_t lnbx = 0, lnby = 0, lL = 0, lnwork = 0, lnwm = 0, lnsb = 0, lnshell = 0, lkI0 = 0, lkI1 = 0;
     int lmu = 0;                         // every strict-interior node's lumped mass is lmass (the bricks read none)
-    int lshl = 0;                        // shell workgroups after the bricks (grids of one resident round)
+    int lshl = 0;                        // shell workgroups after the bricks (grids of one resident round); 2: each
+                                         // k-chunk's perimeter workgroups right after its bricks (lnsc per chunk),
+                                         // the full end planes last
+    uint32_t lnsc = 0;                   // lshl 2: perimeter workgroups per k-chunk
     int lzr = 0;                         // with lmu and the class table on an unattached handle: the update pass
                                          // stores no z, the K_eff pass forms it from r and the node's class
     float lmass = 0.f;

@@ -32,8 +32,9 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_LAT_MASS", "0: the lattice bricks read the per-node mass even when the strict interior's is uniform"},
     {"CWF_LAT_ZR", "0|1: the lattice update pass stores z / the K_eff pass forms z from r and the node class "
                    "(default: the latter from 2M nodes)"},
-    {"CWF_LAT_SHELL_LAST", "0|1: the lattice shell workgroups lead / follow the bricks (default: follow when the "
-                           "grid fits one round of resident workgroups)"},
+    {"CWF_LAT_SHELL_LAST", "0|1|2: the lattice shell workgroups lead / follow the bricks / each k-chunk's perimeter "
+                           "workgroups follow its bricks (default: follow when the grid fits one round of resident "
+                           "workgroups, else interleaved)"},
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},

@@ -465,7 +465,18 @@ void lattice_plan(DevTiles &t)
     // rounds, shell last -2.6%) and follow them when it fits in one (C2: 436 workgroups, shell last +6.2%, keff 14.2
     // -> 12.9 us; same box, two passes)
     const char *sl = knob("CWF_LAT_SHELL_LAST");
-    t.lshl = sl ? (sl[0] == '1' ? 1 : 0) : (t.lnwork <= kLatTargetItems ? 1 : 0);
+    // several rounds: each k-chunk's perimeter workgroups right after its bricks (C3 +0.5-1.4%, C3 hex8 +1.5% over
+    // the shell first, same box: the perimeter gathers find the chunk's lines in the XCD's L2; profiles/r04w_*)
+    t.lshl = sl ? (sl[0] == '2' ? 2 : sl[0] == '1' ? 1 : 0) : (t.lnwork <= kLatTargetItems ? 1 : 2);
+    t.lnsc = 0;
+    if (t.lshl == 2)  // interleaved: per k-chunk its bricks, then the perimeters of its planes; the end planes last
+    {
+        const uint64_t per = 2 * nx + 2 * (ny - 2), nchunk = (planes + L - 1) / L;
+        const uint64_t nlo = (k0 == 0 && k1 > 0) ? nx * ny : 0, nhi = (k1 == nz && nz > 1 && k1 > k0) ? nx * ny : 0;
+        t.lnsc = (uint32_t)((L * per + kLatThreads - 1) / kLatThreads);
+        t.lnwork = (uint32_t)(nchunk * (cols + t.lnsc) + (nlo + kLatThreads - 1) / kLatThreads +
+                              (nhi + kLatThreads - 1) / kLatThreads);
+    }
     t.ntiles = t.lnwork;
 }
 

@@ -131,7 +131,9 @@ def test_lattice_pcg_variants_solve(variant, monkeypatch):
     monkeypatch.setenv("CWF_LAT_L", "3")
     case = scenarios.block_case(40, 19, 9, h=0.1, tol=1e-6, max_iterations=1500)
     s = _system(case)
-    tail = {"z-from-r": ", true, true>", "z-stored": ", true, false>", "per-node-mass": ", false, false>"}[variant]
+    # <..., mass uniform, z from r, affine plane bases>
+    tail = {"z-from-r": ", true, true, true>", "z-stored": ", true, false, true>",
+            "per-node-mass": ", false, false, true>"}[variant]
     assert _kernel(s).endswith(tail)
     assert _apply_err(case, s, seed=5) <= 2e-5
     o = oracle_system(case.packing, case.materials, *case.scalars())
