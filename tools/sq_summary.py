@@ -6,7 +6,10 @@ import collections
 import csv
 import glob
 import os
-import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import norm  # noqa: E402  'ns::k<a, ns::B>' and 'k<a, B>' alike
 
 ap = argparse.ArgumentParser()
 ap.add_argument("dir")
@@ -15,11 +18,10 @@ a = ap.parse_args()
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(a.dir, "*", "*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"cwf::(?:\(anonymous namespace\)::)?([\w<>, ]+)", r["Kernel_Name"])
-        k = m.group(1) if m else r["Kernel_Name"][:40]
+        k = norm(r["Kernel_Name"])
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in acc.items():
-    if a.kernel and not any(s in k for s in a.kernel):
+    if a.kernel and not any(s in k or norm(s) == k for s in a.kernel):
         continue
     print(k)
     avg = {c: sum(v) / len(v) for c, v in cs.items()}
