@@ -76,18 +76,70 @@ bool iso_pattern(const double *D)
 // the node tiles of k_keff_parity_tile. Tile b holds nodes [256 b, 256 b + 256) (three whole 256-DOF reduction
 // chunks, so the p.Ap chunk partials stay fused), its incident tets in ascending element order, and for each of its
 // nodes' incidences the tet's index in that list. FAST handles never build it.
+// above this many tets the host-side breadth-first pass (random reads of 16 B of connectivity per incidence) takes
+// tens of seconds: strips there (C5's 96M tets)
+constexpr uint64_t kParityCompactMaxTets = 1ull << 25;
+
+// Compact PARITY tiles: greedy breadth-first blobs of <= 256 nodes over the node graph (two nodes adjacent when
+// they share a tet), seeded in node order. On C2 the strip tiles (256 consecutive nodes of the caller's
+// lexicographic order, one plane thick) evaluate each tet ~2.4 times; blobs fewer.
+std::vector<uint32_t> parity_compact_tiles(const std::vector<uint32_t> &off, const std::vector<uint32_t> &inc,
+                                           const std::vector<uint32_t> &conn, uint64_t N)
+{
+    std::vector<uint32_t> nodes;
+    nodes.reserve(N + N / 4);
+    std::vector<uint8_t> state(N, 0);  // 0 free, 1 queued for the current tile, 2 placed
+    std::vector<uint32_t> queue;
+    queue.reserve(4096);
+    for (uint64_t seed = 0; seed < N; ++seed)
+    {
+        if (state[seed])
+            continue;
+        queue.clear();
+        queue.push_back((uint32_t)seed);
+        state[seed] = 1;
+        size_t head = 0, placed = 0;
+        while (head < queue.size() && placed < 256)
+        {
+            const uint32_t u = queue[head++];
+            state[u] = 2;
+            nodes.push_back(u);
+            ++placed;
+            for (uint32_t j = off[u]; j < off[u + 1]; ++j)
+                for (int c = 0; c < 4; ++c)
+                {
+                    const uint32_t v = conn[4ull * (inc[j] >> 2) + c];
+                    if (!state[v])
+                    {
+                        state[v] = 1;
+                        queue.push_back(v);
+                    }
+                }
+        }
+        for (size_t q = head; q < queue.size(); ++q)  // queued but not placed: free again
+            state[queue[q]] = 0;
+        nodes.resize((nodes.size() + 255) / 256 * 256, 0xFFFFFFFFu);
+    }
+    return nodes;
+}
+
 int parity_incidence_slots(cwf_hip_system *h)
 {
     DevSys &s = h->ds;
-    const uint64_t N = s.N, E = s.E, nt = (N + 255) / 256;
-    std::vector<uint32_t> off, inc, toff, tets, pinc;
+    const uint64_t N = s.N, E = s.E;
+    // compact tiles for single handles (a shard's PCG loop folds p.Ap into rank-ordered chunk partials in the tile
+    // kernel, which needs tiles of consecutive nodes); CWF_PARITY_TILES=strip keeps the strips
+    const char *pt = knob("CWF_PARITY_TILES");
+    const bool compact = !h->sharded() && E <= kParityCompactMaxTets && !(pt && std::strcmp(pt, "strip") == 0);
+    std::vector<uint32_t> off, inc, toff, tets, pinc, conn, tnodes;
     try
     {
         off.resize(N + 1);
         inc.resize(4 * E);
         pinc.resize(4 * E);
-        toff.resize(nt + 1);
         tets.reserve(3 * E);
+        if (compact)
+            conn.resize(4 * E);
     }
     catch (const std::bad_alloc &)
     {
@@ -95,19 +147,46 @@ int parity_incidence_slots(cwf_hip_system *h)
     }
     HIPTRY(h, hipMemcpy(off.data(), s.off, (N + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost));
     HIPTRY(h, hipMemcpy(inc.data(), s.inc, 4 * E * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (compact)
+    {
+        // the corner ids: the first 16 B of every 64-B element record
+        HIPTRY(h, hipMemcpy2D(conn.data(), 16, s.erec, 64, 16, E, hipMemcpyDeviceToHost));
+        try
+        {
+            tnodes = parity_compact_tiles(off, inc, conn, N);
+        }
+        catch (const std::bad_alloc &)
+        {
+            return set_error(h, CWF_ERR_ALLOC, "host allocation failed");
+        }
+    }
+    const uint64_t nt = compact ? tnodes.size() / 256 : (N + 255) / 256;
+    toff.resize(nt + 1);
     std::vector<uint32_t> loc;
     for (uint64_t b = 0; b < nt; ++b)
     {
-        const uint64_t n0 = 256 * b, n1 = std::min<uint64_t>(N, n0 + 256);
         toff[b] = (uint32_t)tets.size();
         loc.clear();
-        for (uint32_t j = off[n0]; j < off[n1]; ++j)
-            loc.push_back(inc[j] >> 2);
+        const auto tile_node = [&](uint64_t t) -> uint64_t {
+            return compact ? (uint64_t)tnodes[256 * b + t] : 256 * b + t;
+        };
+        for (uint64_t t = 0; t < 256; ++t)
+        {
+            const uint64_t n = tile_node(t);
+            if (n < N)
+                for (uint32_t j = off[n]; j < off[n + 1]; ++j)
+                    loc.push_back(inc[j] >> 2);
+        }
         std::sort(loc.begin(), loc.end());
         loc.erase(std::unique(loc.begin(), loc.end()), loc.end());
-        for (uint32_t j = off[n0]; j < off[n1]; ++j)
-            pinc[j] = (uint32_t)(std::lower_bound(loc.begin(), loc.end(), inc[j] >> 2) - loc.begin()) << 2 |
-                      (inc[j] & 3u);
+        for (uint64_t t = 0; t < 256; ++t)
+        {
+            const uint64_t n = tile_node(t);
+            if (n < N)
+                for (uint32_t j = off[n]; j < off[n + 1]; ++j)
+                    pinc[j] = (uint32_t)(std::lower_bound(loc.begin(), loc.end(), inc[j] >> 2) - loc.begin()) << 2 |
+                              (inc[j] & 3u);
+        }
         try
         {
             tets.insert(tets.end(), loc.begin(), loc.end());
@@ -121,16 +200,21 @@ int parity_incidence_slots(cwf_hip_system *h)
                              "tile_tets=" + std::to_string(tets.size()));
     }
     toff[nt] = (uint32_t)tets.size();
-    uint32_t *dto, *dte, *dpi;
+    uint32_t *dto, *dte, *dpi, *dtn = nullptr;
     if (int st = upload(h, &dto, toff.data(), nt + 1))
         return st;
     if (int st = upload(h, &dte, tets.data(), tets.size()))
         return st;
     if (int st = upload(h, &dpi, pinc.data(), 4 * E))
         return st;
+    if (compact)
+        if (int st = upload(h, &dtn, tnodes.data(), tnodes.size()))
+            return st;
     s.ptile_off = dto;
     s.ptile_tets = dte;
     s.pinc = dpi;
+    s.ptile_nodes = dtn;
+    s.pntile = (uint32_t)nt;
     return 0;
 }
 
@@ -1295,7 +1379,15 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
         return nullptr;
     const DevTiles &t = h->ds.t;
     if (h->mode != CWF_MODE_FAST || !t.ntiles)  // the PCG-loop instantiation (no sanitize) of the element pass
-        return h->ds.iso ? "k_keff_parity_tile<true, false, true>" : "k_keff_parity_tile<false, false, true>";
+    {
+        // the PCG loop's: strips fuse the p.Ap partials (DOT), compact tiles do not (parity_incidence_slots)
+        const char *pt = knob("CWF_PARITY_TILES");
+        const bool compact = h->ds.ptile_nodes || (!h->ds.ptile_off && !h->sharded() && h->ds.E <= kParityCompactMaxTets &&
+                                                    !(pt && !std::strcmp(pt, "strip")));
+        if (compact)
+            return h->ds.iso ? "k_keff_parity_tile<true, false, false, true>" : "k_keff_parity_tile<false, false, false, true>";
+        return h->ds.iso ? "k_keff_parity_tile<true, false, true, false>" : "k_keff_parity_tile<false, false, true, false>";
+    }
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {
         static thread_local char name[96];

@@ -254,6 +254,11 @@ struct DevSys
     const uint32_t *ptile_off = nullptr;
     const uint32_t *ptile_tets = nullptr;
     const uint32_t *pinc = nullptr;
+    // compact tiles (unsharded handles): tile b = the nodes ptile_nodes[256 b ..] (0xFFFFFFFF pads), grown by
+    // breadth-first search over the mesh so a tile is a blob, not a strip of the caller's order; pntile tiles. The
+    // PCG loop's p.Ap chunk partials are then a separate pass (the tiles are not runs of consecutive DOFs)
+    const uint32_t *ptile_nodes = nullptr;
+    uint32_t pntile = 0;
     double sK = 1.0;  // stiffness_scale
     double sM = 0.0;  // mass_factor
     int iso = 0;      // every material has the isotropic Voigt zero pattern

@@ -280,7 +280,7 @@ __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint3
 // work, 293 us).
 constexpr int kTileTets = 256;
 constexpr int kIncAhead = 4;  // a node's next incidence entries held in registers
-template <bool ISO, bool SANITIZE, bool DOT>
+template <bool ISO, bool SANITIZE, bool DOT, bool SET>
 __global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
                                                              float *__restrict__ y, const Ctl *__restrict__ ctl,
                                                              double *__restrict__ pdot, uint32_t nlim,
@@ -295,7 +295,9 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const flo
     // XCD-aware tile order: consecutive tiles (which share halo tets) on one XCD
     const uint32_t ntile = gridDim.x, xcd = blockIdx.x & 7u, per = ntile >> 3, rem = ntile & 7u;
     const uint32_t tile = xcd * per + min(xcd, rem) + (blockIdx.x >> 3);
-    const uint32_t n0 = tile * kBlock, n = n0 + threadIdx.x;
+    // SET (compact tiles): the tile's nodes from ptile_nodes (pads are ~0 >= N); else 256 consecutive nodes
+    const uint32_t n0 = tile * kBlock, n = SET ? s.ptile_nodes[n0 + threadIdx.x] : n0 + threadIdx.x;
+    static_assert(!(SET && DOT), "compact tiles are not runs of consecutive DOFs");
     const uint32_t t0 = s.ptile_off[tile], nt = s.ptile_off[tile + 1] - t0;
     uint32_t j = 0, jend = 0;
     if (n < s.N)
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const flo
             const double vol = (double)cur.vol * s.sK;  // pcg.cpp:642
 #pragma unroll
             for (int a = 0; a < 4; ++a)
-                if (cur.G.c[a] - n0 < (uint32_t)kBlock)  // a corner of this tile
+                if (SET || cur.G.c[a] - n0 < (uint32_t)kBlock)  // a corner of this tile (SET: every corner)
                 {
                     double f[3];
                     corner_force(gx[a], gy[a], gz[a], sig, vol, f);
@@ -1081,11 +1083,21 @@ template <bool SAN, bool DOT>
 void launch_parity_tile(const DevSys &s, const float *x, float *y, const Ctl *ctl, double *pdot, uint32_t nlim,
                         uint32_t chunks, hipStream_t st)
 {
-    const dim3 gn(grid_for(s.N, kBlock)), b(kBlock);
+    const dim3 b(kBlock);
+    if (s.ptile_nodes && !DOT)
+    {
+        const dim3 gn(s.pntile);
+        if (s.iso)
+            k_keff_parity_tile<true, SAN, false, true><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
+        else
+            k_keff_parity_tile<false, SAN, false, true><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
+        return;
+    }
+    const dim3 gn(grid_for(s.N, kBlock));
     if (s.iso)
-        k_keff_parity_tile<true, SAN, DOT><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
+        k_keff_parity_tile<true, SAN, DOT, false><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
     else
-        k_keff_parity_tile<false, SAN, DOT><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
+        k_keff_parity_tile<false, SAN, DOT, false><<<gn, b, 0, st>>>(s, x, y, ctl, pdot, nlim, chunks);
 }
 
 void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, const Ctl *ctl, hipStream_t st)
@@ -1101,7 +1113,7 @@ void parity_keff_ds(const DevSys &s, const float *x, float *y, bool sanitize, co
 void parity_keff_dot(const cwf_hip_system *h, const float *p, float *Ap, const Ctl *ctl, double *pdot, hipStream_t st)
 {
     const DevSys &s = h->ds;
-    if (h->reduction_block != 256)
+    if (h->reduction_block != 256 || s.ptile_nodes)  // compact tiles: the partials in their own pass
     {
         parity_keff_ds(s, p, Ap, false, ctl, st);
         parity_dot_partials_n(3u * s.Nown, (uint32_t)h->reduction_block, p, Ap, nullptr, pdot, nullptr, ctl, st);

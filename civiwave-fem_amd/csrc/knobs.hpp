@@ -36,6 +36,8 @@ inline constexpr Knob kKnobs[] = {
                            "workgroups follow its bricks (default: follow when the grid fits one round of resident "
                            "workgroups, else interleaved)"},
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
+    {"CWF_PARITY_TILES", "strip: PARITY node tiles of 256 consecutive nodes also on a single handle (default there: "
+                         "compact breadth-first tiles and a separate p.Ap partials pass; shards always use strips)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
