@@ -280,8 +280,11 @@ __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint3
 // work, 293 us).
 constexpr int kTileTets = 256;
 constexpr int kIncAhead = 4;  // a node's next incidence entries held in registers
+// The PCG loop's compact-tile instantiation (ISO, no sanitize, SET) is held to 128 VGPRs: 4 waves per SIMD instead
+// of 3 at 132, no spill (C3 PARITY K_eff 1,260 -> 1,124 us, C2 121 -> 124 us, same box: profiles/r04zg_*); the
+// others spill at 128 and keep their registers.
 template <bool ISO, bool SANITIZE, bool DOT, bool SET>
-__global__ __launch_bounds__(kBlock) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
+__global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? 4 : 1) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
                                                              float *__restrict__ y, const Ctl *__restrict__ ctl,
                                                              double *__restrict__ pdot, uint32_t nlim,
                                                              uint32_t chunks)
