@@ -1167,17 +1167,17 @@ __global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *
     uint16_t *sst = reinterpret_cast<uint16_t *>(sq + MS);   // [MS] run start in the local CSR
     __shared__ float dtab[MONO ? 1 : kMaxM * kTab];
     __shared__ double red[2 * (NT / 64)];
-    if constexpr (MODE == 1)
-    {
-        if (!pa.ctl->active)
-            return;
-    }
     const uint32_t nxcd = 8u, xcd = blockIdx.x % nxcd, lb = blockIdx.x / nxcd, nbx = gridDim.x / nxcd;
     const uint32_t t_end = (uint32_t)(((uint64_t)(xcd + 1) * T.ntiles) / nxcd);
     uint32_t t = (uint32_t)(((uint64_t)xcd * T.ntiles) / nxcd) + lb;
     GroupNext cur;
+    // the control flag and the first two tile headers: scalar loads issued together, one round trip (the flag was
+    // a round trip of its own in front of the headers)
+    const int active = MODE == 1 ? pa.ctl->active : 1;
     uint4 hd = t < t_end ? hdr[t] : uint4{0u, 0u, 0u, 0u};
     uint4 hd2 = t + nbx < t_end ? hdr[t + nbx] : uint4{0u, 0u, 0u, 0u};
+    if (!active)
+        return;
     if (t < t_end)
     {
         group_issue_records<NT>(s, hd, cur);
