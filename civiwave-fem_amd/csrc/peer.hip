@@ -145,14 +145,18 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
     __syncthreads();
     if (threadIdx.x == 0)
     {
-        const uint32_t old = __hip_atomic_fetch_add(a.cnt_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // one workgroup (the scalar-only p.Ap step) is its own last arriver: no ticket round trip
+        const uint32_t old = gridDim.x == 1 ? 0u
+                                            : __hip_atomic_fetch_add(a.cnt_ticket, 1u, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1 == gridDim.x)
         {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
             for (uint32_t p = 0; p < a.nranks; ++p)
                 if (p != a.rank)
                     __hip_atomic_store(a.flag[p], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(a.cnt_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (gridDim.x > 1)
+                __hip_atomic_store(a.cnt_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // (2) wait: wave 0, lane p polls peer p's flag line
