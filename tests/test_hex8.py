@@ -196,7 +196,7 @@ def test_gpu_hex8_lattice_z_from_r_solve(monkeypatch):
     for zr in ("0", "1"):
         monkeypatch.setenv("CWF_LAT_ZR", zr)
         s = gpu_hex_system(case)
-        assert _keff_kernel(s).endswith(", true, true, true>" if zr == "1" else ", true, false, true>")
+        assert _keff_kernel(s).rstrip(">").split(", ")[-3:-1] == ["true", "true" if zr == "1" else "false"]
         xs[zr] = np.zeros_like(rhs)
         t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(2000, 1e-6), pcg.PcgVectors(xs[zr], np.zeros_like(rhs))).value()
         assert t.converged
