@@ -1,6 +1,6 @@
 // knobs.hpp -- every environment switch libcwf_hip.so reads, in one place. None is needed for a solve: the
 // defaults are the measured-best configuration (DESIGN.md sections 3 and 6); each switch exists for a test or a
-// same-box A/B (tools/ab_env.sh). knob() refuses (returns NULL for) a name that is not listed here.
+// same-box A/B (tools/gpu_run.sh ab). knob() refuses (returns NULL for) a name that is not listed here.
 #pragma once
 
 #include <cstdlib>
