@@ -122,15 +122,22 @@ def cpu_baseline(case, sK, sM, iters):
                                "converged": bool(o1["telemetry"].converged)})
 
 
-def c3_pmc_traffic(kname):
-    """HBM bytes per launch of kernel `kname` from the newest committed C3 FAST PMC summary that profiled it."""
-    import glob
-
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_fast*_pmc.json")), reverse=True):
+def pmc_traffic(paths, kname, src_hash):
+    """HBM bytes per launch of kernel `kname` from the newest committed PMC summary among `paths` that profiled it
+    AND recorded the running library's source hash of that kernel (cwf_hip_system_keff_source_hash): a profile of an
+    older build of the same template instantiation is not this code's traffic. (None, None) when
+    no profile of the current code exists."""
+    for path in sorted(paths, reverse=True):
         pmc = json.load(open(path))
-        if any(same_kernel(kname, k) for k in pmc.get("kernels", {})):
+        if pmc.get("source_hash") == src_hash and any(same_kernel(kname, k) for k in pmc.get("kernels", {})):
             return pmc.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
+
+
+def c3_pmc_traffic(kname, src_hash):
+    import glob
+
+    return pmc_traffic(glob.glob(os.path.join(ROOT, "profiles", "r*_c3_fast*_pmc.json")), kname, src_hash)
 
 
 def hbm_roofline(L, device, key="c3", steps=2, sample=5, general=False):
@@ -181,7 +188,8 @@ def hbm_roofline(L, device, key="c3", steps=2, sample=5, general=False):
            "kernel": (L.cwf_hip_system_keff_kernel(h) or b"").decode(), "avg_launch_ms": avg,
            "launches": int(n.value), "algorithmic_bytes_per_launch": float(lay_b.value),
            "reference_layout_equiv_gbs": ref_b.value / (avg * 1e-3) / 1e9}
-    out["traffic"], out["traffic_source"] = c3_pmc_traffic(out["kernel"])
+    out["kernel_source_hash"] = (L.cwf_hip_system_keff_source_hash(h) or b"").decode()
+    out["traffic"], out["traffic_source"] = c3_pmc_traffic(out["kernel"], out["kernel_source_hash"])
     st.close()
     st.system.close()
     return out
@@ -442,23 +450,19 @@ def main():
     achieved = alg_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
     ref_equiv = ref_bytes / (avg_keff_ms * 1e-3) / 1e9 if keff_n.value else None
     kname = (L.cwf_hip_system_keff_kernel(h) or b"").decode()
+    src_hash = (L.cwf_hip_system_keff_source_hash(h) or b"").decode()
     traffic, traffic_src = None, None
     tpath = args.traffic
     if tpath == "auto":
         import glob
 
         tag = f"{args.config}_{args.mode}" + ("_hex8" if args.element == "hex8" else "")
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc.json")), reverse=True)
+        cands = glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_pmc.json"))
     else:
         cands = [tpath] if tpath and os.path.exists(tpath) else []
-    for path in cands if world == 1 else []:
-        pmc = json.load(open(path))
-        # only a profile of the same kernel counts (a committed profile of an older kernel is not this one's):
-        # the newest that profiled it
-        if any(same_kernel(kname, k) for k in pmc.get("kernels", {})):
-            traffic = pmc.get("hbm_bytes_per_launch")
-            traffic_src = os.path.relpath(path, ROOT)
-            break
+    if world == 1:
+        # only a profile of the same kernel built from the same sources counts: the newest such
+        traffic, traffic_src = pmc_traffic(cands, kname, src_hash)
     result = None
     stepper.close()
     stepper.system.close()
@@ -492,7 +496,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if (strong and world > 1) or args.scaling == "strong" else "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.mode == "fast" else "f64",
+            # FAST: fp32 element / stencil arithmetic with fp64 dot reductions (configs[4]'s mixed path); PARITY: the
+            # reference's fp64 element math on fp32 data, bit-exact
+            "dtype": "f32 SpMV, f64 reductions" if args.mode == "fast" else "f64",
             "data": ("synthetic (native hex8 block, gravity + tip load)" if args.element == "hex8" else
                      "synthetic (jittered + permuted hex block -> Kuhn tets, gravity + harmonic tip load "
                      "F0 sin(2 pi 5 t) from a 64-point curve, rewritten on the device every step)"
@@ -516,7 +522,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": kname,
+                         "kernel": kname, "kernel_source_hash": src_hash,
                          "avg_launch_ms": avg_keff_ms, "launches": int(keff_n.value),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "reference_layout_bytes_per_launch": ref_bytes,

@@ -1373,6 +1373,19 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
     return 0;
 }
 
+#ifndef CWF_FAST_SRC_HASH
+#define CWF_FAST_SRC_HASH "unknown"
+#endif
+#ifndef CWF_PARITY_SRC_HASH
+#define CWF_PARITY_SRC_HASH "unknown"
+#endif
+const char *cwf_hip_system_keff_source_hash(const cwf_hip_system *h)
+{
+    if (!h)
+        return nullptr;
+    return h->mode != CWF_MODE_FAST || !h->ds.t.ntiles ? CWF_PARITY_SRC_HASH : CWF_FAST_SRC_HASH;
+}
+
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
 {
     if (!h)

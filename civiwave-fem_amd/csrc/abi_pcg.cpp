@@ -18,6 +18,11 @@ std::string pcg_error_message(int code, int iter, std::string *ctx)
         *ctx = "iteration=" + std::to_string(iter);
         return "CG denominator approached zero";  // pcg.cpp:846-849
     }
+    if (code == CWF_ERR_COMM)  // a PEER exchange step's bounded wait (peer.hip): a peer never arrived
+    {
+        *ctx = "step=" + std::to_string(iter);
+        return "peer exchange timed out";
+    }
     if (code == CWF_ERR_RHO_ZERO && iter < 0)
     {
         *ctx = "rho~0";

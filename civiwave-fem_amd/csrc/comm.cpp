@@ -576,6 +576,10 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         return set_error(h, CWF_ERR_ARGUMENT, "rank out of range or taken", "rank=" + std::to_string(rank));
     if (cm->device != h->device)
         return set_error(h, CWF_ERR_ARGUMENT, "communicator and handle are on different devices");
+    // PEER: one member per process, checked before anything is allocated or attached (a failed attach
+    // must not leave h->comm pointing at a communicator the caller then destroys)
+    if (cm->kind == 2 && (cm->peer_member || rank != cm->rank))
+        return set_error(h, CWF_ERR_ARGUMENT, "a peer communicator holds this process's rank only");
     if (plan->local_nodes != h->ds.N || plan->owned_nodes > h->ds.N)
         return set_error(h, CWF_ERR_SIZE, "halo plan does not match the handle",
                          "local_nodes=" + std::to_string(plan->local_nodes) + "\nhandle_nodes=" + std::to_string(h->ds.N));
@@ -645,6 +649,8 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         lattice_plan(t);
     }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
+    if (plan->node_global)
+        h->node_gid.assign(plan->node_global, plan->node_global + plan->local_nodes);
     h->owned_contiguous = true;  // PARITY shards fold chunk partials in global order (comm.cpp parity_setup)
     if (plan->node_global)
         for (uint64_t i = 1; i < plan->owned_nodes; ++i)
@@ -658,12 +664,13 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
     h->rank = rank;
     h->nranks = n;
     if (cm->kind == 2)
-    {
-        if (cm->peer_member || rank != cm->rank)
-            return set_error(h, CWF_ERR_ARGUMENT, "a peer communicator holds this process's rank only");
         if (int st = peer_attach(h))
+        {
+            h->comm = nullptr;  // not attached: cwf_hip_system_destroy must not reach the communicator
+            h->rank = 0;
+            h->nranks = 1;
             return st;
-    }
+        }
     if (cm->kind == 0)
     {
         HIPTRY(h, hipStreamSynchronize(h->stream));

@@ -356,6 +356,7 @@ struct cwf_hip_system
     size_t gp_bytes = 0;  // the slot block gp0 starts (gp1 = gp0 + nranks * pstride)
     uint32_t pstride = 0;
     uint64_t gbegin = 0;            // global id of the first owned node (cwf_hip_system_attach)
+    std::vector<uint64_t> node_gid;  // the plan's global id of every local node (when given): the halo check
     bool owned_contiguous = false;  // owned local i = global gbegin + i
     bool sharded() const { return nranks > 1 || comm != nullptr; }
 };
@@ -374,7 +375,8 @@ struct cwf_hip_comm
     cwf_hip_system *peer_member = nullptr;
     void *mbox = nullptr;
     size_t mbox_bytes = 0;
-    uint32_t *ticket = nullptr;
+    int mbox_kind = 0;  // CWF_PEER_MAILBOX_*
+    uint32_t *ticket = nullptr;  // [0]: the exchange step's ticket; [32]: the sticky device error word
     std::vector<void *> peer_mbox;
     std::vector<uint64_t> peer_nghost, peer_recv_off;
     uint32_t epoch = 0;

@@ -10,15 +10,26 @@
 //           stores and takes a ticket; the last one releases at system scope and stores the step's epoch into
 //           every peer's flag for this rank (system-scope atomic store);
 //   wait    every workgroup polls this rank's flags, one lane per peer, until every peer has reached the epoch
-//           (bounded: a peer that never arrives ends the solve with CWF_ERR_COMM instead of a hang), then acquires
+//           (bounded: a peer that has not arrived after 10 s ends the solve with CWF_ERR_COMM instead of a hang), then acquires
 //           at system scope;
 //   unpack  its share of the received ghost rows and scalar slots into their vectors / slots (system-scope loads).
 //
-// Workgroups wait for peers, not for each other, and the grid is small (<= 128 workgroups of 256 threads, resident
-// together), so every workgroup reaches its ticket. Round 4's first form was three launches (push, wait, unpack)
+// Workgroups wait for peers, not for each other, and the grid is small (<= 64 workgroups of 1024 threads, resident
+// together), so every workgroup reaches its ticket. The ticket is a relaxed agent-scope add: what it orders are the
+// workgroups' write-through (system-scope) stores, each already acknowledged (every storing wave waits vmcnt(0)
+// behind a workgroup barrier before its lane takes the ticket), so the last arriver's system-scope release fence and
+// flag store come after every workgroup's stores have reached the receiver's memory. Round 4's first form was three launches (push, wait, unpack)
 // after the pack pass: 13.7 us per step between two processes on one GPU (profiles/r04ev_peer.log).
 //
-// A mailbox (one hipMalloc per rank, exported with hipIpcGetMemHandle) is a header with the rank's receive layout
+// A comm error is sticky: a step whose wait times out sets the communicator's device error word, and every
+// later step returns at entry (setting the solve's CWF_ERR_COMM again) instead of pushing and spinning to its own
+// timeout, so a dead peer ends a queued batch of exchange steps in one timeout, and the prologue's error survives
+// the init kernel that rewrites the control block.
+//
+// A mailbox (one allocation per rank, exported with hipIpcGetMemHandle: uncached device memory,
+// hipDeviceMallocUncached, so another device's stores over xGMI are seen without relying on the receiver's L2 holding
+// no stale copy; fine-grained or plain device memory where that allocation or its IPC export is refused, recorded in
+// cwf_hip_comm_peer_mailbox_kind) is a header with the rank's receive layout
 // (where each neighbour's ghosts go, read once by the peers at connect), one 64-B flag line per peer, and two
 // copies (by epoch parity) of the scalar-slot area and of the ghost receive area. Two copies suffice: a rank can
 // only push step e + 2 after waiting on step e + 1 of the receiver, which the receiver pushes after unpacking step
@@ -49,7 +60,8 @@ namespace
 constexpr uint64_t kPeerMagic = 0x43574650454552ull;  // "CWFPEER"
 constexpr size_t kHdrBytes = 4096, kFlagLine = 64, kSlot = 4;  // kSlot doubles per rank and gather
 constexpr int kMaxPeerGathers = 2;
-constexpr int kPeerThreads = 1024;  // the fold of a rank's shares is k_fold_pair's 1024-thread fold_all
+constexpr int kPeerThreads = 1024;
+constexpr uint64_t kPeerTimeoutTicks = 10ull * 100000000ull;  // a wait gives a peer 10 s (s_memrealtime: 100 MHz)  // the fold of a rank's shares is k_fold_pair's 1024-thread fold_all
 
 struct MboxHeader  // at offset 0 of every mailbox
 {
@@ -80,6 +92,7 @@ struct PeerStep
     uint32_t *flag[kMaxPeers];        // per rank p: p's flag line for my rank
     uint32_t nranks, rank, epoch;
     uint32_t *cnt_ticket;
+    uint32_t *sticky;  // the communicator's device error word (CWF_ERR_COMM once a wait timed out)
     // wait
     const uint32_t *flags;  // my mailbox's flag lines
     Ctl *ctl;
@@ -97,6 +110,17 @@ struct PeerStep
 __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
 {
     constexpr uint32_t NT = kPeerThreads;
+    // a peer timed out in an earlier step: push nothing, wait for nothing; end the solve (again) with CWF_ERR_COMM
+    if (__hip_atomic_load(a.sticky, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+    {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+        {
+            a.ctl->error = CWF_ERR_COMM;
+            a.ctl->error_iter = (int)a.epoch;
+            a.ctl->active = 0;
+        }
+        return;
+    }
     // (0) workgroup 0: this rank's scalars, folded as k_fold_pair folds them, kept for the push and stored locally
     __shared__ double red[NT / 64], gv[kSlot];
     if (blockIdx.x == 0 && a.fn)
@@ -169,12 +193,13 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
         {
             const uint32_t *f = a.flags + (kFlagLine / 4) * p;
             uint32_t spins = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz wall clock
             while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch)
             {
                 __builtin_amdgcn_s_sleep(4);
-                if (++spins > (1u << 24))  // ~seconds: the peer is gone
+                if ((++spins & 63u) == 0u && __builtin_amdgcn_s_memrealtime() - t0 > kPeerTimeoutTicks)
                 {
-                    ok = false;
+                    ok = false;  // the peer is gone
                     break;
                 }
             }
@@ -186,6 +211,8 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
     __syncthreads();
     if (!ok_s)
     {
+        if (threadIdx.x == 0)
+            __hip_atomic_store(a.sticky, (uint32_t)CWF_ERR_COMM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (blockIdx.x == 0 && threadIdx.x == 0)
         {
             a.ctl->error = CWF_ERR_COMM;
@@ -215,6 +242,39 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
 
 }  // namespace
 
+// the mailbox memory: uncached device memory first (coherent with another device's xGMI stores by construction),
+// then fine-grained, then plain hipMalloc, each only if its IPC export works too (a handle that cannot be exported
+// is no mailbox); cm->mbox_kind records which (CWF_PEER_MAILBOX_*)
+int peer_alloc_mailbox(cwf_hip_system *h, size_t bytes)
+{
+    cwf_hip_comm *cm = h->comm;
+    const unsigned flags[2] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
+    const int kinds[2] = {CWF_PEER_MAILBOX_UNCACHED, CWF_PEER_MAILBOX_FINEGRAINED};
+    for (int i = 0; i < 2; ++i)
+    {
+        void *p = nullptr;
+        if (hipExtMallocWithFlags(&p, bytes, flags[i]) != hipSuccess || !p)
+        {
+            (void)hipGetLastError();
+            continue;
+        }
+        hipIpcMemHandle_t m;
+        if (hipIpcGetMemHandle(&m, p) != hipSuccess)
+        {
+            (void)hipGetLastError();
+            (void)hipFree(p);
+            continue;
+        }
+        cm->mbox = p;
+        cm->mbox_kind = kinds[i];
+        return 0;
+    }
+    if (hipMalloc(&cm->mbox, bytes) != hipSuccess)
+        return set_error(h, CWF_ERR_ALLOC, "failed to allocate the peer mailbox", "bytes=" + std::to_string(bytes));
+    cm->mbox_kind = CWF_PEER_MAILBOX_DEVICE;
+    return 0;
+}
+
 // attach of a PEER comm's member: the mailbox with this rank's receive layout in its header
 int peer_attach(cwf_hip_system *h)
 {
@@ -222,13 +282,14 @@ int peer_attach(cwf_hip_system *h)
     const int n = cm->nranks;
     const uint64_t nghost = h->ds.N - h->ds.Nown;
     const size_t bytes = off_recv(n) + 2 * recv_bytes(nghost);
-    if (hipMalloc(&cm->mbox, bytes) != hipSuccess)
-        return set_error(h, CWF_ERR_ALLOC, "failed to allocate the peer mailbox", "bytes=" + std::to_string(bytes));
+    if (int st = peer_alloc_mailbox(h, bytes))
+        return st;
     cm->mbox_bytes = bytes;
-    if (hipMalloc(reinterpret_cast<void **>(&cm->ticket), 64) != hipSuccess)
+    // the ticket (line 0) and the sticky error word (line 1), on lines of their own
+    if (hipMalloc(reinterpret_cast<void **>(&cm->ticket), 256) != hipSuccess)
         return set_error(h, CWF_ERR_ALLOC, "failed to allocate device buffer");
     HIPTRY(h, hipMemset(cm->mbox, 0, bytes));
-    HIPTRY(h, hipMemset(cm->ticket, 0, 64));
+    HIPTRY(h, hipMemset(cm->ticket, 0, 256));
     MboxHeader hd{};
     hd.magic = kPeerMagic;
     hd.nranks = (uint64_t)n;
@@ -310,6 +371,7 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
     a.rank = (uint32_t)h->rank;
     a.epoch = epoch;
     a.cnt_ticket = cm->ticket;
+    a.sticky = cm->ticket + 32;
     a.flags = reinterpret_cast<const uint32_t *>(static_cast<char *>(cm->mbox) + off_flags());
     a.ctl = h->ctl;
     const uint64_t nghost = h->ds.N - h->ds.Nown;
@@ -420,11 +482,13 @@ int cwf_hip_comm_peer_connect(cwf_hip_comm *cm, const uint8_t *handles)
 
 // `steps` exchange steps shaped like the FAST iteration's second one (the {r.r, r.z} all-gather and the z halo;
 // the first, p.Ap, has no halo) on h's stream, hipEvent-timed: the per-step latency the 8-GPU projection uses
-// (every rank calls it)
+// (every rank calls it). The untimed first step checks the halo's contents; z is clobbered (a solve recomputes it)
 int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_step)
 {
     if (!h || !us_per_step || steps < 1 || !h->sharded() || !h->comm)
         return set_error(h, CWF_ERR_ARGUMENT, "an attached handle and steps >= 1");
+    if (h->comm->kind == 0 && h->nranks > 1)  // its exchange needs every member of the process (solve_pcg_group)
+        return set_error(h, CWF_ERR_UNSUPPORTED, "time the exchange of a RCCL or PEER communicator");
     (void)hipSetDevice(h->device);
     hipEvent_t e0, e1;
     HIPTRY(h, hipEventCreate(&e0));
@@ -439,7 +503,32 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
         fast_fold_rrz(h, 0, h->stream);
         return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_rrz, 2}}, vecs);
     };
+    // the first (untimed) step carries a known pattern: every owned row of z = f(global id), the ghosts poisoned, and
+    // afterwards every ghost row must hold its owner's f(global id). A transport that delivers stale or misplaced
+    // rows (or none) fails the trial here instead of a solve later (bench.py --comm auto then takes RCCL)
+    const uint64_t N = h->ds.N, Nown = h->ds.Nown;
+    const bool check = h->node_gid.size() == N && N > Nown;
+    const auto pat = [&](uint64_t n, int k) { return (float)((h->node_gid[n] * 3u + (uint64_t)k) % 4194304u + 1u); };
+    std::vector<float> zh;
+    if (check)
+    {
+        zh.assign(3 * N, std::nanf(""));
+        for (uint64_t n = 0; n < Nown; ++n)
+            for (int k = 0; k < 3; ++k)
+                zh[3 * n + k] = pat(n, k);
+        HIPTRY(h, hipMemcpyAsync(h->z, zh.data(), zh.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+    }
     int st = step();  // warm
+    if (!st && check)
+    {
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+        HIPTRY(h, hipMemcpy(zh.data(), h->z, zh.size() * sizeof(float), hipMemcpyDeviceToHost));
+        for (uint64_t n = Nown; n < N && !st; ++n)
+            for (int k = 0; k < 3 && !st; ++k)
+                if (!(zh[3 * n + k] == pat(n, k)))
+                    st = set_error(h, CWF_ERR_COMM, "halo check failed",
+                                   "ghost=" + std::to_string(n - Nown) + "\nglobal=" + std::to_string(h->node_gid[n]));
+    }
     if (!st && hipEventRecord(e0, h->stream) != hipSuccess)
         st = set_error(h, CWF_ERR_HIP, "hipEventRecord");
     for (int i = 0; i < steps && !st; ++i)
@@ -450,7 +539,33 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     *us_per_step = 1e3 * (double)ms / steps;
-    return st;
+    if (st)
+        return st;
+    // a step that timed out (a peer that never arrived) only shows in the control block: report it, then clear the
+    // solve fields so the next solve starts clean (the communicator's sticky word stays set: it is dead)
+    Ctl c{};
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    HIPTRY(h, hipMemcpy(&c, h->ctl, sizeof c, hipMemcpyDeviceToHost));
+    if (c.error)
+    {
+        const int code = c.error, at = c.error_iter;
+        c.error = 0;
+        c.error_iter = 0;
+        HIPTRY(h, hipMemcpy(h->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+        return set_error(h, code, code == CWF_ERR_COMM ? "peer exchange timed out" : "exchange step failed",
+                         "step=" + std::to_string(at));
+    }
+    return 0;
+}
+
+int cwf_hip_comm_peer_mailbox_kind(const cwf_hip_comm *cm, int *kind)
+{
+    if (!cm || !kind || cm->kind != 2)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "not a peer communicator");
+    if (!cm->mbox)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "attach the rank's handle first");
+    *kind = cm->mbox_kind;
+    return 0;
 }
 
 }  // extern "C"

@@ -560,6 +560,32 @@ int cwf_scenario_output_frame(cwf_scenario *sc, const char *out_root)
                                sc->probes.size(), &f, sc->t_sim, idx);
 }
 
+int cwf_scenario_state(cwf_scenario *sc, float *u, float *v, float *a, float *element_fields, float *node_fields)
+{
+    if (!sc)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "null pointer");
+    if (!sc->st)
+        return set_error(nullptr, CWF_ERR_ARGUMENT, "scenario was created CWF_SCENARIO_PACK_ONLY");
+    const uint64_t D = 3 * sc->N;
+    float *out[3] = {u, v, a};
+    for (int w = 0; w < 3; ++w)
+        if (out[w])
+            if (int st = cwf_hip_stepper_get_state(sc->st, w, out[w], D, CWF_PTR_HOST))
+                return st;
+    if (!element_fields && !node_fields)
+        return 0;
+    if (int st = cwf_hip_stepper_get_state(sc->st, 0, sc->u.data(), D, CWF_PTR_HOST))
+        return st;
+    if (int st = cwf_hip_derived_fields(sc->sys, sc->u.data(), D, CWF_PTR_HOST, sc->efield.data(), sc->nfield.data(),
+                                        CWF_PTR_HOST))
+        return st;
+    if (element_fields)
+        std::memcpy(element_fields, sc->efield.data(), sc->efield.size() * sizeof(float));
+    if (node_fields)
+        std::memcpy(node_fields, sc->nfield.data(), sc->nfield.size() * sizeof(float));
+    return 0;
+}
+
 int cwf_scenario_packed(const cwf_scenario *sc, const char *name, const void **data, uint64_t *bytes)
 {
     if (!sc || !name || !data || !bytes)

@@ -20,6 +20,7 @@ PTR_HOST, PTR_DEVICE = 0, 1
 MODE_PARITY, MODE_FAST = 0, 1
 DESC_KEEP_NODE_ORDER = 1  # cwf_system_desc.reserved flag (cwf_hip.h)
 SCENARIO_TIME_VARYING_LOADS, SCENARIO_PACK_ONLY = 1, 2  # cwf_scenario_create flags
+PEER_MAILBOX_DEVICE, PEER_MAILBOX_FINEGRAINED, PEER_MAILBOX_UNCACHED = 0, 1, 2  # cwf_hip_comm_peer_mailbox_kind
 
 STATUS = {
     0: "CWF_OK", -1: "CWF_ERR_SIZE", -2: "CWF_ERR_NODE_RANGE", -3: "CWF_ERR_MATERIAL_RANGE",
@@ -135,6 +136,7 @@ def load() -> C.CDLL:
         "cwf_hip_bandwidth_probe": ([i32, u64, i32, P], i32),
         "cwf_hip_system_keff_traffic": ([P, P, P], i32),
         "cwf_hip_system_keff_kernel": ([P], C.c_char_p),
+        "cwf_hip_system_keff_source_hash": ([P], C.c_char_p),
         "cwf_lattice_describe": ([P, i32, P, P, P], i32),
         "cwf_hip_system_set_timing": ([P, i32], i32),
         "cwf_hip_system_timing": ([P, P, P], i32),
@@ -167,6 +169,7 @@ def load() -> C.CDLL:
         "cwf_hip_comm_peer_handle": ([P, P], i32),
         "cwf_hip_comm_peer_connect": ([P, P], i32),
         "cwf_hip_comm_time_exchange": ([P, i32, P], i32),
+        "cwf_hip_comm_peer_mailbox_kind": ([P, P], i32),
         "cwf_hip_system_attach": ([P, P, i32, P], i32),
         "cwf_hip_solve_pcg_group": ([P, i32, P, P, P, P, i32, P], i32),
         "cwf_preprocess_tets": ([u64, u64, P, P, P, P, u64, P, P, P, P, P, P, P, P], i32),
@@ -191,6 +194,7 @@ def load() -> C.CDLL:
         "cwf_scenario_info": ([P, P, P, P], i32),
         "cwf_scenario_step": ([P, i32, P], i32),
         "cwf_scenario_output_frame": ([P, C.c_char_p], i32),
+        "cwf_scenario_state": ([P, P, P, P, P, P], i32),
         "cwf_scenario_packed": ([P, C.c_char_p, P, P], i32),
         "cwf_scenario_external_force": ([P, f64, P, u64], i32),
         "cwf_scenario_destroy": ([P], None),

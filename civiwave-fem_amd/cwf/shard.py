@@ -200,6 +200,13 @@ class Comm:
             raise RuntimeError(f"peer handle: {_lib.last_error(None)}")
         return bytes(buf)
 
+    def mailbox_kind(self) -> int:
+        """_lib.PEER_MAILBOX_{DEVICE,FINEGRAINED,UNCACHED}: the memory this rank's mailbox was allocated in"""
+        k = C.c_int(-1)
+        if _lib.load().cwf_hip_comm_peer_mailbox_kind(self._h, C.byref(k)):
+            raise RuntimeError(f"peer mailbox kind: {_lib.last_error(None)}")
+        return k.value
+
     def connect(self, handles: list):
         blob = b"".join(handles)
         buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)

@@ -147,6 +147,9 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
 /* Name of the kernel the handle's K_eff launches in its current mode ("k_keff_lattice", "k_keff_groups_pipe",
  * "k_keff_tiles_pipe", "k_keff_tiles", "k_keff_hex_tiles" or "k_keff_parity"); NULL for a NULL handle. */
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
+/* 16 hex digits: a hash of the source files and build flags of the translation unit that holds that kernel
+ * (csrc/Makefile FAST_SRC / PARITY_SRC), so a committed PMC profile can be matched to the code that ran */
+const char *cwf_hip_system_keff_source_hash(const cwf_hip_system *h);
 /* Structured-block introspection (host only, no device; not a reference interface): whether a FAST handle
  * created from the tet4 `desc` runs the structured Kuhn-block stencil (lattice.cpp; native hex8 blocks run their
  * own 27-point stencil and are not described here). Returns 1 and fills dims (nodes per
@@ -320,8 +323,19 @@ int cwf_hip_comm_peer_handle(cwf_hip_comm *comm, uint8_t *handle /* [CWF_IPC_HAN
 int cwf_hip_comm_peer_connect(cwf_hip_comm *comm, const uint8_t *handles /* [nranks * CWF_IPC_HANDLE_BYTES] */);
 /* `steps` exchange steps shaped like the FAST PCG iteration's second one (the {r.r, r.z} all-gather and the z
  * halo) on the attached handle's stream, hipEvent-timed: microseconds per step (collective: every rank calls);
- * any communicator kind */
+ * any communicator kind. An untimed first step carries a known pattern in z (owned rows = f(global id), the
+ * plan's node_global) and every ghost row must arrive as its owner's value, else CWF_ERR_COMM "halo check failed"
+ * {ghost, global}; z is clobbered (the next solve recomputes it). */
 int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_step);
+/* the memory this rank's PEER mailbox was allocated in (after attach): uncached device memory
+ * (hipDeviceMallocUncached: another device's xGMI stores are visible without trusting the receiver's L2), else
+ * fine-grained, else plain device memory when neither allocation can be IPC-exported. A PEER step whose wait times
+ * out marks the communicator dead (a sticky device word): every later step returns CWF_ERR_COMM at once, and
+ * cwf_hip_comm_time_exchange reports such a trial as CWF_ERR_COMM. */
+#define CWF_PEER_MAILBOX_DEVICE 0
+#define CWF_PEER_MAILBOX_FINEGRAINED 1
+#define CWF_PEER_MAILBOX_UNCACHED 2
+int cwf_hip_comm_peer_mailbox_kind(const cwf_hip_comm *comm, int *kind);
 
 /* Make `h` (created from a shard's local desc with CWF_DESC_KEEP_NODE_ORDER) rank `rank` of `comm` with the
  * shard's halo plan. Afterwards solve_pcg / stepper_step are collective: scalars are all-gathered and folded
@@ -456,6 +470,11 @@ int cwf_scenario_step(cwf_scenario *sc, int paused, cwf_step_telemetry *telemetr
 /* derived fields of the last stepped frame -> <out_root>/vtu/frame_%05u.vtu every vtu_stride frames
  * and one probe row per probe to <out_root>/probes/probes.csv */
 int cwf_scenario_output_frame(cwf_scenario *sc, const char *out_root);
+/* the Stepper's state after the last step (newmark_stepper.hpp:92-190: the pack's displacement / velocity /
+ * acceleration node buffers, f32 [3N] each) and the derived fields OutputManager::handle_frame computes from it
+ * (output_manager.cpp:49-87 -> derived_fields.cpp:139-211: element f32 [13E], node f32 [13N], the layout of
+ * cwf_hip_derived_fields); any pointer may be NULL */
+int cwf_scenario_state(cwf_scenario *sc, float *u, float *v, float *a, float *element_fields, float *node_fields);
 /* read-only view of one packed host buffer (pack.hpp:93-183 names): position0, external_force, bc_mask,
  * bc_value, lumped_mass, lumped_mass64, connectivity, gradients, volume, material_index, offsets,
  * element_indices, local_indices. Unknown name: CWF_ERR_ARGUMENT. */

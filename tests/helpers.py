@@ -58,3 +58,28 @@ def shard_oracle(sh, case, sK, sM):
                       sh.lumped_mass, offsets, elem, loc)
     stiff = np.concatenate([np.asarray(m.stiffness, np.float64).reshape(-1) for m in case.materials])
     return O.System(packed, stiff, sh.bc_mask, sK, sM, 256)
+
+
+def dense_stiffness(P, coords, tets, stiffness):
+    """The dense CPU solver's K (solver.cpp:159-378) from fp64 gradients/volumes (pre::Outputs, not the f32 pack)."""
+    tets = np.asarray(tets)
+    E = tets.shape[0]
+    g64 = np.zeros((E, 12))
+    v64 = np.zeros(E)
+    for e in range(E):
+        p = coords[tets[e]]
+        e0, e1, e2 = p[1] - p[0], p[2] - p[0], p[3] - p[0]
+        c = np.array([e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]])
+        v6 = e0[0] * c[0] + e0[1] * c[1] + e0[2] * c[2]
+        inv6 = -1.0 / v6
+
+        def cr(a, b):
+            return np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]])
+
+        g = [cr(p[2] - p[1], p[3] - p[1]), cr(p[3] - p[0], p[2] - p[0]), cr(p[1] - p[0], p[3] - p[0]),
+             cr(p[2] - p[0], p[1] - p[0])]
+        g64[e] = np.concatenate(g) * inv6
+        v64[e] = abs(v6) / 6.0
+    return O.dense_assemble(O.Packed(P.node_count, E, P.connectivity, P.gradients, P.volume, P.material_index,
+                                     P.lumped_mass64, P.lumped_mass, P.offsets, P.element_indices, P.local_indices),
+                            tets, g64, v64, np.asarray(stiffness))

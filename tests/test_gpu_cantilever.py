@@ -1,0 +1,145 @@
+"""The reference's own YAML scenario on the GPU: tests/data/cantilever.{yaml,msh} of the
+reference (copied under tests/golden/data) through the native scenario driver -- cwf_scenario_create (device
+handle, not CWF_SCENARIO_PACK_ONLY) and cwf_scenario_step -- for three adaptive-dt Newmark frames.
+
+Checked per frame:
+- PARITY: u, v, a bit for bit against the oracle's Stepper CPU branch (newmark_stepper.cpp:1005-1379) built from
+  the scenario's own packed buffers, the step telemetry (iterations, fp64 residual, dt) with ==;
+- PARITY: u, v, a within the tolerances of the reference's newmark_stepper_test.cpp:232-236 (3e-4, 3e-4, 3e-3) of
+  the dense CPU Newmark solve (solver.cpp:159-378, restated in the oracle) chained from the same start state;
+- PARITY: element strain/stress/von Mises and nodal fields from cwf_hip_derived_fields (via cwf_scenario_state)
+  bit for bit against the oracle's derived_fields (derived_fields.cpp:139-211);
+- FAST: the same within the tolerances stated below.
+Both the reference's load path (loads evaluated once at t = 0, newmark_stepper.cpp:1369-1379) and the viewer's
+time-varying path (the traction under load_curve1 re-evaluated at each step's start, viewer.cpp:262-266) run.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from cwf import _lib, pack, run
+from cwf.physics import compute_rayleigh, effective_scalars, make_coefficients
+from helpers import assert_bitwise, dense_stiffness, oracle_system
+
+pytestmark = pytest.mark.gpu
+
+YAML = os.path.join(os.path.dirname(__file__), "golden", "data", "cantilever.yaml")
+STEPS = 3
+
+
+class DeviceScenario:
+    def __init__(self, path, mode, flags=0):
+        self.L = _lib.load()
+        self.h = C.c_void_p()
+        rc = self.L.cwf_scenario_create(os.fsencode(path), mode, 0, flags, C.byref(self.h))
+        assert rc == 0, _lib.last_error(None)
+        n, e, d = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        assert self.L.cwf_scenario_info(self.h, C.byref(n), C.byref(e), C.byref(d)) == 0
+        self.N, self.E, self.D = n.value, e.value, d.value
+
+    def packed(self, name, dtype):
+        data, nbytes = C.c_void_p(), C.c_uint64()
+        assert self.L.cwf_scenario_packed(self.h, name.encode(), C.byref(data), C.byref(nbytes)) == 0
+        return np.frombuffer(C.string_at(data, nbytes.value), dtype).copy()
+
+    def step(self):
+        tel = _lib.StepTelemetryC()
+        assert self.L.cwf_scenario_step(self.h, 0, C.byref(tel)) == 0, _lib.last_error(None)
+        return tel
+
+    def state(self):
+        u, v, a = (np.zeros(self.D, np.float32) for _ in range(3))
+        el = np.zeros((self.E, 13), np.float32)
+        nd = np.zeros((self.N, 13), np.float32)
+        assert self.L.cwf_scenario_state(self.h, _lib.ptr(u), _lib.ptr(v), _lib.ptr(a), _lib.ptr(el),
+                                         _lib.ptr(nd)) == 0, _lib.last_error(None)
+        return u, v, a, el, nd
+
+    def external_force(self, t):
+        out = np.zeros(self.D, np.float32)
+        assert self.L.cwf_scenario_external_force(self.h, t, _lib.ptr(out), self.D) == 0
+        return out
+
+    def close(self):
+        self.L.cwf_scenario_destroy(self.h)
+
+
+def _oracle_stepper(cfg, P, mats):
+    r = compute_rayleigh(cfg.damping)
+    sK, sM = effective_scalars(make_coefficients(cfg.time.initial_dt), r)
+    o = oracle_system(P, mats, sK, sM)
+    st = O.Stepper(o, P.external_force, P.bc_value, (r.alpha, r.beta), cfg.solver.runtime_tolerance,
+                   cfg.solver.pause_tolerance, cfg.solver.max_iterations, cfg.time.initial_dt,
+                   adaptive=cfg.time.adaptive, min_dt=cfg.time.min_dt, max_dt=cfg.time.max_dt)
+    return st, r
+
+
+@pytest.mark.parametrize("varying", [False, True], ids=["loads_at_t0", "time_varying_loads"])
+@pytest.mark.parametrize("mode", [_lib.MODE_PARITY, _lib.MODE_FAST], ids=["parity", "fast"])
+def test_reference_cantilever_scenario_on_device(mode, varying):
+    cfg, m, P, mats = run.load_scenario(YAML)
+    assert (P.node_count, P.element_count) == (4, 1)
+    flags = _lib.SCENARIO_TIME_VARYING_LOADS if varying else 0
+    sc = DeviceScenario(YAML, mode, flags)
+    try:
+        # the device scenario packed exactly the Python packing the oracle is built from
+        for name, want in (("connectivity", P.connectivity), ("gradients", P.gradients), ("volume", P.volume),
+                           ("lumped_mass", P.lumped_mass), ("bc_mask", P.bc_mask),
+                           ("external_force", P.external_force)):
+            want = np.ascontiguousarray(want).reshape(-1)
+            assert sc.packed(name, want.dtype).tobytes() == want.tobytes(), name
+        ost, r = _oracle_stepper(cfg, P, mats)
+        K = dense_stiffness(P, m.coords, m.tets, mats[0].stiffness)
+        mass = np.repeat(P.lumped_mass64, 3)
+        mask = ((np.repeat(P.bc_mask, 3) & np.tile(np.array([1, 2, 4], np.uint32), P.node_count)) != 0)
+        du, dv, da = (np.zeros(P.dof_count) for _ in range(3))
+        t = 0.0
+        for k in range(STEPS):
+            load = pack.assemble_load_vector(m, cfg, P.lumped_mass64, t if varying else 0.0)
+            if varying:
+                f = sc.external_force(t)
+                assert f.tobytes() == pack._safe_f32(load).tobytes()
+                ost.set_external_force(f)
+            dt = ost.time_step
+            tel = sc.step()
+            otel = ost.step(t)
+            u, v, a, el, nd = sc.state()
+            assert tel.pcg.converged and otel.pcg.converged
+            if mode == _lib.MODE_PARITY:
+                assert tel.pcg.iterations == otel.pcg.iterations, k
+                assert tel.pcg.residual_norm == otel.pcg.residual_norm, k
+                assert (tel.time_step, tel.simulation_time) == (otel.time_step, otel.simulation_time), k
+                assert_bitwise(u, ost.u, f"u frame {k}")
+                assert_bitwise(v, ost.v, f"v frame {k}")
+                assert_bitwise(a, ost.a, f"a frame {k}")
+            else:
+                # FAST: fp32 element math with fp64 reductions; a 3-DOF system converges to the same tolerance
+                scale = max(np.max(np.abs(ost.u)), 1e-30)
+                assert np.max(np.abs(u - ost.u)) <= 1e-4 * scale, k
+                assert np.max(np.abs(v - ost.v)) <= 1e-4 * max(np.max(np.abs(ost.v)), 1e-30), k
+                assert np.max(np.abs(a - ost.a)) <= 1e-4 * max(np.max(np.abs(ost.a)), 1e-30), k
+                assert tel.time_step == otel.time_step, k
+            # the dense CPU Newmark step from the same state (newmark_stepper_test.cpp:198-239 tolerances)
+            dense = O.dense_newmark_step(K, mass, load, mask.astype(np.uint8), np.zeros(P.dof_count),
+                                         (r.alpha, r.beta), dt, du, dv, da, cfg.solver.runtime_tolerance,
+                                         cfg.solver.max_iterations)
+            assert np.max(np.abs(u - dense["u"])) <= 3e-4
+            assert np.max(np.abs(v - dense["v"])) <= 3e-4
+            assert np.max(np.abs(a - dense["a"])) <= 3e-3
+            du, dv, da = u.astype(np.float64), v.astype(np.float64), a.astype(np.float64)
+            # derived fields of the frame (OutputManager::handle_frame's compute_derived_fields)
+            oel, ond = oracle_system(P, mats, 1.0, 0.0).derived_fields(u)
+            if mode == _lib.MODE_PARITY:
+                assert_bitwise(el, oel, f"element fields frame {k}")
+                assert_bitwise(nd, ond, f"node fields frame {k}")
+            else:
+                tol = 1e-5 * max(np.max(np.abs(oel)), 1e-30)
+                assert np.max(np.abs(el - oel)) <= tol and np.max(np.abs(nd - ond)) <= tol, k
+            t = tel.simulation_time + tel.time_step
+        # the traction (1e5 Pa on LOAD_FACE under load_curve1) acts once the curve is re-evaluated: the tip moves
+        assert np.any(u != 0.0)
+    finally:
+        sc.close()

@@ -7,7 +7,11 @@ groups; the kernels, fold orders and halo plans above them are the ones the LOCA
 - so does the FAST iteration on a global-mesh node partition (the fan-group tiles);
 - a PARITY solve over PEER is refused (its chunk-partial all-gathers stay on RCCL / LOCAL);
 - the exchange latency per step is measured (printed; DESIGN.md section 7 uses it). Two processes on one GPU
-  share its CUs, so this is the protocol's latency on one device, not an xGMI figure."""
+  share its CUs, so this is the protocol's latency on one device, not an xGMI figure;
+- the mailboxes are uncached device memory (hipDeviceMallocUncached, IPC-exported): another device's stores are
+  visible to the receiver without trusting its L2 (VERDICT r4 item 1);
+- a rank that connects and then never exchanges ends the others' solve with CWF_ERR_COMM within the wait's bound
+  (10 s), and the exchange trial cwf_hip_comm_time_exchange reports the dead communicator."""
 import multiprocessing as mp
 import os
 import tempfile
@@ -80,6 +84,7 @@ def test_peer_lattice_slabs_equal_local(nranks):
     x = _assemble(out, glob.packing.node_count)
     for d in out.values():
         assert d["kernel"].startswith("k_keff_lattice"), d["kernel"]
+        assert d["mailbox_kind"] == _lib.PEER_MAILBOX_UNCACHED, d["mailbox_kind"]
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
         # refused (the slabs are not whole reduction chunks, and PEER carries the FAST schedule only), never a hang
         assert d["parity_error"] and ("FAST schedule" in d["parity_error"] or "whole" in d["parity_error"]
@@ -123,3 +128,14 @@ def test_peer_global_partition_equals_local():
     assert_bitwise(_assemble(out, P.node_count), xl.reshape(-1), "PEER global partition x vs LOCAL")
     print("PEER exchange step, 2 processes on one GPU: "
           + ", ".join(f"rank {k} {d['exchange_us']:.2f} us" for k, d in sorted(out.items())))
+
+
+def test_peer_dead_rank_ends_the_solve_with_comm_error():
+    shape = (9, 7, 4)
+    out = _run(dict(slab=shape, tol=1e-6, max_iterations=400, dead_rank=1), 2)
+    live = out[0]
+    assert out[1]["dead"] and not live["dead"]
+    assert live["error"] == "peer exchange timed out", live["error"]
+    # one bounded wait (10 s), not one per queued exchange step
+    assert live["seconds"] < 60.0, live["seconds"]
+    assert live["trial_error"] and "timed out" in live["trial_error"], live["trial_error"]

@@ -15,7 +15,7 @@ import pytest
 
 import oracle as O
 from cwf import meshgen, pack, physics, scenarios
-from helpers import kuhn16_reference_case, oracle_system
+from helpers import dense_stiffness, kuhn16_reference_case, oracle_system
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -103,31 +103,7 @@ def test_degenerate_curve_segments():
 
 
 def _dense_setup(case):
-    P = case.packing
-    tets = case.mesh.tets
-    E = tets.shape[0]
-    coords = case.mesh.coords
-    # fp64 gradients/volumes (pre::Outputs, not the f32 pack) for the dense path
-    g64 = np.zeros((E, 12))
-    v64 = np.zeros(E)
-    for e in range(E):
-        p = coords[tets[e]]
-        e0, e1, e2 = p[1] - p[0], p[2] - p[0], p[3] - p[0]
-        c = np.array([e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]])
-        v6 = e0[0] * c[0] + e0[1] * c[1] + e0[2] * c[2]
-        inv6 = -1.0 / v6
-
-        def cr(a, b):
-            return np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]])
-
-        g = [cr(p[2] - p[1], p[3] - p[1]), cr(p[3] - p[0], p[2] - p[0]), cr(p[1] - p[0], p[3] - p[0]),
-             cr(p[2] - p[0], p[1] - p[0])]
-        g64[e] = np.concatenate(g) * inv6
-        v64[e] = abs(v6) / 6.0
-    K = O.dense_assemble(O.Packed(P.node_count, E, P.connectivity, P.gradients, P.volume, P.material_index,
-                                  P.lumped_mass64, P.lumped_mass, P.offsets, P.element_indices, P.local_indices),
-                         tets, g64, v64, np.asarray(case.materials[0].stiffness))
-    return K
+    return dense_stiffness(case.packing, case.mesh.coords, case.mesh.tets, case.materials[0].stiffness)
 
 
 def test_matrix_free_apply_matches_dense_like_pcg_test():

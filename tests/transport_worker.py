@@ -145,6 +145,33 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
             time.sleep(0.05)
         comm.connect([open(os.path.join(rdv, f"rank{p}.bin"), "rb").read() for p in range(nranks)])
         kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
+        mkind = comm.mailbox_kind()
+        if spec.get("dead_rank") is not None:
+            # one rank connects and then never exchanges; the others' solve must end with CWF_ERR_COMM, in bounded time
+            if rank == spec["dead_rank"]:
+                queue.put((rank, "ok", dict(dead=True, mailbox_kind=mkind)))
+                t0 = time.time()
+                while not os.path.exists(os.path.join(rdv, "done")) and time.time() - t0 < 200:
+                    time.sleep(0.05)
+            else:
+                x = np.zeros(3 * sh.local_nodes, np.float32)
+                t0 = time.time()
+                res = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]),
+                                    pcg.PcgVectors(x, None))
+                el = time.time() - t0
+                us_err = None
+                try:
+                    shard.Comm.time_exchange(s, 4)
+                except RuntimeError as e:
+                    us_err = str(e)
+                with open(os.path.join(rdv, "done"), "w") as fh:
+                    fh.write("1")
+                queue.put((rank, "ok", dict(dead=False, mailbox_kind=mkind, seconds=el,
+                                            error=None if res.has_value() else res.error().message,
+                                            trial_error=us_err)))
+            s.close()
+            comm.close()
+            return
         x = np.zeros(3 * sh.local_nodes, np.float32)
         res = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]), pcg.PcgVectors(x, None))
         if not res.has_value():
@@ -159,7 +186,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         own = 3 * sh.owned_nodes
         queue.put((rank, "ok", dict(telemetry=(t.iterations, t.converged, t.residual_norm), kernel=kern,
                                     nodes=sh.node_global[: sh.owned_nodes].astype(np.int64), x=x[:own].copy(),
-                                    exchange_us=us, parity_error=perr)))
+                                    exchange_us=us, parity_error=perr, mailbox_kind=mkind)))
         s.close()
         comm.close()
     except Exception as e:

@@ -59,7 +59,14 @@ def main():
     if a.json:
         sel = {k: v for k, v in out.items() if not a.kernel or any(s in k or norm(s) == norm(k) for s in a.kernel)}
         total = sum(v["hbm_bytes_per_launch"] or 0 for v in sel.values())
-        json.dump(dict(kernels=sel, hbm_bytes_per_launch=total,
+        # provenance: the source hash of the profiled kernel as the profiled bench run printed it (bench.py only takes
+        # this file's traffic for a library built from the same sources)
+        src_hash = None
+        for log in sorted(glob.glob(os.path.join(a.dir, "bench_*.log"))):
+            for line in open(log, errors="replace"):
+                if line.startswith('{"metric"'):
+                    src_hash = src_hash or json.loads(line)["roofline"].get("kernel_source_hash")
+        json.dump(dict(kernels=sel, hbm_bytes_per_launch=total, source_hash=src_hash,
                        note="FETCH_SIZE x2 x1024 + WRITE_SIZE x1024 per launch, summed over the selected "
                             "kernels (MI355X_MICROARCH.md HBM section)"), open(a.json, "w"), indent=1)
 
