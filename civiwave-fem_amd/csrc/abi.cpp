@@ -1160,6 +1160,15 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
     for (float **v : {&h->x, &h->r, &h->p, &h->p2, &h->p3, &h->p4, &h->z, &h->Ap, &h->rhs, &h->tmp})
         if (int st = dalloc(h, v, D))
             return bail(st);
+    if (s.t.lat && s.t.lcls)  // the fused lattice iteration's second r / Ap and its shares (lattice_fused.inc)
+    {
+        if (int st = dalloc(h, &h->r2, D))
+            return bail(st);
+        if (int st = dalloc(h, &h->ap2, D))
+            return bail(st);
+        if (int st = dalloc(h, &h->fsh, 2ull * 5 * std::max<uint32_t>(s.t.lnwork, 1u)))
+            return bail(st);
+    }
     if (int st = dalloc(h, &h->inv, 9 * N))
         return bail(st);
     if (int st = dalloc(h, &h->inv6, 4 * N))
@@ -1352,6 +1361,12 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
+        if (s.t.lat && fast_fused(h))  // the fused iteration (lattice_fused.inc): per owned node r_(j-1), Ap_(j-1),
+        {                              // p_(j-1), the class byte and x read, r_j, p_j, Ap_j and x written; the mass
+                                       // of the shell's nodes (the strict interior's is one value when lmu)
+            *layout_bytes = (uint64_t)s.Nown * (4 * 12 + 1 + 4 * 12) + 4ull * (s.t.lmu ? s.t.lnshell : s.Nown);
+            return 0;
+        }
         if (s.t.lat)  // per owned node: z and p_old read, the new p and the row value written; the mass read
         {             // (only the shell's when the strict interior's is one value, lmu)
             *layout_bytes = (uint64_t)s.Nown * (12 + 12 + 12 + 12 + (s.t.lmu && s.t.lzr ? 1 : 0)) +
@@ -1400,6 +1415,13 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
         if (compact)
             return h->ds.iso ? "k_keff_parity_tile<true, false, false, true>" : "k_keff_parity_tile<false, false, false, true>";
         return h->ds.iso ? "k_keff_parity_tile<true, false, true, false>" : "k_keff_parity_tile<false, false, true, false>";
+    }
+    if (t.lat && fast_fused(h))  // the fused iteration's one launch (lattice_fused.inc)
+    {
+        static thread_local char name[96];
+        snprintf(name, sizeof name, "k_pcg_lattice<%s, %s, %s, %s>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lpstride ? "true" : "false");
+        return name;
     }
     if (t.lat)  // as rocprofv3 names it, less the namespaces
     {

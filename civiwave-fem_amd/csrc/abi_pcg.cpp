@@ -64,7 +64,10 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (cwf_hip_system *m : g)
             HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
-    if (sharded)
+    const bool fused = fast && fast_fused(h);  // one launch per iteration (lattice_fused.inc)
+    if (fused)
+        fast_fused_init(h, rhs[0], set.relative_tolerance, st);
+    else if (sharded)
     {
         if (int e = fast ? sharded_pcg_init(g, rhs, set.relative_tolerance)
                          : sharded_parity_init(g, rhs, set.relative_tolerance))
@@ -131,7 +134,9 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         {
             const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
             hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
-            if (fast)
+            if (fused)
+                fast_fused_iteration(h, (unsigned)(enq + i), st, e0, e1);
+            else if (fast)
             {
                 if (int e = fast_pcg_iteration_group(g, rhs, (unsigned)(enq + i), e0, e1))
                     return e;
@@ -144,7 +149,9 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             else
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
-        if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
+        if (fused)  // convergence of the batch's last launch (repeated idempotently by the next launch's start)
+            fast_fused_check(h, (unsigned)(enq + nb), st);
+        else if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
             for (cwf_hip_system *m : g)
                 fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
         HIPTRY(h, hipGetLastError());
@@ -154,7 +161,9 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         if (set.check_interval <= 0)
             batch = std::min<uint64_t>(batch * 2, kMaxBatch);
     }
-    if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
+    if (fused)  // x is updated in every launch; the solve's r output is the last launch's
+        fast_fused_finish(h, st);
+    else if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
         for (size_t i = 0; i < g.size(); ++i)
             fast_flush_x(g[i], rhs[i], g[i]->stream);
     if (sharded)  // ghost x <- owners, so node-wise stepper updates stay consistent on ghost rows

@@ -308,6 +308,10 @@ struct cwf_hip_system
     // Ap is scratch (apply_keff staging, PARITY's K p, the prologues' K x); FAST PCG never reads it
     float *x = nullptr, *r = nullptr, *p = nullptr, *z = nullptr, *Ap = nullptr, *rhs = nullptr, *tmp = nullptr;
     float *p2 = nullptr, *p3 = nullptr, *p4 = nullptr;  // FAST: p_j lives in {p, p2, p3, p4}[(j + 1) % 4]
+    // the fused lattice iteration (lattice_fused.inc): r and Ap by launch parity (r_j in {r2, r}[j & 1], Ap_j in
+    // {Ap, ap2}[j & 1]) and the launches' five shares per workgroup, [2][5][lnwork]
+    float *r2 = nullptr, *ap2 = nullptr;
+    double *fsh = nullptr;
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's
@@ -435,6 +439,13 @@ void fast_update_pcg(cwf_hip_system *h, const float *rhs, unsigned it, hipStream
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st);
 void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st);  // the lazy x terms still pending
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
+// the fused lattice iteration (lattice_fused.inc): one launch per PCG iteration on an unsharded structured block
+bool fast_fused(const cwf_hip_system *h);
+void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
+void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr,
+                          hipEvent_t e1 = nullptr);
+void fast_fused_check(cwf_hip_system *h, unsigned it, hipStream_t st);
+void fast_fused_finish(cwf_hip_system *h, hipStream_t st);
 
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);

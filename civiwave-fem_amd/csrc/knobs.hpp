@@ -39,6 +39,9 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_PARITY_TILES", "strip: PARITY node tiles of 256 consecutive nodes also on a single handle (default there: "
                          "compact breadth-first tiles and a separate p.Ap partials pass; shards always use strips)"},
     // PCG schedule (spmv_tiles.hip)
+    {"CWF_FUSED", "0: structured blocks run the two-kernel iteration (k_keff_lattice + k_pcg_update_tiles) instead of "
+                  "the fused one-launch iteration (lattice_fused.inc)"},
+    {"CWF_FUSED_MAXWG", "n: the largest lattice grid that runs the fused iteration (default 1024 workgroups)"},
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
     // multi-GPU (comm.cpp)

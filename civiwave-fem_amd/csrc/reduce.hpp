@@ -171,4 +171,76 @@ __device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const d
     tb = b;
 }
 
+// K folds of fold_all's order in one pass: array q is p[q stride .. q stride + count), thread t sums its entries
+// t, t + NT, ... in that order, 2K loads in flight per trip (two rows per array), then each array's wave and block
+// sums as block_sum. red: K NT / 64 doubles. The fused PCG iteration's five scalars (lattice_fused.inc).
+template <int NT, int K>
+__device__ __forceinline__ void fold_k(const double *__restrict__ p, unsigned count, unsigned stride, double *red,
+                                       double out[K])
+{
+    double v[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+        v[q] = 0.0;
+    for (unsigned i = threadIdx.x; i < count; i += 2u * NT)
+    {
+        const bool two = i + NT < count;
+        const unsigned i2 = two ? i + NT : i;
+        double a[K], b[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+        {
+            a[q] = p[(size_t)q * stride + i];
+            b[q] = p[(size_t)q * stride + i2];
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+        {
+            v[q] += a[q];
+            v[q] += two ? b[q] : 0.0;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+    {
+        v[q] = wave_sum(v[q]);
+        if ((threadIdx.x & 63) == 0)
+            red[K * (threadIdx.x >> 6) + q] = v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+    {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w)
+            t += red[K * w + q];
+        out[q] = t;
+    }
+    __syncthreads();
+}
+
+// K block sums in one LDS round (the order of block_sum per value); red: K NT / 64 doubles
+template <int NT, int K> __device__ __forceinline__ void block_sum_k(double v[K], double *red)
+{
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+    {
+        v[q] = wave_sum(v[q]);
+        if ((threadIdx.x & 63) == 0)
+            red[K * (threadIdx.x >> 6) + q] = v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+    {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w)
+            t += red[K * w + q];
+        v[q] = t;
+    }
+    __syncthreads();
+}
+
 }  // namespace cwf

@@ -1726,6 +1726,7 @@ void launch_tiles_g(const DevSys &s, const float *x, const PcgArgs &pa, int nt, 
 
 #include "hex8_tiles.inc"
 #include "lattice.inc"
+#include "lattice_fused.inc"
 
 // pipelined kernel: element forces + local CSR + per tile node {x y z v_x}{v_y v_z}
 inline size_t pipe_lds(const DevSys &s)
@@ -2035,6 +2036,85 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
                h->hist, abl | 32u};
     for (int i = 0; i < reps; ++i)
         launch_tiles<true, false, 1>(s, h->p, pa, tile_threads(), st);
+}
+
+// ---- the fused lattice iteration (lattice_fused.inc) --------------------------------------------------------
+// CWF_FUSED=0: the two-kernel iteration on a structured block; CWF_FUSED_MAXWG: the largest grid that fuses (every
+// workgroup folds five shares of each of the previous launch's workgroups)
+bool fast_fused(const cwf_hip_system *h)
+{
+    static const int on = [] {
+        const char *e = knob("CWF_FUSED");
+        return e ? atoi(e) : 1;
+    }();
+    static const unsigned maxwg = [] {
+        const char *e = knob("CWF_FUSED_MAXWG");
+        return e && atoi(e) > 0 ? (unsigned)atoi(e) : 1024u;
+    }();
+    const DevTiles &t = h->ds.t;
+    return on && h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && !h->sharded() &&
+           t.lnwork <= maxwg && t.ntiles;
+}
+
+namespace
+{
+// launch j of the fused iteration: r_j -> {r2, r}[j & 1], Ap_j -> {Ap, ap2}[j & 1], p_j -> p[(j + 1) % 4], shares
+// -> fsh[j & 1]; launch j reads launch j - 1's (launch 0 reads r from r and Ap from ap2, zeroed at init)
+FusedArgs fused_args(cwf_hip_system *h, unsigned j)
+{
+    const unsigned W = h->ds.t.lnwork;
+    float *const R[2] = {h->r2, h->r}, *const A[2] = {h->Ap, h->ap2};
+    FusedArgs fa{};
+    fa.ctl = h->ctl;
+    fa.sstride = W;
+    fa.sin = h->fsh + (size_t)((j + 1u) & 1u) * 5 * W;
+    fa.nin = W;
+    fa.sout = h->fsh + (size_t)(j & 1u) * 5 * W;
+    fa.j = j;
+    fa.hist = h->hist;
+    fa.rin = R[(j + 1u) & 1u];
+    fa.rout = R[j & 1u];
+    fa.ain = A[(j + 1u) & 1u];
+    fa.aout = A[j & 1u];
+    fa.pin = fast_p_buf(h, j);
+    fa.pout = fast_p_buf(h, j + 1u);
+    fa.x = h->x;
+    return fa;
+}
+}  // namespace
+
+void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st)
+{
+    const DevSys &s = h->ds;
+    const uint32_t nbD = fast_dot_blocks(s.D);
+    fast_block_inverse(h, st);
+    fast_keff(h, h->x, h->Ap, true, nullptr, nullptr, st);
+    launch_init_residual(h, rhs, st);  // r_0 = rhs - A x (Dirichlet: x = rhs, r = 0) into h->r
+    fast_dot(rhs, rhs, nullptr, s.D, h->part0, nullptr, st);
+    fast_dot(h->r, h->r, nullptr, s.D, h->part1, nullptr, st);
+    fast_init_scalars_strided(h, h->part0, h->part1, nbD, 1u, rel_tol, st);
+    // launch 0 reads p_(-1) and Ap_(-1) (times beta = alpha = 0): zero, so no stale non-finite value enters
+    (void)hipMemsetAsync(h->p, 0, sizeof(float) * s.D, st);
+    (void)hipMemsetAsync(h->ap2, 0, sizeof(float) * s.D, st);
+    launch_pcg_lattice(s, fused_args(h, 0), st, nullptr, nullptr);
+}
+
+void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
+{
+    launch_pcg_lattice(h->ds, fused_args(h, it + 1u), st, e0, e1);
+}
+
+// the convergence of the batch's last launch (it iterations enqueued: launch it's r)
+void fast_fused_check(cwf_hip_system *h, unsigned it, hipStream_t st)
+{
+    k_fused_check<<<1, 256, 0, st>>>(fused_args(h, it + 1u));
+}
+
+void fast_fused_finish(cwf_hip_system *h, hipStream_t st)
+{
+    const uint32_t D = h->ds.D;
+    if (D)
+        k_fused_finish<<<std::min<unsigned>(grid_for(D, 256), 1024u), 256, 0, st>>>(h->ctl, h->r2, h->r, D);
 }
 
 void fast_check_pcg(cwf_hip_system *h, unsigned it, hipStream_t st)

@@ -1,4 +1,5 @@
-"""The structured-block FAST operator (lattice.cpp / lattice.inc, k_keff_lattice) against the pinned oracle.
+"""The structured-block FAST operator (lattice.cpp / lattice.inc, k_keff_lattice; lattice_fused.inc, k_pcg_lattice)
+against the pinned oracle.
 
 A FAST handle whose mesh is a Kuhn-split box lattice (one gradient / volume set per Kuhn type) applies K_eff as
 the node-pair stencil of the shared cell stiffness. Its arithmetic is the element loop's regrouped in fp32, so it
@@ -42,6 +43,11 @@ def _kernel(s):
     return (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
 
 
+# the structured-block stencil: the fused one-launch iteration (lattice_fused.inc, the default where its grid is
+# at most CWF_FUSED_MAXWG workgroups) or the two-kernel one (k_keff_lattice + the update pass)
+LATTICE = ("k_pcg_lattice", "k_keff_lattice")
+
+
 def _apply_err(case, s, seed=3):
     o = oracle_system(case.packing, case.materials, *case.scalars())
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -61,7 +67,7 @@ def permuted_block(nx, ny, nz, h=0.1, **kw):
 
 
 def test_lattice_detected(case):
-    assert _kernel(_system(case)).startswith("k_keff_lattice")
+    assert _kernel(_system(case)).startswith(LATTICE)
 
 
 def test_jittered_mesh_is_not_a_lattice():
@@ -94,7 +100,7 @@ def test_lattice_work_item_lengths(L, shell, monkeypatch):
 def test_lattice_permuted_node_order():
     case = permuted_block(9, 7, 6, tol=1e-6, max_iterations=800)
     s = _system(case)
-    assert _kernel(s).startswith("k_keff_lattice")
+    assert _kernel(s).startswith(LATTICE)
     assert _apply_err(case, s) <= 2e-5
     o = oracle_system(case.packing, case.materials, *case.scalars())
     rhs = case.static_rhs()
@@ -125,6 +131,7 @@ def test_lattice_pcg_variants_solve(variant, monkeypatch):
     class in the K_eff pass and no z stored by the update pass (CWF_LAT_ZR=1, the default from 2M nodes), or with z
     stored by the update pass (CWF_LAT_ZR=0, the default below), and the per-node mass through LDS
     (CWF_LAT_MASS=0, which also stores z)."""
+    monkeypatch.setenv("CWF_FUSED", "0")  # the two-kernel iteration's brick variants
     monkeypatch.setenv("CWF_LAT_ZR", "1" if variant == "z-from-r" else "0")
     if variant == "per-node-mass":
         monkeypatch.setenv("CWF_LAT_MASS", "0")
@@ -172,7 +179,7 @@ def test_lattice_slab_shards(nranks):
     P = glob.packing
     sK, sM = glob.scalars()
     single = _system(glob)
-    assert _kernel(single).startswith("k_keff_lattice")
+    assert _kernel(single).startswith(LATTICE)
     rng = np.random.Generator(np.random.PCG64(7))
     x = rng.uniform(-1, 1, P.dof_count).astype(np.float32)
     y1 = np.zeros_like(x)
@@ -185,7 +192,7 @@ def test_lattice_slab_shards(nranks):
         src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
         sh = shard.build_shard(src, begin, r, node_global)
         s = sh.system(glob.materials, sK, sM)
-        assert _kernel(s).startswith("k_keff_lattice")
+        assert _kernel(s).startswith(LATTICE)
         gid = sh.node_global.astype(np.int64)
         own = sh.owned_nodes
         yl = np.zeros(3 * sh.local_nodes, np.float32)
@@ -230,3 +237,31 @@ def test_fast_solve_run_to_run_deterministic(mesh, monkeypatch):
         assert t.iterations == runs[0][0].iterations and t.residual_norm == runs[0][0].residual_norm
         assert np.array_equal(x.view(np.uint32), runs[0][1].view(np.uint32))
         assert np.array_equal(r.view(np.uint32), runs[0][2].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["33x9x5", "rollers", "c1", "rayleigh"])
+def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
+    """The fused one-launch iteration (lattice_fused.inc: r, z, p, x formed in the launch that applies K_eff; beta's
+    numerator r_(j+1).z_(j+1) expanded through r_(j+1) = r_j - alpha Ap_j from the launch's own dots) against the
+    reference loop's two kernels on the same handle geometry: the same solution to 1e-4 of the oracle's and an
+    iteration count within 5% (tools/cg_variants.py emulates both in FAST arithmetic on the CPU)."""
+    case = CASES[name]()
+    rhs = case.static_rhs()
+    mi = case.cfg.solver.max_iterations
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CWF_FUSED", fused)
+        s = _system(case)
+        assert _kernel(s).startswith("k_pcg_lattice" if fused == "1" else "k_keff_lattice"), _kernel(s)
+        x = np.zeros_like(rhs)
+        r = np.zeros_like(rhs)
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(mi, 1e-6), pcg.PcgVectors(x, r)).value()
+        assert t.converged
+        # the r output is the residual of x (rhs - K x, Dirichlet rows 0) to fp32 accuracy
+        out[fused] = (t, x, r)
+    (tf, xf, rf), (tk, xk, _) = out["1"], out["0"]
+    ref = oracle_system(case.packing, case.materials, *case.scalars()).solve_pcg(rhs, mi, 1e-6)
+    assert np.linalg.norm(xf - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    assert abs(tf.iterations - tk.iterations) <= max(3, tk.iterations // 20), (tf.iterations, tk.iterations)
+    assert tf.residual_norm <= 1e-6 * np.linalg.norm(rhs.astype(np.float64)) * 1.0001
+    assert abs(np.linalg.norm(rf.astype(np.float64)) - tf.residual_norm) <= 1e-3 * tf.residual_norm

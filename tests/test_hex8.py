@@ -182,7 +182,8 @@ def test_gpu_hex8_structured_blocks_run_the_lattice_stencil(hcase):
     trilinear cell stiffness (lattice.cpp); a jittered one the hex tiles. Either way the apply test above holds."""
     kern = _keff_kernel(gpu_hex_system(hcase))
     # an isotropic block's stencil is point-symmetric (S_-d = S_d): the paired-direction instantiation
-    want = "k_keff_hex_tiles" if hcase.name.endswith("-jitter") else "k_keff_lattice<1, false, true, LatHex,"
+    want = (("k_keff_hex_tiles",) if hcase.name.endswith("-jitter") else
+            ("k_keff_lattice<1, false, true, LatHex,", "k_pcg_lattice<true, LatHex,"))
     assert kern.startswith(want), kern
 
 
@@ -193,6 +194,7 @@ def test_gpu_hex8_lattice_z_from_r_solve(monkeypatch):
     case = GPU_CASES["tiles"]()
     rhs = case.static_rhs()
     xs = {}
+    monkeypatch.setenv("CWF_FUSED", "0")  # the two-kernel iteration's z source (the fused one always forms z from r)
     for zr in ("0", "1"):
         monkeypatch.setenv("CWF_LAT_ZR", zr)
         s = gpu_hex_system(case)
