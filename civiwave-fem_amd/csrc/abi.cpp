@@ -1168,6 +1168,8 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             return bail(st);
         if (int st = dalloc(h, &h->fsh, 2ull * 5 * std::max<uint32_t>(s.t.lnwork, 1u)))
             return bail(st);
+        if (int st = dalloc(h, &h->g_fsh, 8))  // one rank until attach (comm.cpp grows it to [nranks][8])
+            return bail(st);
     }
     if (int st = dalloc(h, &h->inv, 9 * N))
         return bail(st);
@@ -1361,7 +1363,7 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
-        if (s.t.lat && fast_fused(h))  // the fused iteration (lattice_fused.inc): per owned node r_(j-1), Ap_(j-1),
+        if (s.t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration (lattice_fused.inc): per owned node r_(j-1), Ap_(j-1),
         {                              // p_(j-1), the class byte and x read, r_j, p_j, Ap_j and x written; the mass
                                        // of the shell's nodes (the strict interior's is one value when lmu)
             *layout_bytes = (uint64_t)s.Nown * (4 * 12 + 1 + 4 * 12) + 4ull * (s.t.lmu ? s.t.lnshell : s.Nown);
@@ -1416,11 +1418,12 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
             return h->ds.iso ? "k_keff_parity_tile<true, false, false, true>" : "k_keff_parity_tile<false, false, false, true>";
         return h->ds.iso ? "k_keff_parity_tile<true, false, true, false>" : "k_keff_parity_tile<false, false, true, false>";
     }
-    if (t.lat && fast_fused(h))  // the fused iteration's one launch (lattice_fused.inc)
+    if (t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration's one launch (lattice_fused.inc)
     {
-        static thread_local char name[96];
-        snprintf(name, sizeof name, "k_pcg_lattice<%s, %s, %s, %s>", t.lsym ? "true" : "false",
-                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lpstride ? "true" : "false");
+        static thread_local char name[112];
+        snprintf(name, sizeof name, "k_pcg_lattice<%s, %s, %s, %s, %s>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lpstride ? "true" : "false",
+                 !t.lpstride && h->ds.Nown < h->ds.N ? "true" : "false");
         return name;
     }
     if (t.lat)  // as rocprofv3 names it, less the namespaces

@@ -64,8 +64,14 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (cwf_hip_system *m : g)
             HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
-    const bool fused = fast && fast_fused(h);  // one launch per iteration (lattice_fused.inc)
-    if (fused)
+    // one launch per iteration (lattice_fused.inc); shards: one exchange per iteration, agreed by every rank
+    const bool fused = fast && (sharded ? group_fused(g) : fast_fused(h));
+    if (fused && sharded)
+    {
+        if (int e = sharded_fused_init(g, rhs, set.relative_tolerance))
+            return e;
+    }
+    else if (fused)
         fast_fused_init(h, rhs[0], set.relative_tolerance, st);
     else if (sharded)
     {
@@ -134,7 +140,12 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         {
             const bool timed = h->timing && (enq + i) % (uint64_t)h->timing == 0;
             hipEvent_t e0 = timed ? h->ev[2 * i] : nullptr, e1 = timed ? h->ev[2 * i + 1] : nullptr;
-            if (fused)
+            if (fused && sharded)
+            {
+                if (int e = sharded_fused_iteration(g, (unsigned)(enq + i), e0, e1))
+                    return e;
+            }
+            else if (fused)
                 fast_fused_iteration(h, (unsigned)(enq + i), st, e0, e1);
             else if (fast)
             {
@@ -150,7 +161,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
                 parity_pcg_iteration(h, rhs[0], st, e0, e1);
         }
         if (fused)  // convergence of the batch's last launch (repeated idempotently by the next launch's start)
-            fast_fused_check(h, (unsigned)(enq + nb), st);
+            for (cwf_hip_system *m : g)
+                fast_fused_check(m, (unsigned)(enq + nb), m->stream);
         else if (fast)  // convergence of the batch's last update (repeated idempotently by the next tiles kernel)
             for (cwf_hip_system *m : g)
                 fast_check_pcg(m, (unsigned)(enq + nb), m->stream);
@@ -162,7 +174,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             batch = std::min<uint64_t>(batch * 2, kMaxBatch);
     }
     if (fused)  // x is updated in every launch; the solve's r output is the last launch's
-        fast_fused_finish(h, st);
+        for (cwf_hip_system *m : g)
+            fast_fused_finish(m, m->stream);
     else if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
         for (size_t i = 0; i < g.size(); ++i)
             fast_flush_x(g[i], rhs[i], g[i]->stream);

@@ -292,6 +292,117 @@ int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::
     return comm_exchange(g, {Gather{&cwf_hip_system::g_rrz, 2}}, g[0]->sharded() ? &cwf_hip_system::z : nullptr);
 }
 
+// ---- the sharded fused iteration (lattice_fused.inc on slab shards) ---------------------------------------------
+// One launch and one exchange step per PCG iteration: launch j forms r_j, z_j, p_j, x_j for its owned rows and (from
+// the received Ap_(j-1) rows and its own stored r_(j-1), p_(j-1)) the same r_j, p_j its neighbours form for its ghost
+// rows, so only Ap_j's ghost rows and the five rank totals cross ranks: {rank totals} all-gather + Ap halo, ONE RCCL
+// group or PEER step (against two per iteration in the two-kernel schedule above). Every rank folds the gathered
+// totals in rank order, so every rank takes the same decisions.
+
+// every member (and, through one all-gather, every rank) can run it: the decision is collective, taken at a handle's
+// first sharded solve and kept (the shards' lattice plans do not change)
+bool group_fused(const std::vector<cwf_hip_system *> &g)
+{
+    cwf_hip_system *h0 = g[0];
+    if (h0->fused_agreed >= 0)
+        return h0->fused_agreed == 1;
+    bool mine = true;
+    for (cwf_hip_system *h : g)
+        mine = mine && fast_fused(h) && h->ds.t.lat;
+    for (cwf_hip_system *h : g)
+    {
+        const double v[2] = {mine ? 1.0 : 0.0, 0.0};
+        if (hipMemcpyAsync(h->g_init + 2 * h->rank, v, sizeof v, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            mine = false;
+    }
+    bool all = mine;
+    if (comm_allgather(g, &cwf_hip_system::g_init, 2) == 0)
+    {
+        std::vector<double> f(2 * (size_t)h0->nranks, 0.0);
+        if (hipStreamSynchronize(h0->stream) == hipSuccess &&
+            hipMemcpy(f.data(), h0->g_init, f.size() * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess)
+            for (int r = 0; r < h0->nranks; ++r)
+                all = all && f[2 * (size_t)r] == 1.0;
+        else
+            all = false;
+    }
+    else
+        all = false;
+    for (cwf_hip_system *h : g)
+        h->fused_agreed = all ? 1 : 0;
+    return all;
+}
+
+namespace
+{
+// after launch j: the rank totals of its shares all-gathered into g_fsh, and Ap_j's ghost rows
+int fused_exchange(const std::vector<cwf_hip_system *> &g, unsigned j)
+{
+    cwf_hip_system *h0 = g[0];
+    if (h0->comm && h0->comm->kind == 2 && h0->nranks > 1)
+    {
+        unsigned stride = 0;
+        const double *sh = fast_fused_shares(h0, j, &stride);
+        PeerFold f{sh, nullptr, stride, stride};
+        return peer_exchange(h0, {Gather{&cwf_hip_system::g_fsh, kFusedSlotHost}}, {fast_fused_ap(h0, j)}, &f);
+    }
+    std::vector<std::vector<float *>> vecs;
+    for (cwf_hip_system *h : g)
+    {
+        fast_fused_rank_totals(h, j, h->stream);
+        vecs.push_back({fast_fused_ap(h, j)});
+    }
+    return comm_exchange_vecs(g, {Gather{&cwf_hip_system::g_fsh, kFusedSlotHost}}, vecs);
+}
+}  // namespace
+
+int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+{
+    for (cwf_hip_system *h : g)
+        fast_block_inverse(h, h->stream);
+    if (!g[0]->cls_global)  // the ghosts' classes from their owners, once per handle
+    {
+        for (cwf_hip_system *h : g)
+            fast_fused_cls_out(h, h->stream);
+        if (int st = comm_halo(g, &cwf_hip_system::tmp))
+            return st;
+        for (cwf_hip_system *h : g)
+        {
+            fast_fused_cls_in(h, h->stream);
+            h->cls_global = true;
+        }
+    }
+    if (int st = comm_halo(g, &cwf_hip_system::x))  // warm start: ghost x from the owners
+        return st;
+    for (size_t i = 0; i < g.size(); ++i)
+    {
+        cwf_hip_system *h = g[i];
+        const uint32_t Down = 3u * h->ds.Nown;
+        fast_keff(h, h->x, h->Ap, true, nullptr, nullptr, h->stream);
+        launch_init_residual(h, rhs[i], h->stream);
+        fast_dot(rhs[i], rhs[i], nullptr, Down, h->part0, nullptr, h->stream);
+        fast_dot(h->r, h->r, nullptr, Down, h->part1, nullptr, h->stream);
+        fold_pair(h->part0, h->part1, fast_dot_blocks(Down), h->g_init + 2 * h->rank, h->stream);
+    }
+    if (int st = comm_allgather(g, &cwf_hip_system::g_init, 2))
+        return st;
+    for (cwf_hip_system *h : g)
+        fast_init_scalars_strided(h, h->g_init, h->g_init + 1, (uint32_t)h->nranks, 2u, rel_tol, h->stream);
+    if (int st = comm_halo(g, &cwf_hip_system::r))  // r_0's ghost rows (launch 0 forms ghost p_0 from them)
+        return st;
+    for (cwf_hip_system *h : g)
+        fast_fused_launch0(h, h->stream);
+    return fused_exchange(g, 0);
+}
+
+int sharded_fused_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1)
+{
+    for (size_t i = 0; i < g.size(); ++i)
+        fast_fused_iteration(g[i], it, g[i]->stream, i ? nullptr : e0, i ? nullptr : e1);
+    return fused_exchange(g, it + 1u);
+}
+
 // ---- sharded PARITY (SURVEY.md 8e parity gate): the reference's fold orders across ranks --------------------
 // Each rank's owned nodes are one contiguous range of global node ids, ascending by rank from node 0, and every
 // rank but the last owns a whole number of reduction chunks (3 * owned % reduction_block == 0). Then a rank's
@@ -647,6 +758,17 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         t.lk1 = k0 < k1 ? k1 : 1;
         t.lzr = 0;  // the update pass stores z: the halo exchange carries z, and a ghost's class is a local one
         lattice_plan(t);
+        if (h->fsh)  // the fused iteration's shares for the shard's work items, its gathered rank totals
+        {
+            void *p = nullptr;
+            if (int st = alloc(&p, 2ull * 5 * std::max<uint32_t>(t.lnwork, 1u) * sizeof(double)))
+                return st;
+            h->fsh = static_cast<double *>(p);
+            if (int st = alloc(&p, (size_t)kFusedSlotHost * n * sizeof(double)))
+                return st;
+            h->g_fsh = static_cast<double *>(p);
+            HIPTRY(h, hipMemset(h->g_fsh, 0, (size_t)kFusedSlotHost * n * sizeof(double)));
+        }
     }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
     if (plan->node_global)

@@ -312,6 +312,9 @@ struct cwf_hip_system
     // {Ap, ap2}[j & 1]) and the launches' five shares per workgroup, [2][5][lnwork]
     float *r2 = nullptr, *ap2 = nullptr;
     double *fsh = nullptr;
+    double *g_fsh = nullptr;  // a shard's all-gathered rank totals of the fused shares, [nranks][8] (one rank: [8])
+    bool cls_global = false;  // a shard's ghost class bytes hold their owners' (global) classes
+    int fused_agreed = -1;    // a shard: every rank runs the fused iteration (1) or none (0); -1: not asked yet
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's
@@ -446,6 +449,17 @@ void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEve
                           hipEvent_t e1 = nullptr);
 void fast_fused_check(cwf_hip_system *h, unsigned it, hipStream_t st);
 void fast_fused_finish(cwf_hip_system *h, hipStream_t st);
+void fast_fused_launch0(cwf_hip_system *h, hipStream_t st);
+float *fast_fused_ap(cwf_hip_system *h, unsigned j);
+void fast_fused_rank_totals(cwf_hip_system *h, unsigned j, hipStream_t st);
+const double *fast_fused_shares(const cwf_hip_system *h, unsigned j, unsigned *stride);
+void fast_fused_cls_out(cwf_hip_system *h, hipStream_t st);  // owned class bytes -> tmp (x components)
+void fast_fused_cls_in(cwf_hip_system *h, hipStream_t st);   // ghost class bytes <- tmp
+constexpr size_t kFusedSlotHost = 8;  // doubles per rank of the gathered fused totals (lattice_fused.inc kFusedSlot)
+// comm.cpp: the sharded fused iteration (one launch + one exchange: the rank totals and the Ap halo)
+int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
+int sharded_fused_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1);
+bool group_fused(const std::vector<cwf_hip_system *> &g);
 
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
@@ -481,6 +495,8 @@ struct PeerFold
 {
     const double *a, *b;  // shares of slot 0 and (b) slot 1
     uint32_t n;
+    uint32_t k5_stride = 0;  // > 0: the fused iteration's five share arrays a[q k5_stride + i] into slots 0..4, in
+                             // k_fused_rank_totals' order (fold_k, 256 threads)
 };
 int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs,
                   const PeerFold *fold = nullptr);

@@ -33,7 +33,7 @@
 // (where each neighbour's ghosts go, read once by the peers at connect), one 64-B flag line per peer, and two
 // copies (by epoch parity) of the scalar-slot area and of the ghost receive area. Two copies suffice: a rank can
 // only push step e + 2 after waiting on step e + 1 of the receiver, which the receiver pushes after unpacking step
-// e. Only the FAST schedule goes through it (slots of <= 4 doubles); PARITY's chunk-partial all-gathers stay on
+// e. Only the FAST schedules go through it (slots of <= 8 doubles); PARITY's chunk-partial all-gathers stay on
 // RCCL / LOCAL.
 #include <hip/hip_runtime.h>
 
@@ -58,7 +58,7 @@ namespace cwf
 namespace
 {
 constexpr uint64_t kPeerMagic = 0x43574650454552ull;  // "CWFPEER"
-constexpr size_t kHdrBytes = 4096, kFlagLine = 64, kSlot = 4;  // kSlot doubles per rank and gather
+constexpr size_t kHdrBytes = 4096, kFlagLine = 64, kSlot = 8;  // kSlot doubles per rank and gather
 constexpr int kMaxPeerGathers = 2;
 constexpr int kPeerThreads = 1024;
 constexpr uint64_t kPeerTimeoutTicks = 10ull * 100000000ull;  // a wait gives a peer 10 s (s_memrealtime: 100 MHz)  // the fold of a rank's shares is k_fold_pair's 1024-thread fold_all
@@ -104,7 +104,7 @@ struct PeerStep
     double *gbuf[kMaxPeerGathers];
     // fold (fn > 0): gather 0's own slot(s) from the rank's shares fa / fb, folded by workgroup 0
     const double *fa, *fb;
-    uint32_t fn;
+    uint32_t fn, fk5;  // fk5 > 0: five arrays fa[q fk5 + i] (the fused iteration's shares)
 };
 
 __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
@@ -122,8 +122,23 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
         return;
     }
     // (0) workgroup 0: this rank's scalars, folded as k_fold_pair folds them, kept for the push and stored locally
-    __shared__ double red[NT / 64], gv[kSlot];
-    if (blockIdx.x == 0 && a.fn)
+    __shared__ double red[5 * (NT / 64)], gv[kSlot];
+    if (blockIdx.x == 0 && a.fn && a.fk5)
+    {
+        double v[5];
+        fold_k<NT, 5, 256>(a.fa, a.fn, a.fk5, red, v);  // k_fused_rank_totals' order, bit for bit
+        if (threadIdx.x == 0)
+        {
+            double *own = const_cast<double *>(a.gsrc[0]);
+            for (int q = 0; q < (int)kSlot; ++q)
+            {
+                gv[q] = q < 5 ? v[q] : 0.0;
+                own[q] = gv[q];
+            }
+        }
+        __syncthreads();
+    }
+    else if (blockIdx.x == 0 && a.fn)
     {
         const double ta = fold_all<NT>(a.fa, a.fn, red);
         const double tb = a.fb ? fold_all<NT>(a.fb, a.fn, red) : 0.0;
@@ -384,6 +399,7 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
         a.fa = fold->a;
         a.fb = fold->b;
         a.fn = fold->n;
+        a.fk5 = fold->k5_stride;
     }
     // one workgroup per 1024 pushed nodes or 4096 unpacked floats, <= 64 (all resident: every one reaches its
     // ticket)
@@ -496,7 +512,7 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
     std::vector<cwf_hip_system *> g{h};
     std::vector<std::vector<float *>> vecs{{h->z}};
     // as the iteration runs it: with the fold of the update pass's shares (PEER folds them in the step itself)
-    const PeerFold fold{h->part1, h->part2, fast_rrz_shares(h->ds, 0)};
+    const PeerFold fold{h->part1, h->part2, fast_rrz_shares(h->ds, 0), 0};
     const auto step = [&]() {
         if (h->comm->kind == 2)
             return peer_exchange(h, {Gather{&cwf_hip_system::g_rrz, 2}}, {h->z}, &fold);

@@ -171,27 +171,30 @@ __device__ __forceinline__ void fold_all2(const double *__restrict__ pa, const d
     tb = b;
 }
 
-// K folds of fold_all's order in one pass: array q is p[q stride .. q stride + count), thread t sums its entries
-// t, t + NT, ... in that order, 2K loads in flight per trip (two rows per array), then each array's wave and block
-// sums as block_sum. red: K NT / 64 doubles. The fused PCG iteration's five scalars (lattice_fused.inc).
-template <int NT, int K>
+// K folds of fold_all's order in one pass: element i of array q is p[q stride + i istride] (i < count), thread t
+// sums its elements t, t + NT, ... in that order, 2K loads in flight per trip (two rows per array), then each
+// array's wave and block sums as block_sum. red: K NT / 64 doubles. The fused PCG iteration's five scalars
+// (lattice_fused.inc): a workgroup's shares (istride 1) or the all-gathered per-rank totals (stride 1, istride K).
+// NTV < NT: the fold of an NTV-thread block, bitwise (threads >= NTV hold +0.0, and adding +0.0 to a sum from +0.0
+// changes nothing): the PEER step's 1024-thread workgroup folds a rank's shares as a 256-thread one does.
+template <int NT, int K, int NTV = NT>
 __device__ __forceinline__ void fold_k(const double *__restrict__ p, unsigned count, unsigned stride, double *red,
-                                       double out[K])
+                                       double out[K], unsigned istride = 1)
 {
     double v[K];
 #pragma unroll
     for (int q = 0; q < K; ++q)
         v[q] = 0.0;
-    for (unsigned i = threadIdx.x; i < count; i += 2u * NT)
+    for (unsigned i = threadIdx.x; threadIdx.x < (unsigned)NTV && i < count; i += 2u * NTV)
     {
-        const bool two = i + NT < count;
-        const unsigned i2 = two ? i + NT : i;
+        const bool two = i + NTV < count;
+        const unsigned i2 = two ? i + NTV : i;
         double a[K], b[K];
 #pragma unroll
         for (int q = 0; q < K; ++q)
         {
-            a[q] = p[(size_t)q * stride + i];
-            b[q] = p[(size_t)q * stride + i2];
+            a[q] = p[(size_t)q * stride + (size_t)i * istride];
+            b[q] = p[(size_t)q * stride + (size_t)i2 * istride];
         }
 #pragma unroll
         for (int q = 0; q < K; ++q)

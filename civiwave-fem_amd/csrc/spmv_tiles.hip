@@ -2052,7 +2052,7 @@ bool fast_fused(const cwf_hip_system *h)
         return e && atoi(e) > 0 ? (unsigned)atoi(e) : 1024u;
     }();
     const DevTiles &t = h->ds.t;
-    return on && h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && !h->sharded() &&
+    return on && h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && h->g_fsh &&
            t.lnwork <= maxwg && t.ntiles;
 }
 
@@ -2067,8 +2067,20 @@ FusedArgs fused_args(cwf_hip_system *h, unsigned j)
     FusedArgs fa{};
     fa.ctl = h->ctl;
     fa.sstride = W;
-    fa.sin = h->fsh + (size_t)((j + 1u) & 1u) * 5 * W;
-    fa.nin = W;
+    if (h->sharded())  // every rank folds the all-gathered rank totals, in rank order
+    {
+        fa.sin = h->g_fsh;
+        fa.nin = (unsigned)h->nranks;
+        fa.sin_stride = 1;
+        fa.sis = kFusedSlot;
+    }
+    else
+    {
+        fa.sin = h->fsh + (size_t)((j + 1u) & 1u) * 5 * W;
+        fa.nin = W;
+        fa.sin_stride = W;
+        fa.sis = 1;
+    }
     fa.sout = h->fsh + (size_t)(j & 1u) * 5 * W;
     fa.j = j;
     fa.hist = h->hist;
@@ -2094,14 +2106,59 @@ void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
     fast_dot(h->r, h->r, nullptr, s.D, h->part1, nullptr, st);
     fast_init_scalars_strided(h, h->part0, h->part1, nbD, 1u, rel_tol, st);
     // launch 0 reads p_(-1) and Ap_(-1) (times beta = alpha = 0): zero, so no stale non-finite value enters
-    (void)hipMemsetAsync(h->p, 0, sizeof(float) * s.D, st);
-    (void)hipMemsetAsync(h->ap2, 0, sizeof(float) * s.D, st);
-    launch_pcg_lattice(s, fused_args(h, 0), st, nullptr, nullptr);
+    fast_fused_launch0(h, st);
 }
 
 void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
     launch_pcg_lattice(h->ds, fused_args(h, it + 1u), st, e0, e1);
+}
+
+void fast_fused_launch0(cwf_hip_system *h, hipStream_t st)
+{
+    (void)hipMemsetAsync(h->p, 0, sizeof(float) * h->ds.D, st);
+    (void)hipMemsetAsync(h->ap2, 0, sizeof(float) * h->ds.D, st);
+    launch_pcg_lattice(h->ds, fused_args(h, 0), st, nullptr, nullptr);
+}
+
+// a shard's ghost class bytes from their owners (once per handle, before its first fused solve): the owned classes
+// as floats in tmp's x components, a halo, and the ghosts' back into lcls (a ghost's local class is a boundary type
+// of the shard's sub-lattice; its owner's is the node's class in the whole block, the one its z_j is formed with)
+__global__ __launch_bounds__(256) void k_cls_out(const uint8_t *__restrict__ cls, uint32_t n, float *__restrict__ t)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+        t[3u * i] = (float)cls[i];
+}
+__global__ __launch_bounds__(256) void k_cls_in(const float *__restrict__ t, uint32_t n0, uint32_t n1,
+                                                uint8_t *__restrict__ cls)
+{
+    for (uint32_t i = n0 + blockIdx.x * 256u + threadIdx.x; i < n1; i += gridDim.x * 256u)
+        cls[i] = (uint8_t)t[3u * i];
+}
+void fast_fused_cls_out(cwf_hip_system *h, hipStream_t st)
+{
+    if (h->ds.Nown)
+        k_cls_out<<<std::min<unsigned>(grid_for(h->ds.Nown, 256), 1024u), 256, 0, st>>>(h->ds.t.lcls, h->ds.Nown, h->tmp);
+}
+void fast_fused_cls_in(cwf_hip_system *h, hipStream_t st)
+{
+    if (h->ds.N > h->ds.Nown)
+        k_cls_in<<<std::min<unsigned>(grid_for(h->ds.N - h->ds.Nown, 256), 1024u), 256, 0, st>>>(
+            h->tmp, h->ds.Nown, h->ds.N, const_cast<uint8_t *>(h->ds.t.lcls));
+}
+
+// a shard's launch j: its Ap_j (the vector the exchange after it carries) and its rank totals into g_fsh[rank]
+float *fast_fused_ap(cwf_hip_system *h, unsigned j) { return (j & 1u) ? h->ap2 : h->Ap; }
+void fast_fused_rank_totals(cwf_hip_system *h, unsigned j, hipStream_t st)
+{
+    const unsigned W = h->ds.t.lnwork;
+    k_fused_rank_totals<<<1, 256, 0, st>>>(h->fsh + (size_t)(j & 1u) * 5 * W, W, W,
+                                           h->g_fsh + (size_t)kFusedSlot * h->rank);
+}
+const double *fast_fused_shares(const cwf_hip_system *h, unsigned j, unsigned *stride)
+{
+    *stride = h->ds.t.lnwork;
+    return h->fsh + (size_t)(j & 1u) * 5 * h->ds.t.lnwork;
 }
 
 // the convergence of the batch's last launch (it iterations enqueued: launch it's r)
