@@ -342,9 +342,9 @@ int fused_exchange(const std::vector<cwf_hip_system *> &g, unsigned j)
     cwf_hip_system *h0 = g[0];
     if (h0->comm && h0->comm->kind == 2 && h0->nranks > 1)
     {
-        unsigned stride = 0;
-        const double *sh = fast_fused_shares(h0, j, &stride);
-        PeerFold f{sh, nullptr, stride, stride};
+        unsigned stride = 0, count = 0;
+        const double *sh = fast_fused_shares(h0, j, &stride, &count);
+        PeerFold f{sh, nullptr, count, stride};
         return peer_exchange(h0, {Gather{&cwf_hip_system::g_fsh, kFusedSlotHost}}, {fast_fused_ap(h0, j)}, &f);
     }
     std::vector<std::vector<float *>> vecs;

@@ -315,6 +315,7 @@ struct cwf_hip_system
     double *g_fsh = nullptr;  // a shard's all-gathered rank totals of the fused shares, [nranks][8] (one rank: [8])
     bool cls_global = false;  // a shard's ghost class bytes hold their owners' (global) classes
     int fused_agreed = -1;    // a shard: every rank runs the fused iteration (1) or none (0); -1: not asked yet
+    unsigned fused_grid = 0, fused_items = 0;  // the fused launch's grid and the work items it was sized for
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's
@@ -452,7 +453,7 @@ void fast_fused_finish(cwf_hip_system *h, hipStream_t st);
 void fast_fused_launch0(cwf_hip_system *h, hipStream_t st);
 float *fast_fused_ap(cwf_hip_system *h, unsigned j);
 void fast_fused_rank_totals(cwf_hip_system *h, unsigned j, hipStream_t st);
-const double *fast_fused_shares(const cwf_hip_system *h, unsigned j, unsigned *stride);
+const double *fast_fused_shares(const cwf_hip_system *h, unsigned j, unsigned *stride, unsigned *count);
 void fast_fused_cls_out(cwf_hip_system *h, hipStream_t st);  // owned class bytes -> tmp (x components)
 void fast_fused_cls_in(cwf_hip_system *h, hipStream_t st);   // ghost class bytes <- tmp
 constexpr size_t kFusedSlotHost = 8;  // doubles per rank of the gathered fused totals (lattice_fused.inc kFusedSlot)

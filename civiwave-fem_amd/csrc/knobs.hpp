@@ -41,7 +41,7 @@ inline constexpr Knob kKnobs[] = {
     // PCG schedule (spmv_tiles.hip)
     {"CWF_FUSED", "0: structured blocks run the two-kernel iteration (k_keff_lattice + k_pcg_update_tiles) instead of "
                   "the fused one-launch iteration (lattice_fused.inc)"},
-    {"CWF_FUSED_MAXWG", "n: the largest lattice grid that runs the fused iteration (default 1024 workgroups)"},
+    {"CWF_FUSED_MAXWG", "n: cap on the fused launch's grid (default 1024 workgroups; a grid below the work items walks them persistently)"},
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
     // multi-GPU (comm.cpp)

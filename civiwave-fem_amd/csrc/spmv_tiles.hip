@@ -2052,8 +2052,15 @@ bool fast_fused(const cwf_hip_system *h)
         return e && atoi(e) > 0 ? (unsigned)atoi(e) : 1024u;
     }();
     const DevTiles &t = h->ds.t;
-    return on && h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && h->g_fsh &&
-           t.lnwork <= maxwg && t.ntiles;
+    if (!(on && h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && h->g_fsh && t.ntiles))
+        return false;
+    if (h->fused_grid == 0 || h->fused_items != t.lnwork)  // per plan (attach re-plans a shard's work items)
+    {
+        cwf_hip_system *m = const_cast<cwf_hip_system *>(h);
+        m->fused_grid = pcg_lattice_grid(h->ds, maxwg);
+        m->fused_items = t.lnwork;
+    }
+    return true;
 }
 
 namespace
@@ -2067,6 +2074,7 @@ FusedArgs fused_args(cwf_hip_system *h, unsigned j)
     FusedArgs fa{};
     fa.ctl = h->ctl;
     fa.sstride = W;
+    fa.grid = h->fused_grid;
     if (h->sharded())  // every rank folds the all-gathered rank totals, in rank order
     {
         fa.sin = h->g_fsh;
@@ -2077,7 +2085,7 @@ FusedArgs fused_args(cwf_hip_system *h, unsigned j)
     else
     {
         fa.sin = h->fsh + (size_t)((j + 1u) & 1u) * 5 * W;
-        fa.nin = W;
+        fa.nin = h->fused_grid;
         fa.sin_stride = W;
         fa.sis = 1;
     }
@@ -2152,12 +2160,13 @@ float *fast_fused_ap(cwf_hip_system *h, unsigned j) { return (j & 1u) ? h->ap2 :
 void fast_fused_rank_totals(cwf_hip_system *h, unsigned j, hipStream_t st)
 {
     const unsigned W = h->ds.t.lnwork;
-    k_fused_rank_totals<<<1, 256, 0, st>>>(h->fsh + (size_t)(j & 1u) * 5 * W, W, W,
+    k_fused_rank_totals<<<1, 256, 0, st>>>(h->fsh + (size_t)(j & 1u) * 5 * W, h->fused_grid, W,
                                            h->g_fsh + (size_t)kFusedSlot * h->rank);
 }
-const double *fast_fused_shares(const cwf_hip_system *h, unsigned j, unsigned *stride)
+const double *fast_fused_shares(const cwf_hip_system *h, unsigned j, unsigned *stride, unsigned *count)
 {
     *stride = h->ds.t.lnwork;
+    *count = h->fused_grid;
     return h->fsh + (size_t)(j & 1u) * 5 * h->ds.t.lnwork;
 }
 

@@ -239,12 +239,15 @@ def test_fast_solve_run_to_run_deterministic(mesh, monkeypatch):
         assert np.array_equal(r.view(np.uint32), runs[0][2].view(np.uint32))
 
 
-@pytest.mark.parametrize("name", ["33x9x5", "rollers", "c1", "rayleigh"])
+@pytest.mark.parametrize("name", ["33x9x5", "rollers", "c1", "rayleigh", "33x9x5-persistent"])
 def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
     """The fused one-launch iteration (lattice_fused.inc: r, z, p, x formed in the launch that applies K_eff; beta's
     numerator r_(j+1).z_(j+1) expanded through r_(j+1) = r_j - alpha Ap_j from the launch's own dots) against the
     reference loop's two kernels on the same handle geometry: the same solution to 1e-4 of the oracle's and an
     iteration count within 5% (tools/cg_variants.py emulates both in FAST arithmetic on the CPU)."""
+    if name.endswith("-persistent"):  # a grid of 16 workgroups walking every work item (C3's shape at small scale)
+        monkeypatch.setenv("CWF_FUSED_MAXWG", "16")
+        name = name.split("-")[0]
     case = CASES[name]()
     rhs = case.static_rhs()
     mi = case.cfg.solver.max_iterations
