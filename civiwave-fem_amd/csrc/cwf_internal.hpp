@@ -316,6 +316,7 @@ struct cwf_hip_system
     bool cls_global = false;  // a shard's ghost class bytes hold their owners' (global) classes
     int fused_agreed = -1;    // a shard: every rank runs the fused iteration (1) or none (0); -1: not asked yet
     unsigned fused_grid = 0, fused_items = 0;  // the fused launch's grid and the work items it was sized for
+    bool fused_on = false;                     // CWF_FUSED as it was when the handle first asked
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's

@@ -2043,24 +2043,18 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
 // workgroup folds five shares of each of the previous launch's workgroups)
 bool fast_fused(const cwf_hip_system *h)
 {
-    static const int on = [] {
-        const char *e = knob("CWF_FUSED");
-        return e ? atoi(e) : 1;
-    }();
-    static const unsigned maxwg = [] {
-        const char *e = knob("CWF_FUSED_MAXWG");
-        return e && atoi(e) > 0 ? (unsigned)atoi(e) : 1024u;
-    }();
     const DevTiles &t = h->ds.t;
-    if (!(on && h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && h->g_fsh && t.ntiles))
+    if (!(h->mode == CWF_MODE_FAST && t.lat && t.lcls && t.lcz && h->r2 && h->fsh && h->g_fsh && t.ntiles))
         return false;
-    if (h->fused_grid == 0 || h->fused_items != t.lnwork)  // per plan (attach re-plans a shard's work items)
+    if (h->fused_grid == 0 || h->fused_items != t.lnwork)  // per handle and plan (attach re-plans a shard's items)
     {
         cwf_hip_system *m = const_cast<cwf_hip_system *>(h);
-        m->fused_grid = pcg_lattice_grid(h->ds, maxwg);
+        const char *on = knob("CWF_FUSED"), *cap = knob("CWF_FUSED_MAXWG");
+        m->fused_on = !(on && atoi(on) == 0);
+        m->fused_grid = pcg_lattice_grid(h->ds, cap && atoi(cap) > 0 ? (unsigned)atoi(cap) : 1024u);
         m->fused_items = t.lnwork;
     }
-    return true;
+    return h->fused_on;
 }
 
 namespace
