@@ -1421,9 +1421,10 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     if (t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration's one launch (lattice_fused.inc)
     {
         static thread_local char name[112];
-        snprintf(name, sizeof name, "k_pcg_lattice<%s, %s, %s, %s, %s>", t.lsym ? "true" : "false",
+        snprintf(name, sizeof name, "k_pcg_lattice<%s, %s, %s, %s, %s, %s>", t.lsym ? "true" : "false",
                  t.lhex ? "LatHex" : "LatKuhn", t.lmu ? "true" : "false", t.lpstride ? "true" : "false",
-                 !t.lpstride && h->ds.Nown < h->ds.N ? "true" : "false");
+                 !t.lpstride && h->ds.Nown < h->ds.N ? "true" : "false",
+                 h->fused_grid < t.lnwork ? "true" : "false");
         return name;
     }
     if (t.lat)  // as rocprofv3 names it, less the namespaces
