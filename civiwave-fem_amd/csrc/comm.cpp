@@ -757,6 +757,11 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         t.lk0 = k0 < k1 ? k0 : 0;
         t.lk1 = k0 < k1 ? k1 : 1;
         t.lzr = 0;  // the update pass stores z: the halo exchange carries z, and a ghost's class is a local one
+        // a shard with ghosts takes the plane table even where its planes are affine (rank 0 of a slab stack: the
+        // ghost plane stored right after the owned ones): the fused launch's ghost-plane stores of r_j / p_j are
+        // instantiated on the plane-table kernels only
+        if (h->ds.Nown < h->ds.N)
+            t.lpstride = 0;
         lattice_plan(t);
         if (h->fsh)  // the fused iteration's shares for the shard's work items, its gathered rank totals
         {

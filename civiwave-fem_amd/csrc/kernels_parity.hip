@@ -280,15 +280,11 @@ __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint3
 // work, 293 us).
 constexpr int kTileTets = 256;
 constexpr int kIncAhead = 4;  // a node's next incidence entries held in registers
-// The PCG loop's compact-tile instantiation (ISO, no sanitize, SET): round 4 held it to 128 VGPRs, 4 waves per SIMD
-// instead of 3 at 132, no spill (C3 PARITY K_eff 1,260 -> 1,124 us, C2 121 -> 124 us, same box: profiles/r04zg_*).
-// With two batches in flight it needs 148: CWF_PARITY_TILE_WAVES (compile time, default 3) waves per SIMD; at 4 it
-// spills 64 B per lane. The others keep their registers.
-#ifndef CWF_PARITY_TILE_WAVES
-#define CWF_PARITY_TILE_WAVES 3
-#endif
+// The PCG loop's compact-tile instantiation (ISO, no sanitize, SET) is held to 128 VGPRs: 4 waves per SIMD instead
+// of 3 at 132, no spill (C3 PARITY K_eff 1,260 -> 1,124 us, C2 121 -> 124 us, same box: profiles/r04zg_*); the
+// others spill at 128 and keep their registers.
 template <bool ISO, bool SANITIZE, bool DOT, bool SET>
-__global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? CWF_PARITY_TILE_WAVES : 1) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
+__global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? 4 : 1) void k_keff_parity_tile(DevSys s, const float *__restrict__ x,
                                                              float *__restrict__ y, const Ctl *__restrict__ ctl,
                                                              double *__restrict__ pdot, uint32_t nlim,
                                                              uint32_t chunks)
@@ -318,10 +314,8 @@ __global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? CWF_PARITY_TILE_W
 #pragma unroll
     for (int i = 0; i < kIncAhead; ++i)
         qa[i] = j + i < jend ? s.pinc[j + i] : 0xFFFFFFFFu;
-    // software pipeline over batches, two deep: at batch b the record of batch b + 2 and the corner gathers of batch
-    // b + 1 (whose record arrived during batch b - 1) are issued before batch b's math, so a gather has the whole of
-    // a batch (math, fold, two barriers) to return instead of the fold alone (round 4: one batch ahead, the corner
-    // gathers issued after the math; SQ WAIT_ANY 0.72 of wave cycles)
+    // software pipeline over batches: batch b's operands were gathered during batch b - 1; the next batch's record
+    // is issued before this batch's math and its corner gathers before the fold
     const uint32_t tid = threadIdx.x;
     TetIn<SANITIZE> cur;
     uint32_t e_cur = tid < nt ? s.ptile_tets[t0 + tid] : 0u;
@@ -331,22 +325,15 @@ __global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? CWF_PARITY_TILE_W
         tet_gather<SANITIZE>(s, x, e_cur, cur);
     }
     uint32_t e_nxt = kTileTets + tid < nt ? s.ptile_tets[t0 + kTileTets + tid] : 0u;
-    Grad g_nxt;  // batch b + 1's record, in flight
-    if (kTileTets + tid < nt)
-        load_erec(s.erec, e_nxt, g_nxt);
-    uint32_t e_nn = 2 * kTileTets + tid < nt ? s.ptile_tets[t0 + 2 * kTileTets + tid] : 0u;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     __syncthreads();  // dtab
     for (uint32_t base = 0; base < nt; base += kTileTets)
     {
-        const bool has_nxt = base + kTileTets + tid < nt, has_nn = base + 2 * kTileTets + tid < nt;
+        const bool has_nxt = base + kTileTets + tid < nt;
         TetIn<SANITIZE> nxt;
-        nxt.G = g_nxt;
         if (has_nxt)
-            tet_gather<SANITIZE>(s, x, e_nxt, nxt);
-        if (has_nn)
-            load_erec(s.erec, e_nn, g_nxt);
-        const uint32_t e_n3 = base + 3 * kTileTets + tid < nt ? s.ptile_tets[t0 + base + 3 * kTileTets + tid] : 0u;
+            load_erec(s.erec, e_nxt, nxt.G);
+        const uint32_t e_nn = base + 2 * kTileTets + tid < nt ? s.ptile_tets[t0 + base + 2 * kTileTets + tid] : 0u;
         if (base + tid < nt)
         {
             double gx[4], gy[4], gz[4], sig[6];
@@ -364,6 +351,8 @@ __global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? CWF_PARITY_TILE_W
                     fs[2][sl] = f[2];
                 }
         }
+        if (has_nxt)
+            tet_gather<SANITIZE>(s, x, e_nxt, nxt);
         __syncthreads();
         // incidences are ascending in element order, so in tile-local tet order: the node's entries below lim are
         // this batch's, consumed in order
@@ -399,7 +388,6 @@ __global__ __launch_bounds__(kBlock, ISO && !SANITIZE && SET ? CWF_PARITY_TILE_W
         __syncthreads();
         cur = nxt;
         e_nxt = e_nn;
-        e_nn = e_n3;
     }
     float yv[3] = {0.f, 0.f, 0.f}, xv[3] = {0.f, 0.f, 0.f};
     if (n < s.N)

@@ -40,7 +40,8 @@ inline constexpr Knob kKnobs[] = {
                          "compact breadth-first tiles and a separate p.Ap partials pass; shards always use strips)"},
     // PCG schedule (spmv_tiles.hip)
     {"CWF_FUSED", "0: structured blocks run the two-kernel iteration (k_keff_lattice + k_pcg_update_tiles) instead of "
-                  "the fused one-launch iteration (lattice_fused.inc)"},
+                  "the fused one-launch iteration (lattice_fused.inc); 2: fused also where the grid walks the work items "
+                  "persistently (default: fused only where one round of workgroups covers them)"},
     {"CWF_FUSED_MAXWG", "n: cap on the fused launch's grid (default 1024 workgroups; a grid below the work items walks them persistently)"},
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},

@@ -534,7 +534,25 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
                 zh[3 * n + k] = pat(n, k);
         HIPTRY(h, hipMemcpyAsync(h->z, zh.data(), zh.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
     }
+    // a step that timed out (a peer that never arrived, or a communicator already dead: its steps return at entry)
+    // only shows in the control block: report it, then clear the solve fields so the next solve starts clean (the
+    // communicator's sticky word stays set)
+    const auto step_error = [&]() -> int {
+        Ctl c{};
+        HIPTRY(h, hipStreamSynchronize(h->stream));
+        HIPTRY(h, hipMemcpy(&c, h->ctl, sizeof c, hipMemcpyDeviceToHost));
+        if (!c.error)
+            return 0;
+        const int code = c.error, at = c.error_iter;
+        c.error = 0;
+        c.error_iter = 0;
+        HIPTRY(h, hipMemcpy(h->ctl, &c, sizeof c, hipMemcpyHostToDevice));
+        return set_error(h, code, code == CWF_ERR_COMM ? "peer exchange timed out" : "exchange step failed",
+                         "step=" + std::to_string(at));
+    };
     int st = step();  // warm
+    if (!st)
+        st = step_error();  // before the halo check: a timed-out step delivered nothing
     if (!st && check)
     {
         HIPTRY(h, hipStreamSynchronize(h->stream));
@@ -557,21 +575,7 @@ int cwf_hip_comm_time_exchange(cwf_hip_system *h, int32_t steps, double *us_per_
     *us_per_step = 1e3 * (double)ms / steps;
     if (st)
         return st;
-    // a step that timed out (a peer that never arrived) only shows in the control block: report it, then clear the
-    // solve fields so the next solve starts clean (the communicator's sticky word stays set: it is dead)
-    Ctl c{};
-    HIPTRY(h, hipStreamSynchronize(h->stream));
-    HIPTRY(h, hipMemcpy(&c, h->ctl, sizeof c, hipMemcpyDeviceToHost));
-    if (c.error)
-    {
-        const int code = c.error, at = c.error_iter;
-        c.error = 0;
-        c.error_iter = 0;
-        HIPTRY(h, hipMemcpy(h->ctl, &c, sizeof c, hipMemcpyHostToDevice));
-        return set_error(h, code, code == CWF_ERR_COMM ? "peer exchange timed out" : "exchange step failed",
-                         "step=" + std::to_string(at));
-    }
-    return 0;
+    return step_error();
 }
 
 int cwf_hip_comm_peer_mailbox_kind(const cwf_hip_comm *cm, int *kind)

@@ -2050,9 +2050,14 @@ bool fast_fused(const cwf_hip_system *h)
     {
         cwf_hip_system *m = const_cast<cwf_hip_system *>(h);
         const char *on = knob("CWF_FUSED"), *cap = knob("CWF_FUSED_MAXWG");
-        m->fused_on = !(on && atoi(on) == 0);
         m->fused_grid = pcg_lattice_grid(h->ds, cap && atoi(cap) > 0 ? (unsigned)atoi(cap) : 1024u);
         m->fused_items = t.lnwork;
+        // default: fused where one round of workgroups covers the work items (C2 fused 46.6k vs two-kernel 46.9k
+        // PCG it/s, same box: one launch and one exchange per iteration for the same time). Beyond one round the
+        // persistent walk (234-248 VGPRs, 2 waves/SIMD) loses to the two kernels: C3 8.3k vs 10.8k it/s
+        // (profiles/r05b). CWF_FUSED=2 forces it, 0 turns it off
+        const int v = on ? atoi(on) : 1;
+        m->fused_on = v == 2 || (v == 1 && m->fused_grid >= t.lnwork);
     }
     return h->fused_on;
 }

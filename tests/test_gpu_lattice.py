@@ -245,24 +245,25 @@ def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
     numerator r_(j+1).z_(j+1) expanded through r_(j+1) = r_j - alpha Ap_j from the launch's own dots) against the
     reference loop's two kernels on the same handle geometry: the same solution to 1e-4 of the oracle's and an
     iteration count within 5% (tools/cg_variants.py emulates both in FAST arithmetic on the CPU)."""
-    if name.endswith("-persistent"):  # a grid of 16 workgroups walking every work item (C3's shape at small scale)
-        monkeypatch.setenv("CWF_FUSED_MAXWG", "16")
-        name = name.split("-")[0]
+    on = "1"
+    if name.endswith("-persistent"):  # a grid of 16 workgroups walking every work item (C3's shape at small scale;
+        monkeypatch.setenv("CWF_FUSED_MAXWG", "16")  # forced: by default a grid below the items runs two kernels)
+        name, on = name.split("-")[0], "2"
     case = CASES[name]()
     rhs = case.static_rhs()
     mi = case.cfg.solver.max_iterations
     out = {}
-    for fused in ("1", "0"):
+    for fused in (on, "0"):
         monkeypatch.setenv("CWF_FUSED", fused)
         s = _system(case)
-        assert _kernel(s).startswith("k_pcg_lattice" if fused == "1" else "k_keff_lattice"), _kernel(s)
+        assert _kernel(s).startswith("k_pcg_lattice" if fused != "0" else "k_keff_lattice"), _kernel(s)
         x = np.zeros_like(rhs)
         r = np.zeros_like(rhs)
         t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(mi, 1e-6), pcg.PcgVectors(x, r)).value()
         assert t.converged
         # the r output is the residual of x (rhs - K x, Dirichlet rows 0) to fp32 accuracy
         out[fused] = (t, x, r)
-    (tf, xf, rf), (tk, xk, _) = out["1"], out["0"]
+    (tf, xf, rf), (tk, xk, _) = out[on], out["0"]
     ref = oracle_system(case.packing, case.materials, *case.scalars()).solve_pcg(rhs, mi, 1e-6)
     assert np.linalg.norm(xf - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
     assert abs(tf.iterations - tk.iterations) <= max(3, tk.iterations // 20), (tf.iterations, tk.iterations)

@@ -83,7 +83,8 @@ def test_peer_lattice_slabs_equal_local(nranks):
     glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
     x = _assemble(out, glob.packing.node_count)
     for d in out.values():
-        assert d["kernel"].startswith("k_keff_lattice"), d["kernel"]
+        # the fused lattice iteration with its ghost-plane stores (SHARD), on every rank (rank 0's affine planes too)
+        assert d["kernel"].startswith("k_pcg_lattice") and d["kernel"].endswith("true, false>"), d["kernel"]
         assert d["mailbox_kind"] == _lib.PEER_MAILBOX_UNCACHED, d["mailbox_kind"]
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
         # refused (the slabs are not whole reduction chunks, and PEER carries the FAST schedule only), never a hang
