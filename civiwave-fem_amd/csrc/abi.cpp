@@ -1403,6 +1403,13 @@ const char *cwf_hip_system_keff_source_hash(const cwf_hip_system *h)
     return h->mode != CWF_MODE_FAST || !h->ds.t.ntiles ? CWF_PARITY_SRC_HASH : CWF_FAST_SRC_HASH;
 }
 
+int cwf_hip_system_exchange_schedule(const cwf_hip_system *h)
+{
+    if (!h || !h->sharded() || h->fused_agreed < 0)
+        return -1;
+    return h->fused_agreed == 0 ? 0 : h->px_agreed == 1 ? 2 : 1;
+}
+
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
 {
     if (!h)

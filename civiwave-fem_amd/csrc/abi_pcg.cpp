@@ -174,8 +174,13 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             batch = std::min<uint64_t>(batch * 2, kMaxBatch);
     }
     if (fused)  // x is updated in every launch; the solve's r output is the last launch's
+    {
         for (cwf_hip_system *m : g)
             fast_fused_finish(m, m->stream);
+        if (sharded)
+            if (int e = sharded_fused_end(g))
+                return e;
+    }
     else if (fast)  // x += alpha_j p_j of the iterations since the last lazy x update
         for (size_t i = 0; i < g.size(); ++i)
             fast_flush_x(g[i], rhs[i], g[i]->stream);

@@ -309,28 +309,36 @@ bool group_fused(const std::vector<cwf_hip_system *> &g)
     bool mine = true;
     for (cwf_hip_system *h : g)
         mine = mine && fast_fused(h) && h->ds.t.lat;
+    // and the exchange inside the launches (PEER: one member per process)
+    const bool px = mine && g.size() == 1 && peer_fused_eligible(h0);
     for (cwf_hip_system *h : g)
     {
-        const double v[2] = {mine ? 1.0 : 0.0, 0.0};
+        const double v[2] = {mine ? 1.0 : 0.0, px ? 1.0 : 0.0};
         if (hipMemcpyAsync(h->g_init + 2 * h->rank, v, sizeof v, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
             hipStreamSynchronize(h->stream) != hipSuccess)
             mine = false;
     }
-    bool all = mine;
+    bool all = mine, all_px = px;
     if (comm_allgather(g, &cwf_hip_system::g_init, 2) == 0)
     {
         std::vector<double> f(2 * (size_t)h0->nranks, 0.0);
         if (hipStreamSynchronize(h0->stream) == hipSuccess &&
             hipMemcpy(f.data(), h0->g_init, f.size() * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess)
             for (int r = 0; r < h0->nranks; ++r)
+            {
                 all = all && f[2 * (size_t)r] == 1.0;
+                all_px = all_px && f[2 * (size_t)r + 1] == 1.0;
+            }
         else
             all = false;
     }
     else
         all = false;
     for (cwf_hip_system *h : g)
+    {
         h->fused_agreed = all ? 1 : 0;
+        h->px_agreed = all && all_px ? 1 : 0;
+    }
     return all;
 }
 
@@ -391,16 +399,24 @@ int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector
         fast_init_scalars_strided(h, h->g_init, h->g_init + 1, (uint32_t)h->nranks, 2u, rel_tol, h->stream);
     if (int st = comm_halo(g, &cwf_hip_system::r))  // r_0's ghost rows (launch 0 forms ghost p_0 from them)
         return st;
+    if (g[0]->px_agreed == 1)  // the launches exchange themselves: epochs from here
+        if (int st = peer_fused_begin(g[0]))
+            return st;
     for (cwf_hip_system *h : g)
         fast_fused_launch0(h, h->stream);
-    return fused_exchange(g, 0);
+    return g[0]->px_agreed == 1 ? 0 : fused_exchange(g, 0);
 }
 
 int sharded_fused_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1)
 {
     for (size_t i = 0; i < g.size(); ++i)
         fast_fused_iteration(g[i], it, g[i]->stream, i ? nullptr : e0, i ? nullptr : e1);
-    return fused_exchange(g, it + 1u);
+    return g[0]->px_agreed == 1 ? 0 : fused_exchange(g, it + 1u);
+}
+
+int sharded_fused_end(const std::vector<cwf_hip_system *> &g)
+{
+    return g[0]->px_agreed == 1 ? peer_fused_end(g[0]) : 0;
 }
 
 // ---- sharded PARITY (SURVEY.md 8e parity gate): the reference's fold orders across ranks --------------------

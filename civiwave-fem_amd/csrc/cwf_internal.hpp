@@ -315,6 +315,9 @@ struct cwf_hip_system
     double *g_fsh = nullptr;  // a shard's all-gathered rank totals of the fused shares, [nranks][8] (one rank: [8])
     bool cls_global = false;  // a shard's ghost class bytes hold their owners' (global) classes
     int fused_agreed = -1;    // a shard: every rank runs the fused iteration (1) or none (0); -1: not asked yet
+    int px_agreed = 0;        // ... and exchanges inside its launches (PEER, every rank eligible)
+    int32_t px_send_k[2] = {-1, -1};  // the lattice plane of each neighbour slot's send segment
+    uint32_t px_ebase = 0;            // the communicator's epoch before the solve's launch 0
     unsigned fused_grid = 0, fused_items = 0;  // the fused launch's grid and the work items it was sized for
     bool fused_on = false;                     // CWF_FUSED as it was when the handle first asked
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
@@ -462,6 +465,7 @@ constexpr size_t kFusedSlotHost = 8;  // doubles per rank of the gathered fused 
 int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
 int sharded_fused_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1);
 bool group_fused(const std::vector<cwf_hip_system *> &g);
+int sharded_fused_end(const std::vector<cwf_hip_system *> &g);  // after the last launch (PEER in-kernel epochs)
 
 unsigned fast_tile_blocks(const DevSys &s);
 unsigned fast_pipe_grid(const DevSys &s);
@@ -503,6 +507,29 @@ struct PeerFold
 int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, const std::vector<float *> &vecs,
                   const PeerFold *fold = nullptr);
 void peer_release(cwf_hip_comm *cm);
+// The fused lattice iteration's exchange inside its own launch (PEER only; lattice_fused.inc): launch j of a solve
+// pushes its Ap send rows (whole owned planes) straight into the neighbours' receive areas and, from its last
+// workgroup, the rank totals into every rank's gather area and epoch ebase + j + 1 into every peer's flag; launch
+// j + 1 waits for every peer's epoch ebase + j in its prologue. Launch arguments (this launch's parities):
+struct FusedPeerArgs
+{
+    float *dst[2];          // send entry e: the neighbour's receive area at my segment's first float
+    uint32_t dst_bytes[2];  // the descriptor range of dst[e] (0: no entry)
+    int32_t send_k[2];      // the lattice plane entry e sends (-1: none); row (i, j) -> float 3 (j nx + i)
+    double *gdst[kMaxPeers];    // per rank p: p's gather area, my slot (this rank's too)
+    uint32_t *flag[kMaxPeers];  // per rank p != rank: p's flag line for my rank
+    const uint32_t *flags;      // my flag lines (peer p's first word at flags[16 p])
+    uint32_t *ticket, *sticky, *done;
+    const float *arecv;  // my receive area of the previous launch's epoch (the ghost Ap rows), launch j > 0
+    uint32_t epoch, nranks, rank;
+};
+// this rank's half of the collective decision (a host check of the halo plan: every send segment one whole owned
+// plane in plane order, <= 2 of them; ranks on one device only while all their grids are resident together)
+bool peer_fused_eligible(cwf_hip_system *h);
+void peer_fused_args(const cwf_hip_system *h, unsigned j, FusedPeerArgs &pe, const double **gath_prev);
+int peer_fused_begin(cwf_hip_system *h);  // before launch 0: the epoch base; the launch ticket cleared
+int peer_fused_end(cwf_hip_system *h);    // after the solve: the communicator's epoch = the last launch that pushed
+unsigned pcg_lattice_resident_count(const DevSys &s);  // resident workgroups of the fused launch
 int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                        const std::vector<std::vector<float *>> &vecs);
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);

@@ -410,6 +410,114 @@ int peer_exchange(cwf_hip_system *h, std::initializer_list<Gather> gathers, cons
     return e == hipSuccess ? 0 : hip_fail(h, e, "peer exchange launch");
 }
 
+// ---- the fused lattice iteration's in-kernel exchange (lattice_fused.inc: fused_peer_wait / fused_peer_publish) ----
+bool peer_fused_eligible(cwf_hip_system *h)
+{
+    cwf_hip_comm *cm = h->comm;
+    const char *on = knob("CWF_PEER_FUSED");
+    if (!cm || cm->kind != 2 || cm->nranks < 2 || (on && atoi(on) == 0) || !h->ds.t.lat || h->ds.Nown >= h->ds.N ||
+        cm->peer_mbox.size() != (size_t)cm->nranks || h->nbr.size() > 2 || h->lat_plane.size() != h->ds.t.lnz)
+        return false;
+    // every send segment is one whole owned plane in plane order: row (i, j) of plane k is its 3 (j nx + i)-th float
+    const uint64_t nsend = h->send_off.empty() ? 0 : h->send_off.back();
+    std::vector<uint32_t> idx(nsend);
+    if (nsend && hipMemcpy(idx.data(), h->send_idx, nsend * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
+    const uint32_t per = h->ds.t.lnx * h->ds.t.lny;
+    h->px_send_k[0] = h->px_send_k[1] = -1;
+    for (size_t k = 0; k < h->nbr.size(); ++k)
+    {
+        const uint64_t a = h->send_off[k], b = h->send_off[k + 1];
+        if (b - a != per)
+            return false;
+        int32_t plane = -1;
+        for (uint32_t q = 0; q < h->ds.t.lnz; ++q)
+            if (h->lat_plane[q] == idx[a] && h->lat_plane[q] + per <= h->ds.Nown)
+                plane = (int32_t)q;
+        if (plane < 0)
+            return false;
+        for (uint64_t r = 0; r < per; ++r)
+            if (idx[a + r] != idx[a] + r)
+                return false;
+        h->px_send_k[k] = plane;
+    }
+    // ranks on one device (a rehearsal): each rank's launch waits for the others' previous one, so all their grids
+    // must be resident together
+    bool same = false;
+    for (int p = 0; p < cm->nranks; ++p)
+    {
+        if (p == cm->rank)
+            continue;
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, cm->peer_mbox[p]) != hipSuccess || at.device == cm->device)
+        {
+            (void)hipGetLastError();
+            same = true;
+        }
+    }
+    if (same && (uint64_t)h->fused_grid * (uint64_t)cm->nranks > pcg_lattice_resident_count(h->ds))
+        return false;
+    return true;
+}
+
+void peer_fused_args(const cwf_hip_system *h, unsigned j, FusedPeerArgs &pe, const double **gath_prev)
+{
+    const cwf_hip_comm *cm = h->comm;
+    const int n = cm->nranks;
+    const uint32_t epoch = h->px_ebase + j + 1u, par = epoch & 1u, prev = (epoch - 1u) & 1u;
+    pe = FusedPeerArgs{};
+    for (size_t k = 0; k < 2; ++k)
+    {
+        pe.send_k[k] = -1;
+        if (k >= h->nbr.size() || h->px_send_k[k] < 0)
+            continue;
+        const int q = h->nbr[k];
+        const uint64_t qg = cm->peer_nghost[q], qoff = cm->peer_recv_off[q];
+        char *base = static_cast<char *>(cm->peer_mbox[q]) + off_recv(n) + par * recv_bytes(qg);
+        pe.dst[k] = reinterpret_cast<float *>(base) + 3 * qoff;
+        pe.dst_bytes[k] = (uint32_t)(12ull * (h->send_off[k + 1] - h->send_off[k]));
+        pe.send_k[k] = h->px_send_k[k];
+    }
+    for (int p = 0; p < n; ++p)
+    {
+        char *pb = static_cast<char *>(p == h->rank ? cm->mbox : cm->peer_mbox[p]);
+        pe.gdst[p] = reinterpret_cast<double *>(pb + off_gath(n) + par * gath_bytes(n)) + (size_t)h->rank * kSlot;
+        pe.flag[p] = reinterpret_cast<uint32_t *>(pb + off_flags() + kFlagLine * (size_t)h->rank);
+    }
+    static_assert(kFlagLine == 64, "fused_peer_wait polls flags[16 p]");
+    pe.flags = reinterpret_cast<const uint32_t *>(static_cast<char *>(cm->mbox) + off_flags());
+    pe.ticket = cm->ticket + 16;
+    pe.sticky = cm->ticket + 32;
+    pe.done = cm->ticket + 48;
+    const uint64_t nghost = h->ds.N - h->ds.Nown;
+    pe.arecv = reinterpret_cast<const float *>(static_cast<char *>(cm->mbox) + off_recv(n) + prev * recv_bytes(nghost));
+    pe.epoch = epoch;
+    pe.nranks = (uint32_t)n;
+    pe.rank = (uint32_t)h->rank;
+    // gather 0 of the previous epoch: rank p's totals at [kSlot p]
+    *gath_prev = reinterpret_cast<const double *>(static_cast<char *>(cm->mbox) + off_gath(n) + prev * gath_bytes(n));
+}
+
+int peer_fused_begin(cwf_hip_system *h)
+{
+    cwf_hip_comm *cm = h->comm;
+    h->px_ebase = cm->epoch;
+    HIPTRY(h, hipMemsetAsync(cm->ticket + 16, 0, sizeof(uint32_t), h->stream));
+    return 0;
+}
+
+int peer_fused_end(cwf_hip_system *h)
+{
+    cwf_hip_comm *cm = h->comm;
+    uint32_t done = 0;
+    HIPTRY(h, hipStreamSynchronize(h->stream));
+    HIPTRY(h, hipMemcpy(&done, cm->ticket + 48, sizeof done, hipMemcpyDeviceToHost));
+    // launches that pushed: epochs ebase + 1 .. done (none: the solve ended at its prologue)
+    if (done > h->px_ebase && done - h->px_ebase < (1u << 30))
+        cm->epoch = done;
+    return 0;
+}
+
 }  // namespace cwf
 
 using namespace cwf;

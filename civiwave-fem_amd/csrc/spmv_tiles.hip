@@ -2039,6 +2039,8 @@ void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t s
 }
 
 // ---- the fused lattice iteration (lattice_fused.inc) --------------------------------------------------------
+unsigned pcg_lattice_resident_count(const DevSys &s) { return lattice_resident_count(s); }
+
 // CWF_FUSED=0: the two-kernel iteration on a structured block; CWF_FUSED_MAXWG: the largest grid that fuses (every
 // workgroup folds five shares of each of the previous launch's workgroups)
 bool fast_fused(const cwf_hip_system *h)
@@ -2077,6 +2079,13 @@ FusedArgs fused_args(cwf_hip_system *h, unsigned j)
     if (h->sharded())  // every rank folds the all-gathered rank totals, in rank order
     {
         fa.sin = h->g_fsh;
+        if (h->px_agreed == 1)  // PEER in-kernel: the totals land in the mailbox's gather area (previous epoch)
+        {
+            const double *gp = nullptr;
+            peer_fused_args(h, j, fa.pe, &gp);
+            fa.px = 1;
+            fa.sin = gp;
+        }
         fa.nin = (unsigned)h->nranks;
         fa.sin_stride = 1;
         fa.sis = kFusedSlot;

@@ -136,6 +136,7 @@ def load() -> C.CDLL:
         "cwf_hip_bandwidth_probe": ([i32, u64, i32, P], i32),
         "cwf_hip_system_keff_traffic": ([P, P, P], i32),
         "cwf_hip_system_keff_kernel": ([P], C.c_char_p),
+        "cwf_hip_system_exchange_schedule": ([P], i32),
         "cwf_hip_system_keff_source_hash": ([P], C.c_char_p),
         "cwf_lattice_describe": ([P, i32, P, P, P], i32),
         "cwf_hip_system_set_timing": ([P, i32], i32),

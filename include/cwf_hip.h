@@ -147,6 +147,11 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
 /* Name of the kernel the handle's K_eff launches in its current mode ("k_keff_lattice", "k_keff_groups_pipe",
  * "k_keff_tiles_pipe", "k_keff_tiles", "k_keff_hex_tiles" or "k_keff_parity"); NULL for a NULL handle. */
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
+/* Diagnostic: the PCG schedule a sharded handle's FAST solves run, decided collectively at its first solve:
+ * -1 not decided yet (or not sharded), 0 the two-kernel iteration (two exchange steps per iteration), 1 the fused
+ * lattice iteration with one exchange step per iteration, 2 the fused iteration exchanging inside its launches
+ * (PEER: the Ap send rows, rank totals and epoch flags pushed by the launch itself, no exchange launch). */
+int cwf_hip_system_exchange_schedule(const cwf_hip_system *h);
 /* 16 hex digits: a hash of the source files and build flags of the translation unit that holds that kernel
  * (csrc/Makefile FAST_SRC / PARITY_SRC), so a committed PMC profile can be matched to the code that ran */
 const char *cwf_hip_system_keff_source_hash(const cwf_hip_system *h);

@@ -75,18 +75,28 @@ def _assemble(out, n):
     return x.reshape(-1)
 
 
+@pytest.mark.parametrize("inkernel", [True, False], ids=["in_kernel_exchange", "exchange_step"])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_peer_lattice_slabs_equal_local(nranks):
+def test_peer_lattice_slabs_equal_local(nranks, inkernel):
+    """in_kernel_exchange: the fused launches push their Ap send rows, rank totals and epoch flags themselves and
+    wait for the peers' in their prologue (lattice_fused.inc fused_peer_wait / fused_peer_publish: no exchange
+    launch); exchange_step (CWF_PEER_FUSED=0): one k_peer_step launch after each fused launch. Both equal the LOCAL
+    solve bit for bit, and a second solve on the same communicator repeats the first (the epochs carry over)."""
     shape = (13, 9, 4)
     spec = dict(slab=shape, tol=1e-6, max_iterations=800, timing_steps=1000)
+    if not inkernel:
+        spec["env"] = {"CWF_PEER_FUSED": "0"}
     out = _run(spec, nranks)
     glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
     x = _assemble(out, glob.packing.node_count)
     for d in out.values():
         # the fused lattice iteration with its ghost-plane stores (SHARD), on every rank (rank 0's affine planes too)
         assert d["kernel"].startswith("k_pcg_lattice") and d["kernel"].endswith("true, false>"), d["kernel"]
+        assert d["schedule"] == (2 if inkernel else 1), d["schedule"]
         assert d["mailbox_kind"] == _lib.PEER_MAILBOX_UNCACHED, d["mailbox_kind"]
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
+        assert d["telemetry2"] == d["telemetry"]
+        assert_bitwise(d["x2"], d["x"], "second solve x")
         # refused (the slabs are not whole reduction chunks, and PEER carries the FAST schedule only), never a hang
         assert d["parity_error"] and ("FAST schedule" in d["parity_error"] or "whole" in d["parity_error"]
                                       or "reduction" in d["parity_error"]), d["parity_error"]

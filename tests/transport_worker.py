@@ -178,6 +178,11 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
             queue.put((rank, "error", str(res.error())))
             return
         t = res.value()
+        sched = _lib.load().cwf_hip_system_exchange_schedule(s.handle())
+        # a second solve on the same communicator (the in-kernel exchange's epochs continue across solves)
+        x2 = np.zeros(3 * sh.local_nodes, np.float32)
+        t2 = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]),
+                           pcg.PcgVectors(x2, None)).value()
         us = shard.Comm.time_exchange(s, spec.get("timing_steps", 200))
         # PARITY over PEER is refused (its chunk-partial all-gathers need RCCL / LOCAL)
         s.mode = _lib.MODE_PARITY  # (the handle takes the system's mode at every call)
@@ -186,7 +191,9 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         own = 3 * sh.owned_nodes
         queue.put((rank, "ok", dict(telemetry=(t.iterations, t.converged, t.residual_norm), kernel=kern,
                                     nodes=sh.node_global[: sh.owned_nodes].astype(np.int64), x=x[:own].copy(),
-                                    exchange_us=us, parity_error=perr, mailbox_kind=mkind)))
+                                    exchange_us=us, parity_error=perr, mailbox_kind=mkind, schedule=sched,
+                                    telemetry2=(t2.iterations, t2.converged, t2.residual_norm),
+                                    x2=x2[:own].copy())))
         s.close()
         comm.close()
     except Exception as e:
