@@ -181,8 +181,10 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         sched = _lib.load().cwf_hip_system_exchange_schedule(s.handle())
         # a second solve on the same communicator (the in-kernel exchange's epochs continue across solves)
         x2 = np.zeros(3 * sh.local_nodes, np.float32)
+        t0 = time.perf_counter()
         t2 = pcg.solve_pcg(s, rhs, pcg.PcgSettings(spec["max_iterations"], spec["tol"]),
                            pcg.PcgVectors(x2, None)).value()
+        solve2_s = time.perf_counter() - t0
         us = shard.Comm.time_exchange(s, spec.get("timing_steps", 200))
         # PARITY over PEER is refused (its chunk-partial all-gathers need RCCL / LOCAL)
         s.mode = _lib.MODE_PARITY  # (the handle takes the system's mode at every call)
@@ -193,7 +195,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
                                     nodes=sh.node_global[: sh.owned_nodes].astype(np.int64), x=x[:own].copy(),
                                     exchange_us=us, parity_error=perr, mailbox_kind=mkind, schedule=sched,
                                     telemetry2=(t2.iterations, t2.converged, t2.residual_norm),
-                                    x2=x2[:own].copy())))
+                                    x2=x2[:own].copy(), solve2_s=solve2_s)))
         s.close()
         comm.close()
     except Exception as e:
