@@ -441,8 +441,8 @@ bool peer_fused_eligible(cwf_hip_system *h)
                 return false;
         h->px_send_k[k] = plane;
     }
-    // ranks on one device (a rehearsal): each rank's launch waits for the others' previous one, so all their grids
-    // must be resident together
+    // ranks on one device (a rehearsal): a rank's launch j waits, resident, for the others' launch j - 1, which needs
+    // at least one free slot: the other ranks' launches must leave one (a 2-rank C2 rehearsal: 436 of 512)
     bool same = false;
     for (int p = 0; p < cm->nranks; ++p)
     {
@@ -455,7 +455,7 @@ bool peer_fused_eligible(cwf_hip_system *h)
             same = true;
         }
     }
-    if (same && (uint64_t)h->fused_grid * (uint64_t)cm->nranks > pcg_lattice_resident_count(h->ds))
+    if (same && (uint64_t)h->fused_grid * (uint64_t)(cm->nranks - 1) >= pcg_lattice_resident_count(h->ds))
         return false;
     return true;
 }

@@ -18,8 +18,25 @@ def main():
     shape = tuple(int(v) for v in a[:3]) if len(a) >= 3 else (69, 69, 20)
     nranks = int(a[3]) if len(a) > 3 else 2
     its = int(a[4]) if len(a) > 4 else 400
+    import time
+
+    import numpy as np
+
+    from cwf import _lib, pcg, scenarios
     from test_gpu_peer import _run
 
+    # the same total work as one handle (the ranks' slabs stacked along z) in one process: no exchange at all
+    case = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=1e-30, max_iterations=its)
+    s = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, *case.scalars(), mode=_lib.MODE_FAST)
+    rhs = case.static_rhs()
+    for rep in range(2):
+        x = np.zeros_like(rhs)
+        t0 = time.perf_counter()
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(its, 1e-30), pcg.PcgVectors(x, None)).value()
+        el = time.perf_counter() - t0
+    print(f"{'one handle':14s} block {shape[0]}x{shape[1]}x{shape[2] * nranks}: {t.iterations} iterations, "
+          f"{el / max(t.iterations, 1) * 1e6:.2f} us per iteration", flush=True)
+    s.close()
     for mode, env in (("in-kernel", {}), ("exchange step", {"CWF_PEER_FUSED": "0"})):
         spec = dict(slab=shape, tol=1e-30, max_iterations=its, timing_steps=200, env=env)
         out = _run(spec, nranks)
