@@ -426,8 +426,11 @@ def main():
     L.cwf_hip_system_set_timing(h, 0)
     D = owned_dofs
     local = np.array([elapsed, D * total_iters, total_iters, D], np.float64)
+    # the PCG schedule the ranks agreed on (cwf_hip_system_exchange_schedule): 0 two kernels + two exchange steps,
+    # 1 fused + one exchange step, 2 fused with the exchange inside the launch (PEER)
+    sched = int(L.cwf_hip_system_exchange_schedule(h)) if world > 1 else None
     per_rank = [{"owned_dofs": int(D), "local_tets": int(local_tets), "halo_nodes": int(halo_nodes),
-                 "halo_bytes_per_exchange": 12 * int(halo_nodes), "seconds": elapsed}]
+                 "halo_bytes_per_exchange": 12 * int(halo_nodes), "seconds": elapsed, "schedule": sched}]
     if dist is not None:
         gathered = [None] * world
         dist.all_gather_object(gathered, per_rank[0])

@@ -391,6 +391,7 @@ struct cwf_hip_comm
     uint32_t *ticket = nullptr;  // [0]: the exchange step's ticket; [32]: the sticky device error word
     std::vector<void *> peer_mbox;
     std::vector<uint64_t> peer_nghost, peer_recv_off;
+    std::vector<int> peer_same_device;  // peer p's mailbox is on this rank's device (PCI bus id)
     uint32_t epoch = 0;
 };
 

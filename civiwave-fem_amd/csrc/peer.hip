@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -66,6 +67,7 @@ constexpr uint64_t kPeerTimeoutTicks = 10ull * 100000000ull;  // a wait gives a 
 struct MboxHeader  // at offset 0 of every mailbox
 {
     uint64_t magic, nranks, nghost, recv_off[kMaxPeers], recv_cnt[kMaxPeers];
+    char bus[32];  // the owner's device (hipDeviceGetPCIBusId): peers on the same device are a rehearsal
 };
 static_assert(sizeof(MboxHeader) <= kHdrBytes, "mailbox header");
 
@@ -316,6 +318,12 @@ int peer_attach(cwf_hip_system *h)
         hd.recv_off[h->nbr[k]] = h->recv_off[k];
         hd.recv_cnt[h->nbr[k]] = h->recv_off[k + 1] - h->recv_off[k];
     }
+    if (hipDeviceGetPCIBusId(hd.bus, (int)sizeof hd.bus, cm->device) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        std::snprintf(hd.bus, sizeof hd.bus, "device-%d", cm->device);
+    }
+    hd.bus[sizeof hd.bus - 1] = 0;
     HIPTRY(h, hipMemcpy(cm->mbox, &hd, sizeof hd, hipMemcpyHostToDevice));
     cm->peer_member = h;
     return 0;
@@ -441,21 +449,13 @@ bool peer_fused_eligible(cwf_hip_system *h)
                 return false;
         h->px_send_k[k] = plane;
     }
-    // ranks on one device (a rehearsal): a rank's launch j waits, resident, for the others' launch j - 1, which needs
-    // at least one free slot: the other ranks' launches must leave one (a 2-rank C2 rehearsal: 436 of 512)
+    // ranks on one device (a rehearsal; the mailbox headers' PCI bus ids): a rank's launch j waits, resident, for the
+    // others' launch j - 1, so all the grids must fit together (two 436-workgroup C2 grids in 512 slots measured
+    // slower than the exchange step: profiles/r05k_peer_rehearsal.txt)
     bool same = false;
     for (int p = 0; p < cm->nranks; ++p)
-    {
-        if (p == cm->rank)
-            continue;
-        hipPointerAttribute_t at{};
-        if (hipPointerGetAttributes(&at, cm->peer_mbox[p]) != hipSuccess || at.device == cm->device)
-        {
-            (void)hipGetLastError();
-            same = true;
-        }
-    }
-    if (same && (uint64_t)h->fused_grid * (uint64_t)(cm->nranks - 1) >= pcg_lattice_resident_count(h->ds))
+        same = same || (p != cm->rank && cm->peer_same_device[p] != 0);
+    if (same && (uint64_t)h->fused_grid * (uint64_t)cm->nranks > pcg_lattice_resident_count(h->ds))
         return false;
     return true;
 }
@@ -572,6 +572,9 @@ int cwf_hip_comm_peer_connect(cwf_hip_comm *cm, const uint8_t *handles)
     cm->peer_mbox.assign(n, nullptr);
     cm->peer_nghost.assign(n, 0);
     cm->peer_recv_off.assign(n, 0);
+    cm->peer_same_device.assign(n, 1);
+    MboxHeader mine{};
+    HIPTRY(h, hipMemcpy(&mine, cm->mbox, sizeof mine, hipMemcpyDeviceToHost));
     for (int p = 0; p < n; ++p)
     {
         if (p == cm->rank)
@@ -590,6 +593,8 @@ int cwf_hip_comm_peer_connect(cwf_hip_comm *cm, const uint8_t *handles)
                              "peer=" + std::to_string(p));
         cm->peer_nghost[p] = hd.nghost;
         cm->peer_recv_off[p] = hd.recv_off[cm->rank];
+        hd.bus[sizeof hd.bus - 1] = 0;
+        cm->peer_same_device[p] = std::strncmp(hd.bus, mine.bus, sizeof hd.bus) == 0 ? 1 : 0;
     }
     // every neighbour expects exactly my send segment for it
     for (size_t k = 0; k < h->nbr.size(); ++k)
