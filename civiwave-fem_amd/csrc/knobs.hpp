@@ -44,6 +44,8 @@ inline constexpr Knob kKnobs[] = {
                   "persistently (default: fused only where one round of workgroups covers them)"},
     {"CWF_PEER_FUSED", "0: a PEER shard's fused iteration exchanges through a k_peer_step launch after each fused launch "
                        "instead of inside the launch (lattice_fused.inc fused_peer_wait / fused_peer_publish)"},
+    {"CWF_FUSED_TRACE", "path (ablation build only): per-workgroup phase stamps of one fused launch per solve, appended"},
+    {"CWF_FUSED_TRACE_IT", "n: the iteration whose launch CWF_FUSED_TRACE records (default 50)"},
     {"CWF_FUSED_MAXWG", "n: cap on the fused launch's grid (default 1024 workgroups; a grid below the work items walks them persistently)"},
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},

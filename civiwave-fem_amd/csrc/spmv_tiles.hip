@@ -2066,6 +2066,50 @@ bool fast_fused(const cwf_hip_system *h)
 
 namespace
 {
+#if CWF_ABLATION
+// diagnostic (ablation build): CWF_FUSED_TRACE=path appends the stamps of one launch (CWF_FUSED_TRACE_IT, default
+// 50) of every solve: one line per workgroup "wg kind|planes<<8 hw_id xcc_id t0 t1 t2 t3 t4" (s_memrealtime, 100 MHz)
+uint64_t *g_ftrace = nullptr;
+unsigned g_ftrace_n = 0;
+uint64_t *fused_trace_buffer(const cwf_hip_system *h)
+{
+    if (!knob("CWF_FUSED_TRACE"))
+        return nullptr;
+    if (g_ftrace_n < h->fused_grid)
+    {
+        if (g_ftrace)
+            (void)hipFree(g_ftrace);
+        g_ftrace = nullptr;
+        if (hipMalloc(reinterpret_cast<void **>(&g_ftrace), 64ull * h->fused_grid) != hipSuccess)
+            return nullptr;
+        g_ftrace_n = h->fused_grid;
+    }
+    return g_ftrace;
+}
+void fused_trace_dump(cwf_hip_system *h, unsigned it, hipStream_t st)
+{
+    const char *path = knob("CWF_FUSED_TRACE"), *at = knob("CWF_FUSED_TRACE_IT");
+    if (!path || !g_ftrace || it != (unsigned)(at ? atoi(at) : 50))
+        return;
+    std::vector<uint64_t> v(8ull * h->fused_grid);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(v.data(), g_ftrace, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    if (FILE *f = std::fopen(path, "a"))
+    {
+        std::fprintf(f, "# launch %u grid %u\n", it + 1u, h->fused_grid);
+        for (unsigned b = 0; b < h->fused_grid; ++b)
+        {
+            const uint64_t *w = &v[8ull * b];
+            std::fprintf(f, "%u %llu %llu %llu %llu %llu %llu %llu %llu\n", b, (unsigned long long)w[5],
+                         (unsigned long long)w[6], (unsigned long long)w[7], (unsigned long long)w[0],
+                         (unsigned long long)w[1], (unsigned long long)w[2], (unsigned long long)w[3],
+                         (unsigned long long)w[4]);
+        }
+        std::fclose(f);
+    }
+}
+#endif
 // launch j of the fused iteration: r_j -> {r2, r}[j & 1], Ap_j -> {Ap, ap2}[j & 1], p_j -> p[(j + 1) % 4], shares
 // -> fsh[j & 1]; launch j reads launch j - 1's (launch 0 reads r from r and Ap from ap2, zeroed at init)
 FusedArgs fused_args(cwf_hip_system *h, unsigned j)
@@ -2107,6 +2151,10 @@ FusedArgs fused_args(cwf_hip_system *h, unsigned j)
     fa.pin = fast_p_buf(h, j);
     fa.pout = fast_p_buf(h, j + 1u);
     fa.x = h->x;
+    fa.trace = nullptr;
+#if CWF_ABLATION
+    fa.trace = fused_trace_buffer(h);
+#endif
     return fa;
 }
 }  // namespace
@@ -2128,6 +2176,9 @@ void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
 void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
 {
     launch_pcg_lattice(h->ds, fused_args(h, it + 1u), st, e0, e1);
+#if CWF_ABLATION
+    fused_trace_dump(h, it, st);
+#endif
 }
 
 void fast_fused_launch0(cwf_hip_system *h, hipStream_t st)
