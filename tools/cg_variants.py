@@ -4,7 +4,7 @@ oracle's operator (CPU only; a design check, not a test of the device code).
 
   standard : the reference loop (pcg.cpp:840-901): alpha = rho / p.Ap; r -= alpha Ap; z = M^-1 r; rho' = r.z (a
              second global reduction); beta = rho' / rho; p = z + beta p.   Two reductions per iteration.
-  fused    : one reduction per iteration. Kernel i+1 forms r_{i+1}, z_{i+1}, p_{i+1} and Ap_{i+1} itself, so the
+  fused    : one reduction per iteration (the device's lattice_fused.inc; the convergence test on the direct |r|). Kernel i+1 forms r_{i+1}, z_{i+1}, p_{i+1} and Ap_{i+1} itself, so the
              dots it has at its start are those kernel i reduced: the direct rho_i = r_i.z_i and |r_i|^2 of the
              vectors kernel i formed, and p_i.Ap_i, z_i.Ap_i, Ap_i.M^-1 Ap_i, r_i.Ap_i, Ap_i.Ap_i. Then
                alpha_i = rho_i / p_i.Ap_i                                   (the reference's alpha, direct rho)
@@ -72,7 +72,9 @@ def standard(o, inv, rhs, mask, tol, maxit):
     return maxit, x
 
 
-def fused(o, inv, rhs, mask, tol, maxit):
+def fused(o, inv, rhs, mask, tol, maxit, direct=True):
+    """direct (the device kernel, lattice_fused.inc): the convergence test on the direct |r_j| of the formed r (launch
+    j + 1 tests launch j's r_j.r_j share); else on the recurrence |r_(j+1)|^2 ~ |r_j|^2 - 2 alpha r.Ap + alpha^2 Ap.Ap"""
     x = np.zeros_like(rhs)
     r = rhs.copy()
     r[mask] = 0.0
@@ -94,7 +96,7 @@ def fused(o, inv, rhs, mask, tol, maxit):
         x = (x + np.float32(alpha) * p).astype(np.float32)
         r = (r - np.float32(alpha) * Ap).astype(np.float32)
         r[mask] = 0.0
-        if np.sqrt(max(rr_n, 0.0)) <= tol * nb:
+        if np.sqrt(max(d64(r, r) if direct else rr_n, 0.0)) <= tol * nb:
             return it, x, np.sqrt(d64(r, r)) / nb
         z = prec(inv, r)
         z[mask] = 0.0
