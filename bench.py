@@ -349,15 +349,31 @@ def main():
                 err = e
             handles = [None] * world
             dist.all_gather_object(handles, None if err else comm.handle())
+            trial = None
             if err is None and all(hd is not None for hd in handles):
                 try:
                     comm.connect(handles)
                     shard.Comm.time_exchange(system, 8)  # a peer that never arrives fails here (bounded wait)
+                    # a short trial solve through the schedule the solves will run (on structured slabs the fused
+                    # iteration with its exchange inside the launches): every rank folds the same gathered totals,
+                    # so every rank must report the same finite residual, bit for bit
+                    res = pcg.solve_pcg(system, np.ones(3 * sh.local_nodes, np.float32), pcg.PcgSettings(12, 1e-30),
+                                        pcg.PcgVectors(np.zeros(3 * sh.local_nodes, np.float32), None))
+                    if not res.has_value():
+                        raise RuntimeError(f"trial solve: {res.error().message}")
+                    trial = (int(res.value().iterations), float(res.value().residual_norm),
+                             int(_lib.load().cwf_hip_system_exchange_schedule(system.handle())))
+                    if not np.isfinite(trial[1]):
+                        raise RuntimeError("trial solve: non-finite residual")
                 except Exception as e:  # noqa: BLE001
                     err = e
             ok = [None] * world
-            dist.all_gather_object(ok, err is None and all(hd is not None for hd in handles))
-            if not all(ok):
+            dist.all_gather_object(ok, (err is None and all(hd is not None for hd in handles), trial))
+            if rank == 0 and all(o[0] for o in ok):
+                print(f"# --comm auto: PEER trial solve on every rank: {ok[0][1]}", file=sys.stderr)
+            if not all(o[0] for o in ok) or len({o[1] for o in ok}) != 1:
+                if err is None:
+                    err = RuntimeError(f"trial solves differ across ranks: {[o[1] for o in ok]}")
                 if comm_kind == "peer":
                     raise SystemExit(f"rank {rank}: PEER communicator unavailable: {err}")
                 if rank == 0:
