@@ -14,6 +14,10 @@
 //           at system scope;
 //   unpack  its share of the received ghost rows and scalar slots into their vectors / slots (system-scope loads).
 //
+// The fused lattice iteration on PEER shards runs the same protocol inside its own launches instead (lattice_fused.inc
+// fused_peer_wait / fused_peer_publish; peer_fused_* below set up their arguments): the launch's Ap send rows and
+// rank totals are pushed by the launch, the flags raised by its last workgroup, and the next launch's prologue waits.
+//
 // Workgroups wait for peers, not for each other, and the grid is small (<= 64 workgroups of 1024 threads, resident
 // together), so every workgroup reaches its ticket. The ticket is a relaxed agent-scope add: what it orders are the
 // workgroups' write-through (system-scope) stores, each already acknowledged (every storing wave waits vmcnt(0)
