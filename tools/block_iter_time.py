@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Per-iteration time of a FAST solve on one structured block, one handle (the compute a slab shard of that size runs
+per PCG iteration, without its exchange): fixed iterations (tol 1e-30), the second solve timed (wall clock, host
+read-backs included), the fused iteration against the two-kernel loop (CWF_FUSED=0).
+
+usage: python tools/block_iter_time.py NX NY NZ [ITERATIONS]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "civiwave-fem_amd")]
+
+
+def main():
+    a = sys.argv[1:]
+    nx, ny, nz = (int(v) for v in a[:3])
+    its = int(a[3]) if len(a) > 3 else 300
+    import numpy as np
+
+    from cwf import _lib, pcg, scenarios
+
+    case = scenarios.block_case(nx, ny, nz, h=0.1, tol=1e-30, max_iterations=its)
+    rhs = case.static_rhs()
+    for fused in ("1", "0"):
+        os.environ["CWF_FUSED"] = fused
+        s = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, *case.scalars(), mode=_lib.MODE_FAST)
+        for _ in range(2):
+            x = np.zeros_like(rhs)
+            t0 = time.perf_counter()
+            t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(its, 1e-30), pcg.PcgVectors(x, None)).value()
+            el = time.perf_counter() - t0
+        kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
+        print(f"{nx}x{ny}x{nz} ({3 * nx * ny * nz / 1e6:.2f}M DOF) {'fused' if fused == '1' else 'two kernels'}: "
+              f"{t.iterations} iterations, {el / max(t.iterations, 1) * 1e6:.2f} us per iteration ({kern})", flush=True)
+        s.close()
+
+
+if __name__ == "__main__":
+    main()
