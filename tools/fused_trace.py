@@ -44,6 +44,15 @@ def main():
                       t[m, 4] - t[m, 0]], 1)
         print(f"  {lab:6s} " + "  ".join(f"{n} {np.median(d[:, i]):.2f}/{d[:, i].max():.2f}" for i, n in
                                            enumerate(names)) + "  (median/max us)")
+    if a.shape[1] >= 15:  # the first step's phases (stamps 8 .. 13): write k+1, write k+2, barrier, loads, row k, row k+1
+        st = a[:, 9:15].astype(np.float64) * 0.01
+        ph = np.diff(np.concatenate([t[:, 2:3] + 0 * st[:, :1] + (a[:, 6:7] * 0.01 - a[:, 6:7] * 0.01), st], 1), axis=1)
+        st0 = a[:, 6] * 0.01  # t2 (absolute, before the origin shift)
+        ph = np.diff(np.concatenate([st0[:, None], st], 1), axis=1)
+        m = ~shell
+        names2 = ["write k+1", "write k+2", "barrier", "issue loads", "row k", "row k+1"]
+        print("  first step (bricks): " + "  ".join(f"{n} {np.median(ph[m, i]):.2f}/{ph[m, i].max():.2f}"
+                                                   for i, n in enumerate(names2)) + "  (median/max us)")
     end = t[:, 4]
     order = np.argsort(end)[::-1][:8]
     print("  last to finish: " + ", ".join(f"wg {wg[i]} ({'shell' if shell[i] else 'brick'}, start {t[i, 0]:.2f},"
