@@ -2080,7 +2080,7 @@ uint64_t *fused_trace_buffer(const cwf_hip_system *h)
         if (g_ftrace)
             (void)hipFree(g_ftrace);
         g_ftrace = nullptr;
-        if (hipMalloc(reinterpret_cast<void **>(&g_ftrace), 64ull * h->fused_grid) != hipSuccess)
+        if (hipMalloc(reinterpret_cast<void **>(&g_ftrace), 128ull * h->fused_grid) != hipSuccess)
             return nullptr;
         g_ftrace_n = h->fused_grid;
     }
@@ -2091,7 +2091,7 @@ void fused_trace_dump(cwf_hip_system *h, unsigned it, hipStream_t st)
     const char *path = knob("CWF_FUSED_TRACE"), *at = knob("CWF_FUSED_TRACE_IT");
     if (!path || !g_ftrace || it != (unsigned)(at ? atoi(at) : 50))
         return;
-    std::vector<uint64_t> v(8ull * h->fused_grid);
+    std::vector<uint64_t> v(16ull * h->fused_grid);
     if (hipStreamSynchronize(st) != hipSuccess ||
         hipMemcpy(v.data(), g_ftrace, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         return;
@@ -2100,11 +2100,13 @@ void fused_trace_dump(cwf_hip_system *h, unsigned it, hipStream_t st)
         std::fprintf(f, "# launch %u grid %u\n", it + 1u, h->fused_grid);
         for (unsigned b = 0; b < h->fused_grid; ++b)
         {
-            const uint64_t *w = &v[8ull * b];
-            std::fprintf(f, "%u %llu %llu %llu %llu %llu %llu %llu %llu\n", b, (unsigned long long)w[5],
-                         (unsigned long long)w[6], (unsigned long long)w[7], (unsigned long long)w[0],
-                         (unsigned long long)w[1], (unsigned long long)w[2], (unsigned long long)w[3],
-                         (unsigned long long)w[4]);
+            const uint64_t *w = &v[16ull * b];
+            std::fprintf(f, "%u %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", b,
+                         (unsigned long long)w[5], (unsigned long long)w[6], (unsigned long long)w[7],
+                         (unsigned long long)w[0], (unsigned long long)w[1], (unsigned long long)w[2],
+                         (unsigned long long)w[3], (unsigned long long)w[4], (unsigned long long)w[8],
+                         (unsigned long long)w[9], (unsigned long long)w[10], (unsigned long long)w[11],
+                         (unsigned long long)w[12], (unsigned long long)w[13]);
         }
         std::fclose(f);
     }
