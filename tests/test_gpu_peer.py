@@ -75,23 +75,31 @@ def _assemble(out, n):
     return x.reshape(-1)
 
 
-@pytest.mark.parametrize("inkernel", [True, False], ids=["in_kernel_exchange", "exchange_step"])
+@pytest.mark.parametrize("inkernel", [True, False, "persistent"],
+                         ids=["in_kernel_exchange", "exchange_step", "in_kernel_persistent"])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_peer_lattice_slabs_equal_local(nranks, inkernel):
+def test_peer_lattice_slabs_equal_local(nranks, inkernel, monkeypatch):
     """in_kernel_exchange: the fused launches push their Ap send rows, rank totals and epoch flags themselves and
     wait for the peers' in their prologue (lattice_fused.inc fused_peer_wait / fused_peer_publish: no exchange
     launch); exchange_step (CWF_PEER_FUSED=0): one k_peer_step launch after each fused launch. Both equal the LOCAL
-    solve bit for bit, and a second solve on the same communicator repeats the first (the epochs carry over)."""
+    solve bit for bit, and a second solve on the same communicator repeats the first (the epochs carry over).
+    in_kernel_persistent: the same with an 8-workgroup grid walking the items (CWF_FUSED=2), in both the PEER
+    processes and the LOCAL reference (the last workgroup's rank-total fold over the grid's shares)."""
     shape = (13, 9, 4)
     spec = dict(slab=shape, tol=1e-6, max_iterations=800, timing_steps=1000)
     if not inkernel:
         spec["env"] = {"CWF_PEER_FUSED": "0"}
+    if inkernel == "persistent":
+        spec["env"] = {"CWF_FUSED": "2", "CWF_FUSED_MAXWG": "8"}
+        monkeypatch.setenv("CWF_FUSED", "2")
+        monkeypatch.setenv("CWF_FUSED_MAXWG", "8")
     out = _run(spec, nranks)
     glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
     x = _assemble(out, glob.packing.node_count)
     for d in out.values():
         # the fused lattice iteration with its ghost-plane stores (SHARD), on every rank (rank 0's affine planes too)
-        assert d["kernel"].startswith("k_pcg_lattice") and d["kernel"].endswith("true, false>"), d["kernel"]
+        assert d["kernel"].startswith("k_pcg_lattice") and d["kernel"].endswith(
+            "true, true>" if inkernel == "persistent" else "true, false>"), d["kernel"]
         assert d["schedule"] == (2 if inkernel else 1), d["schedule"]
         assert d["mailbox_kind"] == _lib.PEER_MAILBOX_UNCACHED, d["mailbox_kind"]
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
