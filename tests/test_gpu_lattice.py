@@ -12,6 +12,7 @@ local order: owned planes, then ghost planes) through the LOCAL communicator."""
 import numpy as np
 import pytest
 
+import oracle as O
 from cwf import _lib, meshgen, pack, pcg, scenarios, shard
 from cwf.stepper import Stepper
 from helpers import oracle_system
@@ -239,7 +240,7 @@ def test_fast_solve_run_to_run_deterministic(mesh, monkeypatch):
         assert np.array_equal(r.view(np.uint32), runs[0][2].view(np.uint32))
 
 
-@pytest.mark.parametrize("name", ["33x9x5", "rollers", "c1", "rayleigh", "33x9x5-persistent"])
+@pytest.mark.parametrize("name", ["33x9x5", "rollers", "c1", "rayleigh", "33x9x5-persistent", "hex", "hex-persistent"])
 def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
     """The fused one-launch iteration (lattice_fused.inc: r, z, p, x formed in the launch that applies K_eff; beta's
     numerator r_(j+1).z_(j+1) expanded through r_(j+1) = r_j - alpha Ap_j from the launch's own dots) against the
@@ -249,7 +250,13 @@ def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
     if name.endswith("-persistent"):  # a grid of 16 workgroups walking every work item (C3's shape at small scale;
         monkeypatch.setenv("CWF_FUSED_MAXWG", "16")  # forced: by default a grid below the items runs two kernels)
         name, on = name.split("-")[0], "2"
-    case = CASES[name]()
+    # hex: native hex8 cells (the deeper two-plane prefetch of the 27-point stencil), checked against the fp64 solve
+    # of the oracle operator. Its iteration counts are not compared: this static stiffness-dominated solve asks for a
+    # recurrence residual of 1e-6 |rhs| where the true residual of an fp32 x floors near 3e-3 |rhs|, and there finite
+    # precision CG's count follows each path's rounding (fused 216, two-kernel 310, hex tiles 168-175, fp64 163:
+    # profiles/r05zh_hex_counts.log, tools/hex_counts.py) while every x is within 3e-6 of the fp64 one
+    case = (scenarios.block_case(33, 9, 5, h=0.1, element="hex8", tol=1e-6, max_iterations=800) if name == "hex"
+            else CASES[name]())
     rhs = case.static_rhs()
     mi = case.cfg.solver.max_iterations
     out = {}
@@ -264,9 +271,15 @@ def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
         # the r output is the residual of x (rhs - K x, Dirichlet rows 0) to fp32 accuracy
         out[fused] = (t, x, r)
     (tf, xf, rf), (tk, xk, _) = out[on], out["0"]
-    ref = oracle_system(case.packing, case.materials, *case.scalars()).solve_pcg(rhs, mi, 1e-6)
+    if name == "hex":
+        P = case.packing
+        ref = {"x": O.hex8_solve64(case.mesh.coords, case.mesh.tets, P.material_index, O.make_stiffness(30.0e9, 0.2),
+                                   *case.scalars(), P.lumped_mass, P.bc_mask, rhs)}
+        assert np.linalg.norm(xk - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
+    else:
+        ref = oracle_system(case.packing, case.materials, *case.scalars()).solve_pcg(rhs, mi, 1e-6)
+        assert abs(tf.iterations - tk.iterations) <= max(3, tk.iterations // 20), (tf.iterations, tk.iterations)
     assert np.linalg.norm(xf - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
-    assert abs(tf.iterations - tk.iterations) <= max(3, tk.iterations // 20), (tf.iterations, tk.iterations)
     assert tf.residual_norm <= 1e-6 * np.linalg.norm(rhs.astype(np.float64)) * 1.0001
     assert abs(np.linalg.norm(rf.astype(np.float64)) - tf.residual_norm) <= 1e-3 * tf.residual_norm
 
