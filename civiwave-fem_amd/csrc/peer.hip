@@ -185,7 +185,11 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
             __hip_atomic_store(a.gdst[p] + (size_t)q * a.nranks * kSlot + j, q == 0 && a.fn ? gv[j] : a.gsrc[q][j],
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // every storing wave waits for its write-through stores, then one lane takes the workgroup's ticket
+    // every storing wave waits for its write-through stores, then one lane takes the workgroup's ticket: the
+    // hand-off of the MI355X guide's measured-forms table, row 1 (sc0 sc1 stores, each wave's vmcnt(0), a barrier,
+    // one agent-scope add per workgroup, the last adder told by the returned value); the last arriver then orders
+    // the whole launch's stores before its flag stores with a system-scope release, and the consumer side keeps
+    // its acquire. Relaxed on the ticket itself: the ordering it needs is the waits before it, not the atomic's
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
