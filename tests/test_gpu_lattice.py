@@ -284,21 +284,25 @@ def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
     assert abs(np.linalg.norm(rf.astype(np.float64)) - tf.residual_norm) <= 1e-3 * tf.residual_norm
 
 
+@pytest.mark.parametrize("element", ["tet4", "hex8"])
 @pytest.mark.parametrize("schedule", ["fused", "fused-persistent", "two-kernel"])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_sharded_schedules_equal_one_handle(nranks, schedule, monkeypatch):
+def test_sharded_schedules_equal_one_handle(nranks, schedule, element, monkeypatch):
     """The slab shards (LOCAL communicator) against the one-handle solve of the same block in the same schedule:
     fused (one launch and one exchange per iteration; the ghost planes' r_j / p_j formed locally from the received
     Ap_(j-1)), the fused form walking its items persistently (CWF_FUSED=2 with a 16-workgroup grid: the
     persistent and shard instantiations together), and the two-kernel loop. The shards' owned x follows the one
     handle's after 1, 2, 3 and 20 iterations (the round-5 divergence at iteration 2 was a shard whose affine planes
     skipped the ghost stores; only the scalar folds' order differs: per-workgroup shares against rank totals), and
-    the full solve converges in the same iteration count to within 3."""
+    the full solve converges in the same iteration count to within 3 (Kuhn tets; hex8 cells, the shard
+    instantiations of the 27-point stencil's two-deep prefetch, to within 10%: the note on fp32 CG counts below
+    the attainable residual in test_fused_iteration_matches_two_kernel_loop)."""
     monkeypatch.setenv("CWF_FUSED", {"fused": "1", "fused-persistent": "2", "two-kernel": "0"}[schedule])
     if schedule == "fused-persistent":
         monkeypatch.setenv("CWF_FUSED_MAXWG", "16")
     shape = (11, 7, 3)
-    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=1e-6, max_iterations=800)
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, element=element, tol=1e-6,
+                                max_iterations=800)
     P = glob.packing
     sK, sM = glob.scalars()
     rhs = glob.static_rhs()
@@ -306,7 +310,7 @@ def test_sharded_schedules_equal_one_handle(nranks, schedule, monkeypatch):
     comm = shard.Comm.local(nranks)
     systems, shards, rl = [], [], []
     for r in range(nranks):
-        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, tol=1e-6)
+        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, element=element, tol=1e-6)
         src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
         sh = shard.build_shard(src, begin, r, node_global)
         s = sh.system(glob.materials, sK, sM)
@@ -324,7 +328,8 @@ def test_sharded_schedules_equal_one_handle(nranks, schedule, monkeypatch):
         xg = np.zeros((P.node_count, 3), np.float32)
         for sh, xl in zip(shards, xs):
             xg[sh.node_global[: sh.owned_nodes].astype(np.int64)] = xl.reshape(-1, 3)[: sh.owned_nodes]
-        assert abs(ts.iterations - t1.iterations) <= (0 if tol < 1e-20 else 3), (its, ts.iterations, t1.iterations)
+        slack = 0 if tol < 1e-20 else 3 if element == "tet4" else max(3, t1.iterations // 10)
+        assert abs(ts.iterations - t1.iterations) <= slack, (its, ts.iterations, t1.iterations)
         d = np.linalg.norm(xg.reshape(-1).astype(np.float64) - x1) / np.linalg.norm(x1.astype(np.float64))
         assert d <= (1e-5 if tol < 1e-20 else 1e-4), (schedule, its, d)
     assert t1.converged and ts.converged
