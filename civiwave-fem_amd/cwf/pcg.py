@@ -159,7 +159,9 @@ class MatrixFreeSystem:
             self._h = h
         L = _lib.load()
         L.cwf_hip_system_set_scalars(self._h, self.stiffness_scale, self.mass_factor)
-        L.cwf_hip_system_set_mode(self._h, self.mode)
+        st = L.cwf_hip_system_set_mode(self._h, self.mode)
+        if st:  # a mode the handle cannot take (hex8 or a renumbered handle asked for PARITY): loud, not FAST
+            raise PcgException(self._err(), st)
         return self._h
 
     def close(self):

@@ -19,6 +19,7 @@ import tempfile
 import numpy as np
 import pytest
 
+import oracle as O
 from cwf import _lib, pcg, scenarios, shard
 from helpers import assert_bitwise, oracle_system
 
@@ -45,13 +46,14 @@ def _run(spec, nranks):
     return out
 
 
-def _local_slab(shape, nranks, tol, mi):
-    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=tol, max_iterations=mi)
+def _local_slab(shape, nranks, tol, mi, element="tet4"):
+    glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, element=element, tol=tol,
+                                max_iterations=mi)
     sK, sM = glob.scalars()
     comm = shard.Comm.local(nranks)
     systems, shards, rhs, xs = [], [], [], []
     for r in range(nranks):
-        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, tol=tol)
+        case, node_global, begin = scenarios.slab_case_shape(shape, nranks, r, element=element, tol=tol)
         src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
         sh = shard.build_shard(src, begin, r, node_global)
         s = sh.system(glob.materials, sK, sM)
@@ -75,18 +77,20 @@ def _assemble(out, n):
     return x.reshape(-1)
 
 
+@pytest.mark.parametrize("element", ["tet4", "hex8"])
 @pytest.mark.parametrize("inkernel", [True, False, "persistent"],
                          ids=["in_kernel_exchange", "exchange_step", "in_kernel_persistent"])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_peer_lattice_slabs_equal_local(nranks, inkernel, monkeypatch):
+def test_peer_lattice_slabs_equal_local(nranks, inkernel, element, monkeypatch):
     """in_kernel_exchange: the fused launches push their Ap send rows, rank totals and epoch flags themselves and
     wait for the peers' in their prologue (lattice_fused.inc fused_peer_wait / fused_peer_publish: no exchange
     launch); exchange_step (CWF_PEER_FUSED=0): one k_peer_step launch after each fused launch. Both equal the LOCAL
     solve bit for bit, and a second solve on the same communicator repeats the first (the epochs carry over).
     in_kernel_persistent: the same with an 8-workgroup grid walking the items (CWF_FUSED=2), in both the PEER
-    processes and the LOCAL reference (the last workgroup's rank-total fold over the grid's shares)."""
+    processes and the LOCAL reference (the last workgroup's rank-total fold over the grid's shares). hex8: the
+    27-point stencil's shard instantiations (two-deep prefetch with the mailbox's ghost Ap planes)."""
     shape = (13, 9, 4)
-    spec = dict(slab=shape, tol=1e-6, max_iterations=800, timing_steps=1000)
+    spec = dict(slab=shape, tol=1e-6, max_iterations=800, timing_steps=1000, element=element)
     if not inkernel:
         spec["env"] = {"CWF_PEER_FUSED": "0"}
     if inkernel == "persistent":
@@ -94,7 +98,7 @@ def test_peer_lattice_slabs_equal_local(nranks, inkernel, monkeypatch):
         monkeypatch.setenv("CWF_FUSED", "2")
         monkeypatch.setenv("CWF_FUSED_MAXWG", "8")
     out = _run(spec, nranks)
-    glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800)
+    glob, tl, xl = _local_slab(shape, nranks, 1e-6, 800, element)
     x = _assemble(out, glob.packing.node_count)
     for d in out.values():
         # the fused lattice iteration with its ghost-plane stores (SHARD), on every rank (rank 0's affine planes too)
@@ -107,10 +111,16 @@ def test_peer_lattice_slabs_equal_local(nranks, inkernel, monkeypatch):
         assert_bitwise(d["x2"], d["x"], "second solve x")
         # refused (the slabs are not whole reduction chunks, and PEER carries the FAST schedule only), never a hang
         assert d["parity_error"] and ("FAST schedule" in d["parity_error"] or "whole" in d["parity_error"]
-                                      or "reduction" in d["parity_error"]), d["parity_error"]
+                                      or "reduction" in d["parity_error"]
+                                      or "hex8 elements run in CWF_MODE_FAST only" in d["parity_error"]), d["parity_error"]
     assert_bitwise(x, xl, "PEER lattice slabs x vs LOCAL")
-    ref = oracle_system(glob.packing, glob.materials, *glob.scalars()).solve_pcg(glob.static_rhs(), 800, 1e-6)
     assert tl.converged
+    if element == "hex8":  # the fp64 solve of the hex8 oracle operator
+        P = glob.packing
+        ref = {"x": O.hex8_solve64(glob.mesh.coords, glob.mesh.tets, P.material_index, O.make_stiffness(30.0e9, 0.2),
+                                   *glob.scalars(), P.lumped_mass, P.bc_mask, glob.static_rhs())}
+    else:
+        ref = oracle_system(glob.packing, glob.materials, *glob.scalars()).solve_pcg(glob.static_rhs(), 800, 1e-6)
     assert np.linalg.norm(x - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
     print(f"PEER exchange step, {nranks} processes on one GPU: "
           + ", ".join(f"rank {k} {d['exchange_us']:.2f} us" for k, d in sorted(out.items())))

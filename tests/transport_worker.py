@@ -119,10 +119,11 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
 
         if spec.get("slab"):
             shape = tuple(spec["slab"])
-            glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, tol=spec["tol"],
+            element = spec.get("element", "tet4")
+            glob = scenarios.block_case(shape[0], shape[1], shape[2] * nranks, h=0.1, element=element, tol=spec["tol"],
                                         max_iterations=spec["max_iterations"])
             sK, sM = glob.scalars()
-            case, node_global, begin = scenarios.slab_case_shape(shape, nranks, rank, tol=spec["tol"])
+            case, node_global, begin = scenarios.slab_case_shape(shape, nranks, rank, element=element, tol=spec["tol"])
             src = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, sK, sM, mode=_lib.MODE_FAST)
             sh = shard.build_shard(src, begin, rank, node_global)
             rhs = sh.local_dofs(case.static_rhs())
@@ -188,8 +189,12 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         us = shard.Comm.time_exchange(s, spec.get("timing_steps", 200))
         # PARITY over PEER is refused (its chunk-partial all-gathers need RCCL / LOCAL)
         s.mode = _lib.MODE_PARITY  # (the handle takes the system's mode at every call)
-        pres = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, spec["tol"]), pcg.PcgVectors(np.zeros_like(x), None))
-        perr = None if pres.has_value() else pres.error().message
+        try:
+            pres = pcg.solve_pcg(s, rhs, pcg.PcgSettings(10, spec["tol"]), pcg.PcgVectors(np.zeros_like(x), None))
+            perr = None if pres.has_value() else pres.error().message
+        except pcg.PcgException as e:  # hex8: the handle refuses PARITY itself
+            perr = str(e)
+        s.mode = _lib.MODE_FAST
         own = 3 * sh.owned_nodes
         queue.put((rank, "ok", dict(telemetry=(t.iterations, t.converged, t.residual_norm), kernel=kern,
                                     nodes=sh.node_global[: sh.owned_nodes].astype(np.int64), x=x[:own].copy(),
