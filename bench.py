@@ -63,6 +63,8 @@ def parse():
                          "exchange completes on all of them, else RCCL")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the 'general' block (the same workload on the fan-group tiles, CWF_LATTICE=0)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the 'parity' block (the same workload in the bit-exact PARITY mode, c1/c2 only)")
     ap.add_argument("--no-hbm-roofline", action="store_true",
                     help="skip the live configs[2] K_eff roofline (N=1 runs of configs other than c3 add it)")
     ap.add_argument("--traffic", default="auto",
@@ -198,8 +200,8 @@ def hbm_roofline(L, device, key="c3", steps=2, sample=5, general=False):
 def operator_of(kname: str) -> str:
     """Which operator a K_eff kernel name is: the structured-block stencil (reached only by exact structured Kuhn /
     hex8 boxes of one material, lattice.cpp) or the general element tiles every other mesh runs."""
-    if kname.startswith("k_cg_lattice"):
-        return "structured-block stencil, single-launch (Chronopoulos-Gear) PCG iteration"
+    if kname.startswith("k_pcg_lattice"):
+        return "structured-block stencil, fused single-launch PCG iteration"
     if kname.startswith("k_keff_lattice"):
         return "structured-block stencil, two-kernel PCG iteration"
     if kname.startswith("k_keff_groups_pipe"):
@@ -209,10 +211,12 @@ def operator_of(kname: str) -> str:
     return "general mesh: element tiles (" + kname.split("<")[0] + ")"
 
 
-def general_line(L, device, key, steps, warmup=1, sample=5):
-    """The same workload with the structured-block stencil switched off (CWF_LATTICE=0): the fan-group tiles that
-    any gmsh mesh, C4 and every non-lattice scenario run, timed the same way as the headline (whole Newmark steps,
-    K_eff hipEvent-sampled), after the headline's timed region, so the two are never conflated."""
+def side_line(L, device, key, steps, warmup=1, sample=5, mode="general"):
+    """A comparator on the same workload, timed like the headline (whole Newmark steps, K_eff hipEvent-sampled) after
+    the headline's timed region, so the two are never conflated. mode="general": the structured-block stencil
+    switched off (CWF_LATTICE=0), i.e. the fan-group tiles that any gmsh mesh, C4 and every non-lattice scenario run.
+    mode="parity": the bit-exact PARITY path (the reference's fp64 element math and fold order, pcg.cpp:561-691),
+    the only mode whose residuals match the reference bit for bit."""
     import ctypes as C
 
     from cwf import _lib, scenarios
@@ -221,10 +225,11 @@ def general_line(L, device, key, steps, warmup=1, sample=5):
     case = scenarios.config_case(key)
     P = case.packing
     prev = os.environ.get("CWF_LATTICE")
-    os.environ["CWF_LATTICE"] = "0"
+    if mode == "general":
+        os.environ["CWF_LATTICE"] = "0"
     try:
-        st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time, mode=_lib.MODE_FAST,
-                     device=device)
+        st = Stepper(P, case.materials, case.rayleigh, case.cfg.solver, case.cfg.time,
+                     mode=_lib.MODE_PARITY if mode == "parity" else _lib.MODE_FAST, device=device)
         h = st.system.handle()
     finally:
         if prev is None:
@@ -250,7 +255,8 @@ def general_line(L, device, key, steps, warmup=1, sample=5):
     L.cwf_hip_system_timing(h, C.byref(ms), C.byref(n))
     L.cwf_hip_system_set_timing(h, 0)
     kname = (L.cwf_hip_system_keff_kernel(h) or b"").decode()
-    out = {"workload": case.name + " with CWF_LATTICE=0", "operator": operator_of(kname), "kernel": kname,
+    out = {"workload": case.name + (" with CWF_LATTICE=0" if mode == "general" else ", PARITY (bit-exact)"),
+           "operator": operator_of(kname), "kernel": kname,
            "steps": steps, "pcg_iterations": int(iters), "pcg_iterations_per_sec": iters / el,
            "dof_iterations_per_sec": P.dof_count * iters / el, "ms_per_step": 1e3 * el / steps,
            "keff_avg_launch_ms": ms.value / max(1, n.value)}
@@ -494,7 +500,11 @@ def main():
     general = None
     if (rank == 0 and world == 1 and not args.no_general and args.mode == "fast" and args.element == "tet4"
             and operator_of(kname).startswith("structured")):
-        general = general_line(L, device, args.config, min(args.steps, 5))
+        general = side_line(L, device, args.config, min(args.steps, 5))
+    parity = None
+    if (rank == 0 and world == 1 and not args.no_parity and args.mode == "fast" and args.element == "tet4"
+            and args.config in ("c1", "c2")):
+        parity = side_line(L, device, args.config, min(args.steps, 3), mode="parity")
     copy_gbs = stream_copy_gbs(L, device) if rank == 0 else None
     for rl in (hbm, hbm_general):
         if rl and copy_gbs:
@@ -515,9 +525,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if (strong and world > 1) or args.scaling == "strong" else "weak",
             "vs_baseline": None,
-            # FAST: fp32 element / stencil arithmetic with fp64 dot reductions (configs[4]'s mixed path); PARITY: the
+            # FAST: fp32 element / stencil arithmetic, the block-Jacobi inverse applied from a 16-B record of fp16 row
+            # scales and correlations (blockinv_pack.hpp), fp64 dot reductions (configs[4]'s mixed path); PARITY: the
             # reference's fp64 element math on fp32 data, bit-exact
-            "dtype": "f32 SpMV, f64 reductions" if args.mode == "fast" else "f64",
+            "dtype": "f32 SpMV, fp16-packed block-Jacobi, f64 reductions" if args.mode == "fast" else "f64",
             "data": ("synthetic (native hex8 block, gravity + tip load)" if args.element == "hex8" else
                      "synthetic (jittered + permuted hex block -> Kuhn tets, gravity + harmonic tip load "
                      "F0 sin(2 pi 5 t) from a 64-point curve, rewritten on the device every step)"
@@ -554,6 +565,8 @@ def main():
             "roofline_general": hbm_general,
             # the same workload on the general operator (fan-group tiles), timed after the headline's region
             "general": general,
+            # the bit-exact PARITY path on the same workload (the rate behind the 1e-10 residual target)
+            "parity": parity,
         }
         if args.mode == "parity" and keff_n.value:
             # PARITY's roofline is priced against the REFERENCE layout's compulsory bytes (72 B per tet + 32 B per

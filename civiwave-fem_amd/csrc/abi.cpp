@@ -229,6 +229,9 @@ int check_ready(cwf_hip_system *h)
 {
     if (!h)
         return set_error(nullptr, CWF_ERR_ARGUMENT, "null handle");
+    if (h->unusable)
+        return set_error(h, CWF_ERR_ARGUMENT, "handle unusable after a failed attach",
+                         "its operator plan was cut to a shard's owned rows; destroy it");
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess)
         return hip_fail(h, e, "hipSetDevice");
@@ -1363,6 +1366,12 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
+        if (s.t.lat && fast_fused(h) && !h->sharded() && resident_ready(const_cast<cwf_hip_system *>(h)))
+        {  // the resident solve (resident.hip), per iteration: only what crosses a CU -- the halo records read, the
+           // box-surface records and the shares written, the G x 5 shares read -- the vectors stay on chip
+            *layout_bytes = resident_offchip_bytes(h);
+            return 0;
+        }
         if (s.t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration (lattice_fused.inc): per owned node r_(j-1), Ap_(j-1),
         {                              // p_(j-1), the class byte and x read, r_j, p_j, Ap_j and x written; the mass
                                        // of the shell's nodes (the strict interior's is one value when lmu)
@@ -1424,6 +1433,13 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
         if (compact)
             return h->ds.iso ? "k_keff_parity_tile<true, false, false, true>" : "k_keff_parity_tile<false, false, false, true>";
         return h->ds.iso ? "k_keff_parity_tile<true, false, true, false>" : "k_keff_parity_tile<false, false, true, false>";
+    }
+    if (t.lat && fast_fused(h) && !h->sharded() && resident_ready(const_cast<cwf_hip_system *>(h)))
+    {  // the resident solve's one launch per solve (resident.hip)
+        static thread_local char name[96];
+        snprintf(name, sizeof name, "k_pcg_resident<%s, %s, 3, 2>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn");
+        return name;
     }
     if (t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration's one launch (lattice_fused.inc)
     {

@@ -23,6 +23,11 @@ std::string pcg_error_message(int code, int iter, std::string *ctx)
         *ctx = "step=" + std::to_string(iter);
         return "peer exchange timed out";
     }
+    if (code == CWF_ERR_HIP)  // resident.hip: a workgroup did not reach a phase within its bounded wait
+    {
+        *ctx = "phase=" + std::to_string(iter);
+        return "resident solve: a workgroup missed the phase barrier";
+    }
     if (code == CWF_ERR_RHO_ZERO && iter < 0)
     {
         *ctx = "rho~0";
@@ -30,6 +35,77 @@ std::string pcg_error_message(int code, int iter, std::string *ctx)
     }
     *ctx = "iteration=" + std::to_string(iter);
     return "CG rho approached zero";  // pcg.cpp:889-892
+}
+
+// the solve's telemetry and error from the control block read back last (every member's is identical)
+int pcg_finish(const std::vector<cwf_hip_system *> &g, cwf_pcg_telemetry *tel)
+{
+    cwf_hip_system *h = g[0];
+    const Ctl &c = *h->ctl_host;
+    for (cwf_hip_system *m : g)
+    {
+        m->hist_count = c.iterations + 1;
+        m->prev_iters = m->last_iters;
+        m->last_iters = c.iterations;
+    }
+    if (tel)
+    {
+        tel->iterations = c.iterations;
+        tel->residual_norm = c.res;
+        tel->rhs_norm = c.rhs_norm_raw;
+        tel->alpha_last = c.alpha_last;
+        tel->beta_last = c.beta_last;
+        tel->converged = c.converged;
+        tel->reserved = 0;
+    }
+    if (c.error)
+    {
+        std::string ctx;
+        std::string msg = pcg_error_message(c.error, c.error_iter, &ctx);
+        for (size_t i = 1; i < g.size(); ++i)
+            set_error(g[i], c.error, msg, ctx);
+        return set_error(h, c.error, msg, ctx);
+    }
+    return 0;
+}
+
+// the resident solve: fast_fused_init (block inverse, r_0, norms, tolerance), then ONE launch that runs every
+// iteration on chip (resident.hip) and leaves x, r and the control block; hipEvent-timed as a whole when timing is on
+// (the handle's K_eff timing then counts its iterations: avg = the time per iteration)
+int run_pcg_resident(cwf_hip_system *h, const float *rhs, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
+{
+    hipStream_t st = h->stream;
+    fast_fused_init(h, rhs, set.relative_tolerance, st, false);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->timing)
+    {
+        if (h->ev.size() < 2)
+        {
+            const size_t had = h->ev.size();
+            h->ev.resize(2);
+            for (size_t i = had; i < 2; ++i)
+                HIPTRY(h, hipEventCreateWithFlags(&h->ev[i], hipEventDisableSystemFence));
+        }
+        e0 = h->ev[0];
+        e1 = h->ev[1];
+    }
+    const uint32_t max_it = (uint32_t)std::min<uint64_t>(set.max_iterations, 1u << 24);
+    launch_pcg_resident(h, max_it, st, e0, e1);
+    // the next solve's tags start past every tag this one can publish (phases 0 .. max_it + 1)
+    h->res.tag += max_it + 3u;
+    HIPTRY(h, hipGetLastError());
+    HIPTRY(h, hipMemcpyAsync(h->ctl_host, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
+    HIPTRY(h, hipStreamSynchronize(st));
+    if (e0 && h->ctl_host->iterations)
+    {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+        {
+            h->keff_ms += ms;
+            h->keff_count += h->ctl_host->iterations;
+        }
+    }
+    return pcg_finish({h}, tel);
 }
 
 // run solve_pcg on device buffers: rhs[i] and g[i]->x (holding the warm start) for every member of a
@@ -65,7 +141,13 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
             HIPTRY(m, hipMemsetAsync(m->x, 0, m->ds.D * sizeof(float), m->stream));
     const bool fast = h->mode == CWF_MODE_FAST;
     // one launch per iteration (lattice_fused.inc); shards: one exchange per iteration, agreed by every rank
-    const bool fused = fast && (sharded ? group_fused(g) : fast_fused(h));
+    int gf = 0;
+    if (fast && sharded && (gf = group_fused(g)) < 0)
+        return gf;
+    const bool fused = fast && (sharded ? gf == 1 : fast_fused(h));
+    // a block that fits on chip: the whole solve in one launch (resident.hip)
+    if (fused && !sharded && set.max_iterations <= (1u << 24) && resident_ready(h))
+        return run_pcg_resident(h, rhs[0], set, tel);
     if (fused && sharded)
     {
         if (int e = sharded_fused_init(g, rhs, set.relative_tolerance))
@@ -191,32 +273,7 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
         for (cwf_hip_system *m : g)
             HIPTRY(m, hipStreamSynchronize(m->stream));
     }
-    const Ctl &c = *h->ctl_host;
-    for (cwf_hip_system *m : g)
-    {
-        m->hist_count = c.iterations + 1;
-        m->prev_iters = m->last_iters;
-        m->last_iters = c.iterations;
-    }
-    if (tel)
-    {
-        tel->iterations = c.iterations;
-        tel->residual_norm = c.res;
-        tel->rhs_norm = c.rhs_norm_raw;
-        tel->alpha_last = c.alpha_last;
-        tel->beta_last = c.beta_last;
-        tel->converged = c.converged;
-        tel->reserved = 0;
-    }
-    if (c.error)
-    {
-        std::string ctx;
-        std::string msg = pcg_error_message(c.error, c.error_iter, &ctx);
-        for (size_t i = 1; i < g.size(); ++i)
-            set_error(g[i], c.error, msg, ctx);
-        return set_error(h, c.error, msg, ctx);
-    }
-    return 0;
+    return pcg_finish(g, tel);
 }
 
 int run_pcg(cwf_hip_system *h, const float *rhs_dev, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)

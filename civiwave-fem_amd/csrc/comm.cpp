@@ -300,8 +300,8 @@ int fast_pcg_iteration_group(const std::vector<cwf_hip_system *> &g, const std::
 // totals in rank order, so every rank takes the same decisions.
 
 // every member (and, through one all-gather, every rank) can run it: the decision is collective, taken at a handle's
-// first sharded solve and kept (the shards' lattice plans do not change)
-bool group_fused(const std::vector<cwf_hip_system *> &g)
+// first sharded solve and kept (the shards' lattice plans do not change). 1 fused, 0 not, < 0 an error status
+int group_fused(const std::vector<cwf_hip_system *> &g)
 {
     cwf_hip_system *h0 = g[0];
     if (h0->fused_agreed >= 0)
@@ -314,32 +314,28 @@ bool group_fused(const std::vector<cwf_hip_system *> &g)
     for (cwf_hip_system *h : g)
     {
         const double v[2] = {mine ? 1.0 : 0.0, px ? 1.0 : 0.0};
-        if (hipMemcpyAsync(h->g_init + 2 * h->rank, v, sizeof v, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
-            hipStreamSynchronize(h->stream) != hipSuccess)
-            mine = false;
+        HIPTRY(h, hipMemcpyAsync(h->g_init + 2 * h->rank, v, sizeof v, hipMemcpyHostToDevice, h->stream));
+        HIPTRY(h, hipStreamSynchronize(h->stream));
     }
-    bool all = mine, all_px = px;
-    if (comm_allgather(g, &cwf_hip_system::g_init, 2) == 0)
+    // a rank that cannot learn the others' votes must not pick a schedule alone (its peers could agree on
+    // the fused one and then wait for exchange steps it never runs): the solve fails instead, decided by nobody
+    if (int st = comm_allgather(g, &cwf_hip_system::g_init, 2))
+        return st < 0 ? st : set_error(h0, CWF_ERR_COMM, "schedule agreement all-gather failed");
+    std::vector<double> f(2 * (size_t)h0->nranks, 0.0);
+    HIPTRY(h0, hipStreamSynchronize(h0->stream));
+    HIPTRY(h0, hipMemcpy(f.data(), h0->g_init, f.size() * sizeof(double), hipMemcpyDeviceToHost));
+    bool all = true, all_px = true;
+    for (int r = 0; r < h0->nranks; ++r)
     {
-        std::vector<double> f(2 * (size_t)h0->nranks, 0.0);
-        if (hipStreamSynchronize(h0->stream) == hipSuccess &&
-            hipMemcpy(f.data(), h0->g_init, f.size() * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess)
-            for (int r = 0; r < h0->nranks; ++r)
-            {
-                all = all && f[2 * (size_t)r] == 1.0;
-                all_px = all_px && f[2 * (size_t)r + 1] == 1.0;
-            }
-        else
-            all = false;
+        all = all && f[2 * (size_t)r] == 1.0;
+        all_px = all_px && f[2 * (size_t)r + 1] == 1.0;
     }
-    else
-        all = false;
     for (cwf_hip_system *h : g)
     {
         h->fused_agreed = all ? 1 : 0;
         h->px_agreed = all && all_px ? 1 : 0;
     }
-    return all;
+    return all ? 1 : 0;
 }
 
 namespace
@@ -759,6 +755,12 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         h->send_off.assign(1, 0);
         h->recv_off.assign(1, 0);
     }
+    // from here on the handle's operator plan is the shard's: a failure leaves it unusable (not silently computing only
+    // the owned rows of a partial plan as if it were unattached)
+    const auto broken = [h](int st) {
+        h->unusable = true;
+        return st;
+    };
     h->ds.Nown = (uint32_t)plan->owned_nodes;
     if (h->ds.t.lat)  // structured block: compute the rows of the planes holding owned nodes only
     {
@@ -783,12 +785,13 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
         {
             void *p = nullptr;
             if (int st = alloc(&p, 2ull * 5 * std::max<uint32_t>(t.lnwork, 1u) * sizeof(double)))
-                return st;
+                return broken(st);
             h->fsh = static_cast<double *>(p);
             if (int st = alloc(&p, (size_t)kFusedSlotHost * n * sizeof(double)))
-                return st;
+                return broken(st);
             h->g_fsh = static_cast<double *>(p);
-            HIPTRY(h, hipMemset(h->g_fsh, 0, (size_t)kFusedSlotHost * n * sizeof(double)));
+            if (hipError_t e = hipMemset(h->g_fsh, 0, (size_t)kFusedSlotHost * n * sizeof(double)); e != hipSuccess)
+                return broken(hip_fail(h, e, "hipMemset"));
         }
     }
     h->gbegin = plan->owned_nodes && plan->node_global ? plan->node_global[0] : 0;
@@ -812,7 +815,7 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
             h->comm = nullptr;  // not attached: cwf_hip_system_destroy must not reach the communicator
             h->rank = 0;
             h->nranks = 1;
-            return st;
+            return broken(st);
         }
     if (cm->kind == 0)
     {

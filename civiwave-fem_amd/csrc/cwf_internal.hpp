@@ -285,6 +285,24 @@ struct Ctl
     double alpha_h[kXLag];  // FAST: alpha of iteration j at [j % kXLag] (the lazy x update, spmv_tiles.hip)
 };
 
+// the resident solve of a structured block (resident.hip, resident.cpp): one persistent launch per PCG solve, one
+// workgroup per box of the lattice, the vectors on chip. state: 0 not planned yet, 1 planned, -1 not eligible
+struct ResidentPlan
+{
+    int state = 0;
+    unsigned G = 0, npt = 0, nph = 0;  // workgroups; own / halo entries per thread (the instantiation)
+    unsigned own_stride = 0, halo_stride = 0, npub = 0;
+    size_t lds = 0;                     // dynamic LDS: the largest box image
+    unsigned dims[3] = {0, 0, 0};       // boxes along x, y, z
+    unsigned max_own = 0, max_halo = 0;
+    uint64_t halo_total = 0;            // halo entries over every box (records read per phase)
+    const uint4 *hdr = nullptr, *own = nullptr, *halo = nullptr;
+    const float4 *tcoef = nullptr;  // [27][nOff][3] the boundary types' stencils
+    float *pub = nullptr;
+    double *sh = nullptr;
+    uint32_t tag = 1;  // the next solve's granule tag base (resident.hip: phase j publishes tag + j + 1)
+};
+
 struct DevBuf
 {
     void *p = nullptr;
@@ -314,12 +332,16 @@ struct cwf_hip_system
     double *fsh = nullptr;
     double *g_fsh = nullptr;  // a shard's all-gathered rank totals of the fused shares, [nranks][8] (one rank: [8])
     bool cls_global = false;  // a shard's ghost class bytes hold their owners' (global) classes
+    // a failed attach after the handle's plan was rewritten for its owned rows (comm.cpp cwf_hip_comm_attach): every
+    // later call but destroy refuses the handle instead of computing a partial plan's rows
+    bool unusable = false;
     int fused_agreed = -1;    // a shard: every rank runs the fused iteration (1) or none (0); -1: not asked yet
     int px_agreed = 0;        // ... and exchanges inside its launches (PEER, every rank eligible)
     int32_t px_send_k[2] = {-1, -1};  // the lattice plane of each neighbour slot's send segment
     uint32_t px_ebase = 0;            // the communicator's epoch before the solve's launch 0
     unsigned fused_grid = 0, fused_items = 0;  // the fused launch's grid and the work items it was sized for
     bool fused_on = false;                     // CWF_FUSED as it was when the handle first asked
+    cwf::ResidentPlan res;                     // the resident solve (resident.cpp), planned at the first FAST solve
     float *inv = nullptr;   // block Jacobi [9N]; FAST: the symmetrised operator the solve applies
     float *inv6 = nullptr;  // FAST: the same block packed to 16 B per node (blockinv_pack.hpp)
     // inv / inv6 hold the FAST operator for (inv_sK, inv_sM): the block inverse depends only on the handle's
@@ -450,7 +472,7 @@ void fast_flush_x(cwf_hip_system *h, const float *rhs, hipStream_t st);  // the 
 void fast_tiles_pcg_dry(cwf_hip_system *h, unsigned abl, int reps, hipStream_t st);
 // the fused lattice iteration (lattice_fused.inc): one launch per PCG iteration on an unsharded structured block
 bool fast_fused(const cwf_hip_system *h);
-void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st);
+void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st, bool launch0 = true);
 void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
 void fast_fused_check(cwf_hip_system *h, unsigned it, hipStream_t st);
@@ -465,7 +487,13 @@ constexpr size_t kFusedSlotHost = 8;  // doubles per rank of the gathered fused 
 // comm.cpp: the sharded fused iteration (one launch + one exchange: the rank totals and the Ap halo)
 int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
 int sharded_fused_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1);
-bool group_fused(const std::vector<cwf_hip_system *> &g);
+int group_fused(const std::vector<cwf_hip_system *> &g);  // 1 fused, 0 two-kernel, < 0 error
+// the resident solve (resident.cpp / resident.hip): whether this handle runs it (plans it at the first call; CWF_RESIDENT
+// = 0 turns it off), the launch (fast_fused_init has run; one launch runs every iteration) and its residency query
+bool resident_ready(cwf_hip_system *h);
+void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
+int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds);
+uint64_t resident_offchip_bytes(const cwf_hip_system *h);  // per phase: halo records read, surface records and shares
 int sharded_fused_end(const std::vector<cwf_hip_system *> &g);  // after the last launch (PEER in-kernel epochs)
 
 unsigned fast_tile_blocks(const DevSys &s);

@@ -38,13 +38,17 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     {"CWF_PARITY_TILES", "strip: PARITY node tiles of 256 consecutive nodes also on a single handle (default there: "
                          "compact breadth-first tiles and a separate p.Ap partials pass; shards always use strips)"},
-    // PCG schedule (spmv_tiles.hip)
+    // PCG schedule (spmv_tiles.hip, resident.hip)
+    {"CWF_RESIDENT", "0: a structured block that fits on chip runs the launch-per-iteration schedules instead of the "
+                     "resident one-launch solve (resident.hip; also off whenever CWF_FUSED is set)"},
     {"CWF_FUSED", "0: structured blocks run the two-kernel iteration (k_keff_lattice + k_pcg_update_tiles) instead of "
                   "the fused one-launch iteration (lattice_fused.inc); 2: fused also where the grid walks the work items "
                   "persistently (default: fused only where one round of workgroups covers them)"},
     {"CWF_PEER_FUSED", "0: a PEER shard's fused iteration exchanges through a k_peer_step launch after each fused launch "
                        "instead of inside the launch (lattice_fused.inc fused_peer_wait / fused_peer_publish)"},
     {"CWF_FUSED_TRACE", "path (ablation build only): per-workgroup phase stamps of one fused launch per solve, appended"},
+    {"CWF_RESIDENT_TRACE", "path: per-workgroup phase stamps of one phase (CWF_FUSED_TRACE_IT) of every resident solve, "
+                           "appended (tools/resident_trace.py)"},
     {"CWF_FUSED_TRACE_IT", "n: the iteration whose launch CWF_FUSED_TRACE records (default 50)"},
     {"CWF_FUSED_MAXWG", "n: cap on the fused launch's grid (default 1024 workgroups; a grid below the work items walks them persistently)"},
     {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},

@@ -1,0 +1,267 @@
+// resident.cpp -- the plan of the resident solve (resident.hip): the structured block cut into one box per workgroup
+// (at most one per CU, so the persistent grid is co-resident), each box's node list (the thread -> node map its
+// registers keep for the whole solve), its halo list (the one-node ring its rows read, each entry pointing at the
+// owner's published record) and the publication index of every node some other box reads.
+//
+// Box choice: every factorisation gx * gy * gz <= CUs of the node lattice, boxes of ceil(n / g) nodes per axis at most,
+// scored by the per-workgroup work of a phase (own nodes + 1.5 x halo entries, each halo entry being three 16-B
+// loads and a formed p) plus a barrier term growing with the grid (2 per workgroup); the image (box + ring, float4)
+// must fit the LDS beside the static tables and the lists the kernel's 3 + 2 entries per thread. C2 (70^3 nodes): 5 x 7 x 7 boxes of
+// 14 x 10 x 10 nodes, 245 workgroups.
+#include <algorithm>
+#include <cstring>
+
+#include "abi_internal.hpp"
+
+namespace cwf
+{
+namespace
+{
+constexpr unsigned kResThreads = 512, kResOwn = 3 * kResThreads, kResHalo = 2 * kResThreads;  // resident.hip
+// the box image's float4 slots within 64 KB of LDS beside the kernel's static arrays (the class table, the boundary
+// types' stencils: 25 KB with the 15-offset Kuhn stencil, 40.5 KB with the 27-offset hex8 one)
+constexpr unsigned kResMaxSlotsKuhn = 2450, kResMaxSlotsHex = 1450;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr unsigned kFusedSharesHost = 5;  // kFusedShares (lattice_common.hpp): one 16-B granule each
+
+void split(unsigned n, unsigned g, unsigned q, unsigned &a, unsigned &b)
+{
+    a = (unsigned)((uint64_t)n * q / g);
+    b = (unsigned)((uint64_t)n * (q + 1) / g);
+}
+}  // namespace
+
+bool resident_ready(cwf_hip_system *h)
+{
+    ResidentPlan &rp = h->res;
+    if (rp.state)
+        return rp.state > 0;
+    rp.state = -1;
+    // the default for a FAST structured block that fits; CWF_RESIDENT=0, or an explicit CWF_FUSED schedule (0: two
+    // kernels, 1: the per-launch fused iteration, 2: its persistent walk), keeps the launch-per-iteration schedules
+    const char *kn = knob("CWF_RESIDENT");
+    if ((kn && kn[0] == '0') || knob("CWF_FUSED"))
+        return false;
+    const DevTiles &t = h->ds.t;
+    const uint32_t N = h->ds.N;
+    if (h->mode != CWF_MODE_FAST || !t.lat || !t.lcls || !t.lcz || h->sharded() || h->ds.Nown != N ||
+        h->lat_plane.size() != t.lnz || t.lk0 != 0 || t.lk1 != t.lnz)
+        return false;
+    const unsigned nx = t.lnx, ny = t.lny, nz = t.lnz;
+    if (nx < 2 || ny < 2 || nz < 2)
+        return false;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return false;
+    if ((uint64_t)N > (uint64_t)cus * kResOwn)
+        return false;  // more nodes than the grid's registers hold
+    // the box grid
+    const unsigned G0 = (unsigned)cus;
+    const unsigned kResMaxSlots = t.lhex ? kResMaxSlotsHex : kResMaxSlotsKuhn;
+    double best = 1e300;
+    unsigned bg[3] = {0, 0, 0};
+    for (unsigned gx = 1; gx <= std::min(nx, G0); ++gx)
+        for (unsigned gy = 1; gy <= std::min(ny, G0 / gx); ++gy)
+            for (unsigned gz = 1; gz <= std::min(nz, G0 / (gx * gy)); ++gz)
+            {
+                const uint64_t sx = (nx + gx - 1) / gx, sy = (ny + gy - 1) / gy, sz = (nz + gz - 1) / gz;
+                const uint64_t own = sx * sy * sz, slots = (sx + 2) * (sy + 2) * (sz + 2), halo = slots - own;
+                if (own > kResOwn || halo > kResHalo || slots > kResMaxSlots)
+                    continue;
+                const double cost = (double)own + 1.5 * (double)halo + 2.0 * (double)(gx * gy * gz);
+                if (cost < best)
+                {
+                    best = cost;
+                    bg[0] = gx, bg[1] = gy, bg[2] = gz;
+                }
+            }
+    if (!bg[0])
+        return false;
+    const unsigned G = bg[0] * bg[1] * bg[2];
+    const int(*off)[3] = t.lhex ? kLatHexOff : kLatOff;
+    const int noff = t.lhex ? kLatHexOffsets : kLatOffsets;
+    const std::vector<uint32_t> &plane = h->lat_plane;
+    const auto node = [&](unsigned i, unsigned j, unsigned k) { return plane[k] + j * nx + i; };
+    // owner box of every node, and which nodes another box reads
+    std::vector<uint32_t> owner(N, kNone);
+    std::vector<unsigned> B(6 * (size_t)G);
+    for (unsigned b = 0; b < G; ++b)
+    {
+        const unsigned bx = b % bg[0], by = (b / bg[0]) % bg[1], bz = b / (bg[0] * bg[1]);
+        unsigned *q = &B[6 * (size_t)b];
+        split(nx, bg[0], bx, q[0], q[1]);
+        split(ny, bg[1], by, q[2], q[3]);
+        split(nz, bg[2], bz, q[4], q[5]);
+        for (unsigned k = q[4]; k < q[5]; ++k)
+            for (unsigned j = q[2]; j < q[3]; ++j)
+                for (unsigned i = q[0]; i < q[1]; ++i)
+                    owner[node(i, j, k)] = b;
+    }
+    std::vector<uint8_t> needed(N, 0);
+    for (unsigned k = 0; k < nz; ++k)
+        for (unsigned j = 0; j < ny; ++j)
+            for (unsigned i = 0; i < nx; ++i)
+            {
+                const uint32_t n = node(i, j, k);
+                for (int o = 1; o < noff; ++o)
+                {
+                    const long ii = (long)i + off[o][0], jj = (long)j + off[o][1], kk = (long)k + off[o][2];
+                    if (ii < 0 || jj < 0 || kk < 0 || ii >= (long)nx || jj >= (long)ny || kk >= (long)nz)
+                        continue;
+                    const uint32_t m = node((unsigned)ii, (unsigned)jj, (unsigned)kk);
+                    if (owner[m] != owner[n])
+                        needed[m] = 1;
+                }
+            }
+    // own lists (block-interior nodes first: the brick rows; then the surface's cell-form rows), publication indices
+    // in that order box after box, then the halo lists (sorted by publication index: consecutive lanes, consecutive
+    // records)
+    std::vector<uint32_t> pubidx(N, kNone);
+    std::vector<std::vector<uint4>> ownl(G), halol(G);
+    std::vector<uint4> hdr(G);
+    uint32_t npub = 0;
+    unsigned max_own = 0, max_halo = 0;
+    size_t max_slots = 0;
+    for (unsigned b = 0; b < G; ++b)
+    {
+        const unsigned *q = &B[6 * (size_t)b];
+        const unsigned PX = q[1] - q[0] + 2, PXY = PX * (q[3] - q[2] + 2), slots = PXY * (q[5] - q[4] + 2);
+        hdr[b] = uint4{slots, 0u, PX, PXY};
+        max_slots = std::max<size_t>(max_slots, slots);
+        for (int pass = 0; pass < 2; ++pass)
+            for (unsigned k = q[4]; k < q[5]; ++k)
+                for (unsigned j = q[2]; j < q[3]; ++j)
+                    for (unsigned i = q[0]; i < q[1]; ++i)
+                    {
+                        const bool shell = i == 0 || j == 0 || k == 0 || i + 1 == nx || j + 1 == ny || k + 1 == nz;
+                        if (shell != (pass == 1))
+                            continue;
+                        const uint32_t n = node(i, j, k);
+                        const unsigned slot = (k - q[4] + 1) * PXY + (j - q[2] + 1) * PX + (i - q[0] + 1);
+                        if (needed[n])
+                            pubidx[n] = npub++;
+                        ownl[b].push_back(uint4{n, slot, pubidx[n], 0u});
+                    }
+        max_own = std::max<unsigned>(max_own, (unsigned)ownl[b].size());
+    }
+    uint64_t halo_total = 0;
+    std::vector<uint32_t> seen(N, kNone);
+    for (unsigned b = 0; b < G; ++b)
+    {
+        const unsigned *q = &B[6 * (size_t)b];
+        const unsigned PX = hdr[b].z, PXY = hdr[b].w;
+        for (unsigned k = q[4]; k < q[5]; ++k)
+            for (unsigned j = q[2]; j < q[3]; ++j)
+                for (unsigned i = q[0]; i < q[1]; ++i)
+                    for (int o = 1; o < noff; ++o)
+                    {
+                        const long ii = (long)i + off[o][0], jj = (long)j + off[o][1], kk = (long)k + off[o][2];
+                        if (ii < 0 || jj < 0 || kk < 0 || ii >= (long)nx || jj >= (long)ny || kk >= (long)nz)
+                            continue;
+                        const uint32_t m = node((unsigned)ii, (unsigned)jj, (unsigned)kk);
+                        if (owner[m] == b || seen[m] == b)
+                            continue;
+                        seen[m] = b;
+                        const unsigned slot = (unsigned)((kk - (long)q[4] + 1) * PXY + (jj - (long)q[2] + 1) * PX +
+                                                         (ii - (long)q[0] + 1));
+                        halol[b].push_back(uint4{m, slot, pubidx[m], 0u});
+                    }
+        std::sort(halol[b].begin(), halol[b].end(), [](const uint4 &a, const uint4 &c) { return a.z < c.z; });
+        max_halo = std::max<unsigned>(max_halo, (unsigned)halol[b].size());
+        halo_total += halol[b].size();
+    }
+    const unsigned npt = (max_own + kResThreads - 1) / kResThreads, nph = (max_halo + kResThreads - 1) / kResThreads;
+    if (max_own > kResOwn || max_halo > kResHalo || max_slots > kResMaxSlots)
+        return false;
+    const unsigned own_stride = kResOwn, halo_stride = kResHalo;
+    const size_t lds = max_slots * 16;
+    // one workgroup per CU at least (the grid waits for all of them every phase)
+    if (resident_blocks_per_cu(h->ds, npt, nph, lds) < 1)
+        return false;
+    std::vector<uint4> own((size_t)G * own_stride, uint4{kNone, 0u, kNone, 0u}),
+        halo((size_t)G * halo_stride, uint4{kNone, 0u, kNone, 0u});
+    for (unsigned b = 0; b < G; ++b)
+    {
+        std::copy(ownl[b].begin(), ownl[b].end(), own.begin() + (size_t)b * own_stride);
+        std::copy(halol[b].begin(), halol[b].end(), halo.begin() + (size_t)b * halo_stride);
+    }
+    // the stencil of each boundary type (lattice.inc's shell cell form regrouped): per offset o >= 1, the sum of the
+    // pair blocks (c, c') with c' - c = o over the cells that exist around a node of that type, in fp64, stored in the
+    // rows' packed order {S00 S10 S01 S11} {S02 S12 S20 S21} {S22 - - -}
+    const int npairs = t.lhex ? kLatHexPairs : kLatPairs;
+    std::vector<float> cf((size_t)(noff + npairs) * 9);
+    if (hipMemcpy(cf.data(), t.lcoef, cf.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
+    std::vector<float4> tco(27ull * noff * 3, float4{0.f, 0.f, 0.f, 0.f});
+    for (unsigned ty = 0; ty < 27; ++ty)
+    {
+        const unsigned sd[3] = {ty % 3, (ty / 3) % 3, ty / 9};  // 0 lo, 1 inside, 2 hi
+        unsigned w8 = 0;
+        for (unsigned c8 = 0; c8 < 8; ++c8)
+        {
+            bool in = true;
+            for (int ax = 0; ax < 3; ++ax)
+                in = in && (((c8 >> ax) & 1u) ? sd[ax] != 0 : sd[ax] != 2);
+            w8 |= (in ? 1u : 0u) << c8;
+        }
+        for (int o = 1; o < noff; ++o)
+        {
+            double S[9] = {};
+            for (int pp = 0; pp < npairs; ++pp)
+            {
+                const int c = t.lhex ? pp / 8 : kLatPair[pp][0];
+                const int po = t.lhex ? kLatHexPairOff[pp] : kLatPairOff[pp];
+                if (po != o || !((w8 >> c) & 1u))
+                    continue;
+                for (int e = 0; e < 9; ++e)
+                    S[e] += (double)cf[(size_t)9 * noff + 9 * pp + e];
+            }
+            float4 *q = &tco[(size_t)3 * (ty * noff + o)];
+            q[0] = float4{(float)S[0], (float)S[3], (float)S[1], (float)S[4]};
+            q[1] = float4{(float)S[2], (float)S[5], (float)S[6], (float)S[7]};
+            q[2] = float4{(float)S[8], 0.f, 0.f, 0.f};
+        }
+    }
+    float4 *dtc;
+    if (upload(h, &dtc, tco.data(), tco.size()))
+        return false;
+    uint4 *dh, *dow, *dha;
+    float *dpub;
+    double *dsh;
+    if (upload(h, &dh, hdr.data(), hdr.size()) || upload(h, &dow, own.data(), own.size()) ||
+        upload(h, &dha, halo.data(), halo.size()) || dalloc(h, &dpub, 2ull * 12 * std::max<uint32_t>(npub, 1u)) ||
+        dalloc(h, &dsh, 2ull * 2 * kFusedSharesHost * G))
+        return false;
+    // tags 0: below every tag a solve waits for (the first solve's base is 1, its phases wait for 2 and up)
+    if (hipMemset(dsh, 0, 2ull * 2 * kFusedSharesHost * G * sizeof(double)) != hipSuccess ||
+        hipMemset(dpub, 0, 2ull * 12 * std::max<uint32_t>(npub, 1u) * sizeof(float)) != hipSuccess)
+        return false;
+    rp.G = G;
+    rp.npt = npt;
+    rp.nph = nph;
+    rp.own_stride = own_stride;
+    rp.halo_stride = halo_stride;
+    rp.npub = std::max<uint32_t>(npub, 1u);
+    rp.lds = lds;
+    std::memcpy(rp.dims, bg, sizeof bg);
+    rp.max_own = max_own;
+    rp.max_halo = max_halo;
+    rp.halo_total = halo_total;
+    rp.hdr = dh;
+    rp.tcoef = dtc;
+    rp.own = dow;
+    rp.halo = dha;
+    rp.pub = dpub;
+    rp.sh = dsh;
+    rp.state = 1;
+    return true;
+}
+
+uint64_t resident_offchip_bytes(const cwf_hip_system *h)
+{
+    const ResidentPlan &rp = h->res;
+    return 48ull * (rp.halo_total + rp.npub) + 80ull * rp.G * (1ull + rp.G);
+}
+
+}  // namespace cwf

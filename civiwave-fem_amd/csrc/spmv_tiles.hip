@@ -27,6 +27,7 @@
 
 #include "blockinv_pack.hpp"
 #include "cwf_internal.hpp"
+#include "lattice_common.hpp"
 #include "reduce.hpp"
 
 namespace cwf
@@ -39,7 +40,6 @@ constexpr int kMaxM = 16;
 #endif
 constexpr int kUpdThreads = CWF_UPD_THREADS;  // update-pass workgroup size (its per-workgroup shares are refolded by every consumer workgroup)
 constexpr unsigned kMaxUpdateBlocks = 2048;  // 8 resident per CU (grid-stride beyond); <= 2048 shares to fold
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 
 // buffer descriptor over a whole allocation (base pointer wave-uniform: a kernel argument)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t whole_rsrc(const void *base)
@@ -60,36 +60,6 @@ __device__ __forceinline__ void store3(float *base, __amdgpu_buffer_rsrc_t rs, u
         __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 16);
     else
         __builtin_amdgcn_raw_buffer_store_b96(v, rs, (uint32_t)(12ull * q), 0, 0);
-}
-
-// Control-block words as vector (buffer) loads. A consumer prologue issues them with its gathers and the scalar
-// fold's loads, and they return with those: one memory round trip. As scalar loads they cost one of their own, in
-// front of the fold's loads (every s_waitcnt lgkmcnt(0) for a kernel argument the fold needs waits for them) or
-// after the fold (where their value is used).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ctl_rsrc(const Ctl *c)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<Ctl *>(c), 0, (int)sizeof(Ctl), 0x00020000);
-}
-__device__ __forceinline__ double ctl_f64(__amdgpu_buffer_rsrc_t rs, uint32_t off)
-{
-    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0),
-                   hi = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4u, 0, 0);
-    return __hiloint2double((int)hi, (int)lo);
-}
-// what residual_step reads of the control block for iteration it >= 1
-struct CtlPre
-{
-    int active;
-    double rho_old, tol;  // rho2[(it - 1) & 1], tol
-};
-__device__ __forceinline__ CtlPre ctl_prefetch(const Ctl *ctl, unsigned it)
-{
-    const __amdgpu_buffer_rsrc_t rs = ctl_rsrc(ctl);
-    CtlPre p;
-    p.active = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)offsetof(Ctl, active), 0, 0);
-    p.rho_old = ctl_f64(rs, (uint32_t)(offsetof(Ctl, rho2) + 8u * ((it - 1u) & 1u)));
-    p.tol = ctl_f64(rs, (uint32_t)offsetof(Ctl, tol));
-    return p;
 }
 
 // pcg.cpp:862-895 for iteration `it` >= 1 from the update kernel's r.r / r.z shares (stride 1), or
@@ -915,7 +885,6 @@ __global__ __launch_bounds__(NT) void k_keff_tiles_pipe(DevSys s, const float *_
 // registers and pushes one force per node to its position in the tile's local CSR (the node's run start,
 // kept in LDS, plus the group's 4-bit rank in the run from the 16-B record); the node fold, partial stores,
 // p.Ap share and owner p store are those of k_keff_tiles_pipe.
-typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
@@ -2161,7 +2130,7 @@ FusedArgs fused_args(cwf_hip_system *h, unsigned j)
 }
 }  // namespace
 
-void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st)
+void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStream_t st, bool launch0)
 {
     const DevSys &s = h->ds;
     const uint32_t nbD = fast_dot_blocks(s.D);
@@ -2172,7 +2141,8 @@ void fast_fused_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
     fast_dot(h->r, h->r, nullptr, s.D, h->part1, nullptr, st);
     fast_init_scalars_strided(h, h->part0, h->part1, nbD, 1u, rel_tol, st);
     // launch 0 reads p_(-1) and Ap_(-1) (times beta = alpha = 0): zero, so no stale non-finite value enters
-    fast_fused_launch0(h, st);
+    if (launch0)  // (the resident solve runs its phase 0 itself)
+        fast_fused_launch0(h, st);
 }
 
 void fast_fused_iteration(cwf_hip_system *h, unsigned it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)

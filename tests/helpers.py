@@ -83,3 +83,21 @@ def dense_stiffness(P, coords, tets, stiffness):
     return O.dense_assemble(O.Packed(P.node_count, E, P.connectivity, P.gradients, P.volume, P.material_index,
                                      P.lumped_mass64, P.lumped_mass, P.offsets, P.element_indices, P.local_indices),
                             tets, g64, v64, np.asarray(stiffness))
+
+
+# FAST vs PARITY after a Newmark step at the runtime tolerance (3e-4). Both increments solve the same RHS (the first
+# step from rest) to |b - K x| <= tol |b| in their own recurrence residual. A residual-side bound |K_p (x_f - x_p)| <=
+# 2 tol |b| does NOT hold here, and not because either solve is off: an fp32 x carries rounding noise of ~|K| eps32 |x|
+# in its true residual, which on these blocks is 10-40x tol |b| (measured, profiles/r06a_gpu_tests.log: C2 573 against
+# 58, C3 4,831 against 133, C4 2,815 against 55) while the increments agree to 0.9-1.3e-6 of |x|. So the check is on
+# the solutions: FAST's operator is within 2e-5 of PARITY's and both solves stop in the same iteration count (+-3),
+# which leaves the increments and states equal to well below the 1e-4 relative every FAST solve test states.
+STEP_REL_TOL = 1e-4
+
+
+def check_step_against_parity(xf, xp, uf, up, what):
+    """The FAST step's increment xf and displacement uf against the PARITY step's xp, up."""
+    rel_x = float(np.linalg.norm(xf.astype(np.float64) - xp) / np.linalg.norm(xp.astype(np.float64)))
+    rel_u = float(np.linalg.norm(uf.astype(np.float64) - up) / np.linalg.norm(up.astype(np.float64)))
+    print(f"{what}: |x_f - x_p|/|x_p| = {rel_x:.3e}, |u_f - u_p|/|u_p| = {rel_u:.3e}")
+    assert rel_x <= STEP_REL_TOL and rel_u <= STEP_REL_TOL, (what, rel_x, rel_u)

@@ -251,34 +251,40 @@ def test_fused_iteration_matches_two_kernel_loop(name, monkeypatch):
         monkeypatch.setenv("CWF_FUSED_MAXWG", "16")  # forced: by default a grid below the items runs two kernels)
         name, on = name.split("-")[0], "2"
     # hex: native hex8 cells (the deeper two-plane prefetch of the 27-point stencil), checked against the fp64 solve
-    # of the oracle operator. Its iteration counts are not compared: this static stiffness-dominated solve asks for a
-    # recurrence residual of 1e-6 |rhs| where the true residual of an fp32 x floors near 3e-3 |rhs|, and there finite
-    # precision CG's count follows each path's rounding (fused 216, two-kernel 310, hex tiles 168-175, fp64 163:
-    # profiles/r05zh_hex_counts.log, tools/hex_counts.py) while every x is within 3e-6 of the fp64 one
+    # of the oracle operator at tol 1e-6, its iteration counts at tol 1e-4. At 1e-6 this static
+    # stiffness-dominated solve asks for a recurrence residual where the true residual of an fp32 x floors near
+    # 3e-3 |rhs|, and there finite-precision CG's count follows each path's rounding (fused 216, two-kernel 310, hex
+    # tiles 168-175, fp64 163: profiles/r05zh_hex_counts.log, tools/hex_counts.py; DESIGN.md section 9, a known fp32
+    # floor effect); at the reachable 1e-4 the counts are compared as for tet4
     case = (scenarios.block_case(33, 9, 5, h=0.1, element="hex8", tol=1e-6, max_iterations=800) if name == "hex"
             else CASES[name]())
     rhs = case.static_rhs()
     mi = case.cfg.solver.max_iterations
-    out = {}
-    for fused in (on, "0"):
+
+    def solve(fused, tol):
         monkeypatch.setenv("CWF_FUSED", fused)
         s = _system(case)
         assert _kernel(s).startswith("k_pcg_lattice" if fused != "0" else "k_keff_lattice"), _kernel(s)
         x = np.zeros_like(rhs)
         r = np.zeros_like(rhs)
-        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(mi, 1e-6), pcg.PcgVectors(x, r)).value()
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(mi, tol), pcg.PcgVectors(x, r)).value()
         assert t.converged
         # the r output is the residual of x (rhs - K x, Dirichlet rows 0) to fp32 accuracy
-        out[fused] = (t, x, r)
-    (tf, xf, rf), (tk, xk, _) = out[on], out["0"]
+        return t, x, r
+
+    (tf, xf, rf), (tk, xk, _) = solve(on, 1e-6), solve("0", 1e-6)
     if name == "hex":
+        (tf4, _, _), (tk4, _, _) = solve(on, 1e-4), solve("0", 1e-4)
+        print(f"hex8 fused / two-kernel iterations: tol 1e-4 {tf4.iterations} / {tk4.iterations}, "
+              f"tol 1e-6 {tf.iterations} / {tk.iterations}")
+        assert abs(tf4.iterations - tk4.iterations) <= max(3, tk4.iterations // 20), (tf4.iterations, tk4.iterations)
         P = case.packing
         ref = {"x": O.hex8_solve64(case.mesh.coords, case.mesh.tets, P.material_index, O.make_stiffness(30.0e9, 0.2),
                                    *case.scalars(), P.lumped_mass, P.bc_mask, rhs)}
         assert np.linalg.norm(xk - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
     else:
-        ref = oracle_system(case.packing, case.materials, *case.scalars()).solve_pcg(rhs, mi, 1e-6)
         assert abs(tf.iterations - tk.iterations) <= max(3, tk.iterations // 20), (tf.iterations, tk.iterations)
+        ref = oracle_system(case.packing, case.materials, *case.scalars()).solve_pcg(rhs, mi, 1e-6)
     assert np.linalg.norm(xf - ref["x"]) <= 1e-4 * np.linalg.norm(ref["x"])
     assert tf.residual_norm <= 1e-6 * np.linalg.norm(rhs.astype(np.float64)) * 1.0001
     assert abs(np.linalg.norm(rf.astype(np.float64)) - tf.residual_norm) <= 1e-3 * tf.residual_norm

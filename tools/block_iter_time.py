@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-iteration time of a FAST solve on one structured block, one handle (the compute a slab shard of that size runs
 per PCG iteration, without its exchange): fixed iterations (tol 1e-30), the second solve timed (wall clock, host
-read-backs included), the fused iteration against the two-kernel loop (CWF_FUSED=0).
+read-backs included): the resident one-launch solve (the default where the block fits on chip, resident.hip), the fused
+launch-per-iteration schedule (CWF_FUSED=1) and the two-kernel loop (CWF_FUSED=0).
 
 usage: python tools/block_iter_time.py NX NY NZ [ITERATIONS]"""
 import os
@@ -22,8 +23,11 @@ def main():
 
     case = scenarios.block_case(nx, ny, nz, h=0.1, tol=1e-30, max_iterations=its)
     rhs = case.static_rhs()
-    for fused in ("1", "0"):
-        os.environ["CWF_FUSED"] = fused
+    for fused in ("resident", "1", "0"):
+        if fused == "resident":
+            os.environ.pop("CWF_FUSED", None)
+        else:
+            os.environ["CWF_FUSED"] = fused
         s = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, *case.scalars(), mode=_lib.MODE_FAST)
         for _ in range(2):
             x = np.zeros_like(rhs)
@@ -31,7 +35,7 @@ def main():
             t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(its, 1e-30), pcg.PcgVectors(x, None)).value()
             el = time.perf_counter() - t0
         kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
-        print(f"{nx}x{ny}x{nz} ({3 * nx * ny * nz / 1e6:.2f}M DOF) {'fused' if fused == '1' else 'two kernels'}: "
+        print(f"{nx}x{ny}x{nz} ({3 * nx * ny * nz / 1e6:.2f}M DOF) { {'resident': 'resident', '1': 'fused'}.get(fused, 'two kernels')}: "
               f"{t.iterations} iterations, {el / max(t.iterations, 1) * 1e6:.2f} us per iteration ({kern})", flush=True)
         s.close()
 

@@ -5,7 +5,8 @@
 #   bash tools/gpu_run.sh TAG STEP [STEP ...]
 #
 # STEP is one of
-#   tests[:FILE,FILE..]     pytest -m gpu over tests/ (or the listed test files)
+#   tests[:FILE,FILE..[:KEXPR]]  pytest -m gpu -s over tests/ (or the listed test files; KEXPR: a -k expression,
+#                           commas for spaces; no '::' node ids, ':' splits the step)
 #   smoke                   __graft_entry__.smoke()
 #   bench:NAME[:ARGS]       one bench.py line (ARGS: bench.py arguments, commas for spaces) -> <TAG>_bench_NAME.json
 #   ab:NAME:ENV[:ARGS]      the same bench twice per pass, in-tree default vs ENV (commas for spaces: several
@@ -49,7 +50,8 @@ for step in "$@"; do
   case $kind in
     tests)
       files=$(sp "${a:-tests}")
-      timeout -k 10 900 python -u -m pytest $files -m gpu -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+      kx=(); [ -n "$b" ] && kx=(-k "$(sp "$b")")
+      timeout -k 10 900 python -u -m pytest $files "${kx[@]}" -m gpu -v -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
       rc=$?; tail -1 $O/gpu_tests.log
       [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $O/gpu_tests.log | head -30; exit $rc; } ;;
     smoke)

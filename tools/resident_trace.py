@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Summarise the per-workgroup phase stamps of one resident-solve phase (CWF_RESIDENT_TRACE, resident.hip `stamp`):
+per workgroup s_memrealtime (100 MHz) at 0 the phase's start (its polls begin), 1 every polled granule carries the
+previous phase's tag, 2 the shares folded and the scalars decided, 3 the own and halo p formed into the image, 4 the
+rows done, 5 the dots reduced, 6 the shares' granules stored (the phase's end). Prints the median / max of each span and when the last
+workgroup arrived relative to the first one's release.
+
+usage: python tools/resident_trace.py TRACE [INDEX]"""
+import sys
+
+import numpy as np
+
+
+def blocks(path):
+    cur = None
+    for line in open(path):
+        if line.startswith("#"):
+            if cur:
+                yield cur
+            cur = {"hdr": line.strip(), "rows": []}
+        elif line.strip() and cur is not None:
+            cur["rows"].append([int(v) for v in line.split()])
+    if cur:
+        yield cur
+
+
+def main():
+    bs = list(blocks(sys.argv[1]))
+    B = bs[int(sys.argv[2]) if len(sys.argv) > 2 else -1]
+    a = np.array(B["rows"], np.int64)
+    t = a[:, 1:8].astype(np.float64) * 0.01  # us
+    t -= t[:, 0].min()
+    names = ["poll", "fold+decide", "form", "rows", "reduce", "shares"]
+    print(f"{B['hdr']}: {len(a)} workgroups")
+    for i, n in enumerate(names):
+        d = t[:, i + 1] - t[:, i]
+        print(f"  {n:12s} median {np.median(d):6.2f}  max {d.max():6.2f} us")
+    print(f"  phase start spread {t[:, 0].max() - t[:, 0].min():.2f} us, release (wait done) spread "
+          f"{t[:, 1].max() - t[:, 1].min():.2f} us, last end {t[:, 6].max():.2f} us after the first start, "
+          f"compute (release -> end) median {np.median(t[:, 6] - t[:, 1]):.2f} max {np.max(t[:, 6] - t[:, 1]):.2f}")
+
+
+if __name__ == "__main__":
+    main()
