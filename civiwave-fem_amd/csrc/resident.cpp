@@ -114,7 +114,7 @@ bool resident_ready(cwf_hip_system *h)
                         needed[m] = 1;
                 }
             }
-    // own lists (block-interior nodes first: the brick rows; then the surface's cell-form rows), publication indices
+    // own lists (block-surface nodes first: their type-stencil rows; then the interior's brick rows), publication indices
     // in that order box after box, then the halo lists (sorted by publication index: consecutive lanes, consecutive
     // records)
     std::vector<uint32_t> pubidx(N, kNone);
@@ -135,8 +135,8 @@ bool resident_ready(cwf_hip_system *h)
                     for (unsigned i = q[0]; i < q[1]; ++i)
                     {
                         const bool shell = i == 0 || j == 0 || k == 0 || i + 1 == nx || j + 1 == ny || k + 1 == nz;
-                        if (shell != (pass == 1))
-                            continue;
+                        if (shell != (pass == 0))  // the surface first: its slower rows land in the first
+                            continue;              // wave-slots, one wave per SIMD in turn, not in the last waves
                         const uint32_t n = node(i, j, k);
                         const unsigned slot = (k - q[4] + 1) * PXY + (j - q[2] + 1) * PX + (i - q[0] + 1);
                         if (needed[n])

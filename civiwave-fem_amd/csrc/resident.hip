@@ -110,7 +110,7 @@ __device__ __forceinline__ void block_sum_lds(double v[K], double *red)
 }
 
 template <bool SYM, class E, int NPT, int NPH>
-__global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, const float *__restrict__ coef)
+__global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pcg_resident(DevSys s, ResArgs ra, const float *__restrict__ coef)
 {
     extern __shared__ float4 pl[];  // the box + one-node halo image of p_j (out-of-block entries stay 0)
     __shared__ double red[kFusedShares * (kResNT / 64)];
@@ -132,6 +132,7 @@ __global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, c
         pl[i] = float4{0.f, 0.f, 0.f, 0.f};
     for (uint32_t i = tid; i < 27u * E::nOff * 3u; i += kResNT)
         tcf[i] = ra.tcoef[i];
+
     if (tid < kLatClasses)
     {
         const float4 zA = T.lcz[2u * tid], zB = T.lcz[2u * tid + 1u];
@@ -189,6 +190,27 @@ __global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, c
     {
         float alpha = 0.f, beta = 0.f;
         float hr[NPH][3], ha[NPH][3], hp[NPH][3];
+        u32x4 w0[NPH], w1[NPH], w2[NPH];  // phase j - 1's halo records (granules {r, tag} {Ap, tag} {p, tag})
+        const uint32_t par = (j - 1u) & 1u, want = ra.tag0 + j;
+        // the workgroup's vote on `ok` (slot round mod 3; the next round's slot is reset before this round's
+        // barrier: its last readers passed a barrier since). Every thread counts the same rounds: uniform
+        uint32_t round = 0;
+        const auto all_ok = [&](bool ok) {
+            if (tid == 0)
+                vote[(round + 1u) % 3u] = 1;
+            if (!ok)
+                vote[round % 3u] = 0;
+            lds_sync();
+            return vote[round % 3u] != 0;
+        };
+        const auto give_up = [&]() {
+            if (tid == 0)
+            {
+                ra.ctl->error = CWF_ERR_HIP;
+                ra.ctl->error_iter = (int)j;
+                ra.ctl->active = 0;
+            }
+        };
         if (j == 0)  // phase 0 (alpha = beta = 0; Ap_(-1) = p_(-1) = 0): the halo's r_0 from fast_fused_init's r
         {
 #pragma unroll
@@ -208,49 +230,36 @@ __global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, c
             // phase j - 1's five shares of every workgroup and this box's halo records, polled until every granule
             // carries phase j - 1's tag (each 16-B granule is one write-through store with its own tag: no counter,
             // no ordering between granules needed). Bounded: a workgroup that never publishes ends the solve
-            const uint32_t par = (j - 1u) & 1u, want = ra.tag0 + j;
-            u32x4 g[kFusedShares], w0[NPH], w1[NPH], w2[NPH];
-            for (uint32_t round = 0;; ++round)
+            u32x4 g[kFusedShares];
+            // the five share granules of every workgroup (thread t < G: workgroup t's), polled until all carry
+            // phase j - 1's tag; then this box's halo records are requested and arrive while the shares are folded
+            // and the own nodes formed (a producer stores its halo records before its shares, so they have nearly
+            // always landed by then; a record with another tag is read again below)
+            for (;; ++round)
             {
 #pragma unroll
                 for (int q = 0; q < kFusedShares; ++q)
                     g[q] = ld4_sc1(rsh, tid < G ? 16u * ((par * G + tid) * kFusedShares + (uint32_t)q) : kResOob);
-#pragma unroll
-                for (int h = 0; h < NPH; ++h)
-                {
-                    const uint32_t po = hn[h] != kResNone ? 48u * (par * ra.npub + hpub[h]) : kResOob;
-                    w0[h] = ld4_sc1(rpub, po);
-                    w1[h] = ld4_sc1(rpub, po + 16u);
-                    w2[h] = ld4_sc1(rpub, po + 32u);
-                }
                 bool ok = true;
-                if (tid < G)
 #pragma unroll
-                    for (int q = 0; q < kFusedShares; ++q)
-                        ok = ok && g[q].z == want;
-#pragma unroll
-                for (int h = 0; h < NPH; ++h)
-                    ok = ok && (hn[h] == kResNone || (w0[h].w == want && w1[h].w == want && w2[h].w == want));
-                // the workgroup's vote (slot round mod 3; the next round's slot is reset before this round's barrier:
-                // its last readers passed the barrier before this one)
-                if (tid == 0)
-                    vote[(round + 1u) % 3u] = 1;
-                if (!ok)
-                    vote[round % 3u] = 0;
-                lds_sync();
-                if (vote[round % 3u])
+                for (int q = 0; q < kFusedShares; ++q)
+                    ok = ok && (tid >= G || g[q].z == want);
+                if (all_ok(ok))
                     break;
-                if (round >= kResMaxRounds)  // uniform: every thread counts the same rounds
+                if (round >= kResMaxRounds)
                 {
-                    if (tid == 0)
-                    {
-                        ra.ctl->error = CWF_ERR_HIP;
-                        ra.ctl->error_iter = (int)j;
-                        ra.ctl->active = 0;
-                    }
+                    give_up();
                     return;  // x, r are not written: the solve fails
                 }
                 __builtin_amdgcn_s_sleep(2);
+            }
+#pragma unroll
+            for (int h = 0; h < NPH; ++h)
+            {
+                const uint32_t po = hn[h] != kResNone ? 48u * (par * ra.npub + hpub[h]) : kResOob;
+                w0[h] = ld4_sc1(rpub, po);
+                w1[h] = ld4_sc1(rpub, po + 16u);
+                w2[h] = ld4_sc1(rpub, po + 32u);
             }
             stamp(j, 1);
             double v[kFusedShares];
@@ -264,16 +273,6 @@ __global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, c
             if (!go)
                 break;
             stamp(j, 2);
-#pragma unroll
-            for (int h = 0; h < NPH; ++h)
-            {
-                hr[h][0] = __uint_as_float(w0[h].x), hr[h][1] = __uint_as_float(w0[h].y);
-                hr[h][2] = __uint_as_float(w0[h].z);
-                ha[h][0] = __uint_as_float(w1[h].x), ha[h][1] = __uint_as_float(w1[h].y);
-                ha[h][2] = __uint_as_float(w1[h].z);
-                hp[h][0] = __uint_as_float(w2[h].x), hp[h][1] = __uint_as_float(w2[h].y);
-                hp[h][2] = __uint_as_float(w2[h].z);
-            }
         }
         // form r_j, z_j, p_j (x_j) of the own nodes and p_j of the halo into the image. The per-node indices are
         // opaque per phase, so no address derived from them is hoisted out of the phase loop into a VGPR
@@ -303,14 +302,49 @@ __global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, c
             pl[oslot[u]] = float4{pn[0], pn[1], pn[2], 0.f};
             fused_entry_dots(rn, zz, d);
         }
-#pragma unroll
-        for (int h = 0; h < NPH; ++h)
+        // the halo's p_j: phase 0 from fast_fused_init's r; later phases from the records requested above, each
+        // granule checked for its tag (a record that had not landed is read again: a bounded, voted re-read)
+        for (;; ++round)
         {
-            if (hn[h] == kResNone)
-                continue;
-            float rn[3], zz[3], pn[3];
-            fused_form(czA, czB, hc[h], alpha, beta, hr[h], ha[h], hp[h], rn, zz, pn);
-            pl[hslot[h]] = float4{pn[0], pn[1], pn[2], 0.f};
+            bool hok = true;
+#pragma unroll
+            for (int h = 0; h < NPH; ++h)
+            {
+                if (hn[h] == kResNone)
+                    continue;
+                if (j > 0)
+                {
+                    if (w0[h].w != want || w1[h].w != want || w2[h].w != want)
+                    {
+                        hok = false;
+                        continue;
+                    }
+                    hr[h][0] = __uint_as_float(w0[h].x), hr[h][1] = __uint_as_float(w0[h].y);
+                    hr[h][2] = __uint_as_float(w0[h].z);
+                    ha[h][0] = __uint_as_float(w1[h].x), ha[h][1] = __uint_as_float(w1[h].y);
+                    ha[h][2] = __uint_as_float(w1[h].z);
+                    hp[h][0] = __uint_as_float(w2[h].x), hp[h][1] = __uint_as_float(w2[h].y);
+                    hp[h][2] = __uint_as_float(w2[h].z);
+                }
+                float rn[3], zz[3], pn[3];
+                fused_form(czA, czB, hc[h], alpha, beta, hr[h], ha[h], hp[h], rn, zz, pn);
+                pl[hslot[h]] = float4{pn[0], pn[1], pn[2], 0.f};
+            }
+            if (j == 0 || all_ok(hok))
+                break;
+            if (round >= kResMaxRounds)
+            {
+                give_up();
+                return;
+            }
+#pragma unroll
+            for (int h = 0; h < NPH; ++h)
+            {
+                const uint32_t po = hn[h] != kResNone ? 48u * (par * ra.npub + hpub[h]) : kResOob;
+                w0[h] = ld4_sc1(rpub, po);
+                w1[h] = ld4_sc1(rpub, po + 16u);
+                w2[h] = ld4_sc1(rpub, po + 32u);
+            }
         }
         lds_sync();
         stamp(j, 3);
@@ -351,8 +385,8 @@ __global__ __launch_bounds__(kResNT) void k_pcg_resident(DevSys s, ResArgs ra, c
                 acc[1] = acc01.y;
                 acc[2] = acc2;
             }
-            else  // the brick rows' difference form (lattice_fused.inc rows1)
-            {
+            else  // the brick rows' difference form (lattice_fused.inc rows1); the blocks as scalar loads (from LDS
+            {     // as well: rows 3.5 -> 4.7 us per phase on C2)
                 int zoff;
                 asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
                 const float *__restrict__ cf = coef + zoff;
