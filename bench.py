@@ -200,6 +200,8 @@ def hbm_roofline(L, device, key="c3", steps=2, sample=5, general=False):
 def operator_of(kname: str) -> str:
     """Which operator a K_eff kernel name is: the structured-block stencil (reached only by exact structured Kuhn /
     hex8 boxes of one material, lattice.cpp) or the general element tiles every other mesh runs."""
+    if kname.startswith("k_pcg_resident"):
+        return "structured-block stencil, resident one-launch PCG solve (vectors on chip, one workgroup per box)"
     if kname.startswith("k_pcg_lattice"):
         return "structured-block stencil, fused single-launch PCG iteration"
     if kname.startswith("k_keff_lattice"):

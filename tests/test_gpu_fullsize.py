@@ -3,9 +3,9 @@
 C2 = configs[1] (69^3 hex block -> 1,971,054 Kuhn tets, 1.03M DOF): PARITY is bit-exact against the
 pinned oracle at full size: apply_keff, the block-Jacobi inverse, and 25 PCG iterations (x, r, the fp64
 residual history, the max-iterations stop).
-C2 in FAST, the benchmarked kernel at the benchmarked size: the fused one-launch iteration
-k_pcg_lattice on its one-round grid (436 workgroups, 112 of them shell workgroups, 436 x 5 shares folded per prologue)
-solves a static system at tol 1e-6 to the PARITY solution (which is the oracle's solve_pcg bit for bit: the 25-iteration
+C2 in FAST, the benchmarked kernel at the benchmarked size: the resident one-launch solve
+k_pcg_resident (245 workgroups, one per box) and the fused launch-per-iteration k_pcg_lattice (its one-round grid of 436
+workgroups, 112 of them shell workgroups, 436 x 5 shares folded per prologue) each solve a static system at tol 1e-6 to the PARITY solution (which is the oracle's solve_pcg bit for bit: the 25-iteration
 test below and the full C1 solve in test_gpu_configs.py) within 1e-4 relative, in its iteration count +-5%; and two
 Newmark steps at the config's runtime tolerance follow the PARITY Stepper's (iterations +-3, u / v / the increment
 within helpers.STEP_REL_TOL = 1e-4 relative, where 0.9e-6 is measured).
@@ -151,11 +151,22 @@ def test_c3_fast_newmark_step_matches_parity(c3):
 
 
 # ------------------------------------------------------------------------------------------------ C2 FAST (the bench)
-def test_c2_fast_static_solve_is_the_fused_lattice_and_matches_parity(c2):
+# the benchmarked path (the default: the resident one-launch solve, one 512-thread workgroup per 14 x 10 x 10 box) and
+# the launch-per-iteration fused schedule it replaced (CWF_FUSED=1: its one-round grid of 436 workgroups)
+C2_SCHEDULES = {"resident": (None, "k_pcg_resident<true, LatKuhn, 3, 2>"),
+                "fused": ("1", "k_pcg_lattice<true, LatKuhn, true, true, false, false>")}
+
+
+@pytest.mark.parametrize("schedule", sorted(C2_SCHEDULES))
+def test_c2_fast_static_solve_matches_parity(c2, schedule, monkeypatch):
+    env, want = C2_SCHEDULES[schedule]
+    if env is None:
+        monkeypatch.delenv("CWF_FUSED", raising=False)
+    else:
+        monkeypatch.setenv("CWF_FUSED", env)
     sf = _system(c2, _lib.MODE_FAST)
     k = _kernel(sf)
-    # the one-item instantiation on the one-round grid the bench runs (the last template flag: persistent)
-    assert k.startswith("k_pcg_lattice<true, LatKuhn, true, true, false, false>"), k
+    assert k == want, k
     sp = _system(c2, _lib.MODE_PARITY)
     rhs = c2.static_rhs()
     out = {}
@@ -166,7 +177,8 @@ def test_c2_fast_static_solve_is_the_fused_lattice_and_matches_parity(c2):
         out[name] = (t, x, r)
     (tf, xf, rf), (tp, xp, _) = out["fast"], out["parity"]
     rel = float(np.linalg.norm(xf.astype(np.float64) - xp) / np.linalg.norm(xp.astype(np.float64)))
-    print(f"C2 static tol 1e-6: FAST {tf.iterations} it, PARITY {tp.iterations} it, |x_f - x_p|/|x_p| = {rel:.3e}")
+    print(f"C2 static tol 1e-6 ({schedule}): FAST {tf.iterations} it, PARITY {tp.iterations} it, "
+          f"|x_f - x_p|/|x_p| = {rel:.3e}")
     assert rel <= 1e-4
     assert abs(tf.iterations - tp.iterations) <= max(3, tp.iterations // 20), (tf.iterations, tp.iterations)
     # the r output is the solve's own residual (fp32 recurrence) and meets the tolerance
@@ -176,11 +188,17 @@ def test_c2_fast_static_solve_is_the_fused_lattice_and_matches_parity(c2):
     sp.close()
 
 
-def test_c2_fast_newmark_steps_follow_the_parity_stepper(c2):
+@pytest.mark.parametrize("schedule", sorted(C2_SCHEDULES))
+def test_c2_fast_newmark_steps_follow_the_parity_stepper(c2, schedule, monkeypatch):
+    env, want = C2_SCHEDULES[schedule]
+    if env is None:
+        monkeypatch.delenv("CWF_FUSED", raising=False)
+    else:
+        monkeypatch.setenv("CWF_FUSED", env)
     P = c2.packing
     sts = {m: Stepper(P, c2.materials, c2.rayleigh, c2.cfg.solver, c2.cfg.time, mode=m)
            for m in (_lib.MODE_PARITY, _lib.MODE_FAST)}
-    assert _kernel(sts[_lib.MODE_FAST].system).startswith("k_pcg_lattice"), _kernel(sts[_lib.MODE_FAST].system)
+    assert _kernel(sts[_lib.MODE_FAST].system) == want, _kernel(sts[_lib.MODE_FAST].system)
     for k in range(2):
         tp = sts[_lib.MODE_PARITY].step(0.01 * k).value().pcg
         tf = sts[_lib.MODE_FAST].step(0.01 * k).value().pcg

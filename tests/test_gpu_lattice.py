@@ -44,9 +44,10 @@ def _kernel(s):
     return (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
 
 
-# the structured-block stencil: the fused one-launch iteration (lattice_fused.inc, the default where its grid is
-# at most CWF_FUSED_MAXWG workgroups) or the two-kernel one (k_keff_lattice + the update pass)
-LATTICE = ("k_pcg_lattice", "k_keff_lattice")
+# the structured-block stencil: the resident one-launch solve (resident.hip, the default where the block fits on chip;
+# tests/test_gpu_resident.py), the fused one-launch iteration (lattice_fused.inc, where its grid is at most
+# CWF_FUSED_MAXWG workgroups) or the two-kernel one (k_keff_lattice + the update pass)
+LATTICE = ("k_pcg_resident", "k_pcg_lattice", "k_keff_lattice")
 
 
 def _apply_err(case, s, seed=3):

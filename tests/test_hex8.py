@@ -183,7 +183,7 @@ def test_gpu_hex8_structured_blocks_run_the_lattice_stencil(hcase):
     kern = _keff_kernel(gpu_hex_system(hcase))
     # an isotropic block's stencil is point-symmetric (S_-d = S_d): the paired-direction instantiation
     want = (("k_keff_hex_tiles",) if hcase.name.endswith("-jitter") else
-            ("k_keff_lattice<1, false, true, LatHex,", "k_pcg_lattice<true, LatHex,"))
+            ("k_keff_lattice<1, false, true, LatHex,", "k_pcg_lattice<true, LatHex,", "k_pcg_resident<true, LatHex,"))
     assert kern.startswith(want), kern
 
 
