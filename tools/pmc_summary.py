@@ -58,17 +58,32 @@ def main():
                           hbm_gbs=bw)
     if a.json:
         sel = {k: v for k, v in out.items() if not a.kernel or any(s in k or norm(s) == norm(k) for s in a.kernel)}
-        total = sum(v["hbm_bytes_per_launch"] or 0 for v in sel.values())
         # provenance: the source hash of the profiled kernel as the profiled bench run printed it (bench.py only takes
         # this file's traffic for a library built from the same sources)
-        src_hash = None
+        src_hash, bench = None, None
         for log in sorted(glob.glob(os.path.join(a.dir, "bench_*.log"))):
             for line in open(log, errors="replace"):
                 if line.startswith('{"metric"'):
-                    src_hash = src_hash or json.loads(line)["roofline"].get("kernel_source_hash")
-        json.dump(dict(kernels=sel, hbm_bytes_per_launch=total, source_hash=src_hash,
-                       note="FETCH_SIZE x2 x1024 + WRITE_SIZE x1024 per launch, summed over the selected "
-                            "kernels (MI355X_MICROARCH.md HBM section)"), open(a.json, "w"), indent=1)
+                    bench = bench or json.loads(line)
+                    src_hash = src_hash or bench["roofline"].get("kernel_source_hash")
+        note = ("FETCH_SIZE x2 x1024 + WRITE_SIZE x1024 per launch, summed over the selected kernels "
+                "(MI355X_MICROARCH.md HBM section)")
+        # the resident solve is ONE launch per PCG solve: its per-launch figures are per solve. Profiled with
+        # --warmup 0 every launch is a timed Newmark step's, so iterations per launch = the line's PCG iterations /
+        # steps, and the figures bench.py prices per iteration are the per-launch ones divided by that
+        for k, v in sel.items():
+            if k.startswith("k_pcg_resident") and bench and bench.get("warmup") == 0 and bench.get("steps"):
+                ipl = bench["pcg_iterations"] / bench["steps"]
+                v["iterations_per_launch"] = ipl
+                v["avg_ns_per_iteration"] = v["avg_ns"] / ipl
+                if v["hbm_bytes_per_launch"] is not None:
+                    v["hbm_bytes_per_launch"] /= ipl
+                    v["read_bytes"] /= ipl
+                    v["write_bytes"] /= ipl
+                note += "; k_pcg_resident: per PCG iteration (one launch = one solve of iterations_per_launch)"
+        total = sum(v["hbm_bytes_per_launch"] or 0 for v in sel.values())
+        json.dump(dict(kernels=sel, hbm_bytes_per_launch=total, source_hash=src_hash, note=note), open(a.json, "w"),
+                  indent=1)
 
 
 if __name__ == "__main__":
