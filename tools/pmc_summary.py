@@ -72,7 +72,7 @@ def main():
         # --warmup 0 every launch is a timed Newmark step's, so iterations per launch = the line's PCG iterations /
         # steps, and the figures bench.py prices per iteration are the per-launch ones divided by that
         for k, v in sel.items():
-            if k.startswith("k_pcg_resident") and bench and bench.get("warmup") == 0 and bench.get("steps"):
+            if norm(k).startswith("k_pcg_resident") and bench and bench.get("warmup") == 0 and bench.get("steps"):
                 ipl = bench["pcg_iterations"] / bench["steps"]
                 v["iterations_per_launch"] = ipl
                 v["avg_ns_per_iteration"] = v["avg_ns"] / ipl
