@@ -1437,8 +1437,8 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
     if (t.lat && fast_fused(h) && !h->sharded() && resident_ready(const_cast<cwf_hip_system *>(h)))
     {  // the resident solve's one launch per solve (resident.hip)
         static thread_local char name[96];
-        snprintf(name, sizeof name, "k_pcg_resident<%s, %s, 3, 2>", t.lsym ? "true" : "false",
-                 t.lhex ? "LatHex" : "LatKuhn");
+        snprintf(name, sizeof name, "k_pcg_resident<%s, %s, %u, %u>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", h->res.npt, h->res.nph);
         return name;
     }
     if (t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration's one launch (lattice_fused.inc)

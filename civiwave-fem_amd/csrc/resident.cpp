@@ -6,7 +6,7 @@
 // Box choice: every factorisation gx * gy * gz <= CUs of the node lattice, boxes of ceil(n / g) nodes per axis at most,
 // scored by the per-workgroup work of a phase (own nodes + 1.5 x halo entries, each halo entry being three 16-B
 // loads and a formed p) plus a barrier term growing with the grid (2 per workgroup); the image (box + ring, float4)
-// must fit the LDS beside the static tables and the lists the kernel's 3 + 2 entries per thread. C2 (70^3 nodes): 5 x 7 x 7 boxes of
+// must fit the LDS beside the static tables and the lists the kernel's 4 + 3 entries per thread. C2 (70^3 nodes): 5 x 7 x 7 boxes of
 // 14 x 10 x 10 nodes, 245 workgroups.
 #include <algorithm>
 #include <cstring>
@@ -17,10 +17,11 @@ namespace cwf
 {
 namespace
 {
-constexpr unsigned kResThreads = 512, kResOwn = 3 * kResThreads, kResHalo = 2 * kResThreads;  // resident.hip
-// the box image's float4 slots within 64 KB of LDS beside the kernel's static arrays (the class table, the boundary
-// types' stencils: 25 KB with the 15-offset Kuhn stencil, 40.5 KB with the 27-offset hex8 one)
-constexpr unsigned kResMaxSlotsKuhn = 2450, kResMaxSlotsHex = 1450;
+constexpr unsigned kResThreads = 512, kResOwn = 4 * kResThreads, kResHalo = 3 * kResThreads;  // resident.hip
+// the box image's float4 slots within the 160 KB of LDS a gfx950 workgroup may hold, beside the kernel's static
+// arrays (the own entries' r, Ap, x: 72 KB; the class table and the boundary types' stencils: 25 KB with the
+// 15-offset Kuhn stencil, 40.5 KB with the 27-offset hex8 one)
+constexpr unsigned kResMaxSlotsKuhn = 3800, kResMaxSlotsHex = 2800;  // (the register-state instantiation has 72 KB more)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr unsigned kFusedSharesHost = 5;  // kFusedShares (lattice_common.hpp): one 16-B granule each
 
@@ -174,7 +175,8 @@ bool resident_ready(cwf_hip_system *h)
     const unsigned npt = (max_own + kResThreads - 1) / kResThreads, nph = (max_halo + kResThreads - 1) / kResThreads;
     if (max_own > kResOwn || max_halo > kResHalo || max_slots > kResMaxSlots)
         return false;
-    const unsigned own_stride = kResOwn, halo_stride = kResHalo;
+    const bool small = npt <= 3 && nph <= 2;
+    const unsigned own_stride = (small ? 3u : 4u) * kResThreads, halo_stride = (small ? 2u : 3u) * kResThreads;
     const size_t lds = max_slots * 16;
     // one workgroup per CU at least (the grid waits for all of them every phase)
     if (resident_blocks_per_cu(h->ds, npt, nph, lds) < 1)
@@ -238,8 +240,8 @@ bool resident_ready(cwf_hip_system *h)
         hipMemset(dpub, 0, 2ull * 12 * std::max<uint32_t>(npub, 1u) * sizeof(float)) != hipSuccess)
         return false;
     rp.G = G;
-    rp.npt = npt;
-    rp.nph = nph;
+    rp.npt = npt <= 3 && nph <= 2 ? 3 : 4;  // the instantiation (resident.hip)
+    rp.nph = npt <= 3 && nph <= 2 ? 2 : 3;
     rp.own_stride = own_stride;
     rp.halo_stride = halo_stride;
     rp.npub = std::max<uint32_t>(npub, 1u);

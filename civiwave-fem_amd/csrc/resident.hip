@@ -38,7 +38,7 @@ namespace cwf
 {
 namespace
 {
-constexpr int kResNT = 512, kResNPT = 3, kResNPH = 2;  // threads; own / ring entries per thread
+constexpr int kResNT = 512;
 constexpr uint32_t kResMaxRounds = 4000000u;  // poll rounds before a phase gives up (>= 4 s: a round is >= 1 us)
 constexpr uint32_t kResNone = 0xFFFFFFFFu;
 constexpr uint32_t kResOob = 0xFFFFFF00u;  // a byte offset past every range-checked buffer here, +32 included (no wrap)
@@ -85,7 +85,8 @@ __device__ __forceinline__ void lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// block_sum_k's fixed order (wave sums, then the waves in order) over lds_sync
+// block_sum_k's fixed order (wave sums, then the waves in order) over lds_sync. No trailing barrier: each caller's next
+// write of `red` is behind other workgroup barriers of the phase (the halo vote / image barrier, the next phase's polls)
 template <int NT, int K>
 __device__ __forceinline__ void block_sum_lds(double v[K], double *red)
 {
@@ -106,7 +107,6 @@ __device__ __forceinline__ void block_sum_lds(double v[K], double *red)
             t += red[K * w + q];
         v[q] = t;
     }
-    lds_sync();
 }
 
 template <bool SYM, class E, int NPT, int NPH>
@@ -118,6 +118,18 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     __shared__ float2 czB[kLatClasses];
     __shared__ float4 tcf[27 * E::nOff * 3];  // the boundary types' stencils (type 13, the interior, unused)
     __shared__ int vote[3];  // the poll rounds' workgroup vote, by round mod 3
+    // the own entries' r, Ap, x and p: in registers for boxes of <= 3 nodes per thread (C2's 14 x 10 x 10), else
+    // (LST) r, Ap, x in LDS (lane-linear: conflict-free) and p in the image (each slot formed by one thread), so 4
+    // nodes per thread fit without spilling (the C3 / 8 slab's 19 x 19 x 5; LDS state cost C2 0.9 us per phase)
+    constexpr bool LST = NPT > 3;
+    __shared__ float st[LST ? 9 : 1][LST ? NPT * kResNT : 1];
+    float sreg[LST ? 1 : NPT][LST ? 1 : 12];  // r, Ap, x, p
+    const auto S = [&](int u, int q) -> float & {  // q: 0-2 r, 3-5 Ap, 6-8 x (9-11 p: registers only)
+        if constexpr (LST)
+            return st[q][threadIdx.x + (uint32_t)u * kResNT];
+        else
+            return sreg[u][q];
+    };
     const DevTiles &T = s.t;
     const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
     const uint4 hd = ra.hdr[b];
@@ -143,38 +155,39 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const __amdgpu_buffer_rsrc_t rx = sized_rsrc(ra.x, vbytes), rr = sized_rsrc(ra.r, vbytes),
                                  rcls = sized_rsrc(T.lcls, s.N), rmass = sized_rsrc(s.mass, 4u * s.N),
                                  rpub = sized_rsrc(ra.pub, 96u * ra.npub), rsh = sized_rsrc(ra.sh, 160u * G);
-    // own nodes: their state for the whole solve
-    uint32_t on[NPT], oslot[NPT], opub[NPT], oc[NPT];
-    float r[NPT][3], a[NPT][3], p[NPT][3], x[NPT][3], z[NPT][3], m[NPT];
+    // own nodes: their r, Ap, x in LDS (st), p in the image, for the whole solve; in registers only the node, its
+    // image slot and class, publication index and mass (4 per node: 4 nodes per thread fit without spilling)
+    uint32_t on[NPT], osc[NPT], opub[NPT];  // node; image slot | class << 16; publication index
+    float m[NPT];
 #pragma unroll
     for (int u = 0; u < NPT; ++u)
     {
-        const uint4 e = ra.own[(size_t)b * ra.own_stride + tid + (uint32_t)u * kResNT];
+        const uint32_t e0 = tid + (uint32_t)u * kResNT;
+        const uint4 e = ra.own[(size_t)b * ra.own_stride + e0];
         on[u] = e.x;
-        oslot[u] = e.y & 0xFFFFu;
         opub[u] = e.z;
         const bool v = e.x != kResNone;
         const uint32_t nb = v ? 12u * e.x : 12u * kLatOob3;
         const u32x3 wr = __builtin_amdgcn_raw_buffer_load_b96(rr, nb, 0, 0),
                     wx = __builtin_amdgcn_raw_buffer_load_b96(rx, nb, 0, 0);
-        r[u][0] = __uint_as_float(wr.x), r[u][1] = __uint_as_float(wr.y), r[u][2] = __uint_as_float(wr.z);
-        x[u][0] = __uint_as_float(wx.x), x[u][1] = __uint_as_float(wx.y), x[u][2] = __uint_as_float(wx.z);
-        oc[u] = __builtin_amdgcn_raw_buffer_load_b8(rcls, v ? e.x : kResNone, 0, 0);
+        S(u, 0) = __uint_as_float(wr.x), S(u, 1) = __uint_as_float(wr.y), S(u, 2) = __uint_as_float(wr.z);
+        S(u, 3) = S(u, 4) = S(u, 5) = 0.f;
+        S(u, 6) = __uint_as_float(wx.x), S(u, 7) = __uint_as_float(wx.y), S(u, 8) = __uint_as_float(wx.z);
+        if constexpr (!LST)
+            sreg[u][9] = sreg[u][10] = sreg[u][11] = 0.f;
+        osc[u] = (e.y & 0xFFFFu) | (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rcls, v ? e.x : kResNone, 0, 0) << 16;
         m[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmass, v ? 4u * e.x : 4u * kLatOob1, 0, 0));
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            a[u][c] = p[u][c] = z[u][c] = 0.f;
     }
     // halo entries: their owners' records
-    uint32_t hn[NPH], hslot[NPH], hpub[NPH], hc[NPH];
+    uint32_t hn[NPH], hsc[NPH], hpub[NPH];  // node; image slot | class << 16; the owner's publication index
 #pragma unroll
     for (int h = 0; h < NPH; ++h)
     {
         const uint4 e = ra.halo[(size_t)b * ra.halo_stride + tid + (uint32_t)h * kResNT];
         hn[h] = e.x;
-        hslot[h] = e.y;
         hpub[h] = e.z;
-        hc[h] = __builtin_amdgcn_raw_buffer_load_b8(rcls, e.x != kResNone ? e.x : kResNone, 0, 0);
+        hsc[h] = e.y | (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rcls, e.x != kResNone ? e.x : kResNone, 0, 0)
+                           << 16;
     }
     const CtlPre pre = ctl_prefetch(ra.ctl, 1u);  // tol and active (set by fast_fused_init)
     // the node's neighbours in the image (workgroup-uniform)
@@ -267,6 +280,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             for (int q = 0; q < kFusedShares; ++q)
                 v[q] = tid < G ? __hiloint2double((int)g[q].y, (int)g[q].x) : 0.0;
             block_sum_lds<kResNT, kFusedShares>(v, red);  // fixed order: every workgroup the same totals
+            stamp(j, 7);
             go = fused_decide(ra.ctl, ra.hist, j, pre, v, &alpha, &beta);
             if (go && j - 1u == ra.max_it)  // max_iterations updates made (the host loop's last launch)
                 go = false;
@@ -278,10 +292,10 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         // opaque per phase, so no address derived from them is hoisted out of the phase loop into a VGPR
 #pragma unroll
         for (int u = 0; u < NPT; ++u)
-            asm volatile("" : "+v"(oslot[u]), "+v"(opub[u]));
+            asm volatile("" : "+v"(osc[u]), "+v"(opub[u]), "+v"(on[u]));
 #pragma unroll
         for (int h = 0; h < NPH; ++h)
-            asm volatile("" : "+v"(hslot[h]), "+v"(hpub[h]), "+v"(hn[h]));
+            asm volatile("" : "+v"(hsc[h]), "+v"(hpub[h]), "+v"(hn[h]));
         double d[kFusedShares] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int u = 0; u < NPT; ++u)
@@ -289,17 +303,22 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             __builtin_amdgcn_sched_barrier(0);  // one node's working set at a time (no cross-node hoisting)
             if (on[u] == kResNone)
                 continue;
+            const uint32_t e0 = tid + (uint32_t)u * kResNT, slot = osc[u] & 0xFFFFu;
+            // p_(j-1): this thread formed it last phase (0 at phase 0)
+            const float4 po = LST ? pl[slot] : float4{S(u, 9), S(u, 10), S(u, 11), 0.f};
+            const float rr0[3] = {S(u, 0), S(u, 1), S(u, 2)}, aa0[3] = {S(u, 3), S(u, 4), S(u, 5)},
+                        pp0[3] = {po.x, po.y, po.z};
             float rn[3], zz[3], pn[3];
-            fused_form(czA, czB, oc[u], alpha, beta, r[u], a[u], p[u], rn, zz, pn);
+            fused_form(czA, czB, osc[u] >> 16, alpha, beta, rr0, aa0, pp0, rn, zz, pn);
 #pragma unroll
             for (int c = 0; c < 3; ++c)
             {
-                x[u][c] = fmaf(alpha, p[u][c], x[u][c]);
-                r[u][c] = rn[c];
-                z[u][c] = zz[c];
-                p[u][c] = pn[c];
+                S(u, 6 + c) = fmaf(alpha, pp0[c], S(u, 6 + c));  // x_j = x_(j-1) + alpha_(j-1) p_(j-1)
+                S(u, c) = rn[c];
+                if constexpr (!LST)
+                    S(u, 9 + c) = pn[c];
             }
-            pl[oslot[u]] = float4{pn[0], pn[1], pn[2], 0.f};
+            pl[slot] = float4{pn[0], pn[1], pn[2], 0.f};
             fused_entry_dots(rn, zz, d);
         }
         // the halo's p_j: phase 0 from fast_fused_init's r; later phases from the records requested above, each
@@ -327,10 +346,15 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     hp[h][2] = __uint_as_float(w2[h].z);
                 }
                 float rn[3], zz[3], pn[3];
-                fused_form(czA, czB, hc[h], alpha, beta, hr[h], ha[h], hp[h], rn, zz, pn);
-                pl[hslot[h]] = float4{pn[0], pn[1], pn[2], 0.f};
+                fused_form(czA, czB, hsc[h] >> 16, alpha, beta, hr[h], ha[h], hp[h], rn, zz, pn);
+                pl[hsc[h] & 0xFFFFu] = float4{pn[0], pn[1], pn[2], 0.f};
             }
-            if (j == 0 || all_ok(hok))
+            if (j == 0)
+            {
+                lds_sync();  // the image complete before the rows
+                break;
+            }
+            if (all_ok(hok))  // (its barrier also completes the image: the own entries were written before it)
                 break;
             if (round >= kResMaxRounds)
             {
@@ -346,7 +370,6 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 w2[h] = ld4_sc1(rpub, po + 32u);
             }
         }
-        lds_sync();
         stamp(j, 3);
         // rows: Ap_j = K_eff p_j, the dots of the row, the box-surface records for the neighbours' next phase
 #pragma unroll
@@ -355,12 +378,14 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             __builtin_amdgcn_sched_barrier(0);  // one row's LDS reads in flight at a time (VGPRs)
             if (on[u] == kResNone)
                 continue;
-            int c0 = (int)oslot[u];
+            int c0 = (int)(osc[u] & 0xFFFFu);
             asm volatile("" : "+v"(c0));  // opaque per phase: the rows' image addresses are not hoisted out of the phase
                                           // loop (56 loop-invariant addresses would pin as many VGPRs)
-            const float u0[3] = {p[u][0], p[u][1], p[u][2]};
+            const uint32_t e0 = tid + (uint32_t)u * kResNT;
+            const float4 q0 = LST ? pl[c0] : float4{S(u, 9), S(u, 10), S(u, 11), 0.f};
+            const float u0[3] = {q0.x, q0.y, q0.z};
             float acc[3];
-            const uint32_t ty = oc[u] >> 3;  // boundary type (lo / inside / hi along x, y, z)
+            const uint32_t cls = osc[u] >> 16, ty = cls >> 3;  // boundary type (lo / inside / hi along x, y, z)
             if (ty != 13u)  // a block-surface node: its type's stencil (the cell form's pair blocks of the cells that
             {               // exist, summed per offset at plan time), every offset on its own
                 const float4 *tb = tcf + ty * (uint32_t)(E::nOff * 3);
@@ -428,11 +453,14 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 an[c] = fmaf(mm, u0[c], sK * acc[c]);
 #pragma unroll
             for (int c = 0; c < 3; ++c)
-                a[u][c] = an[c];
-            fused_row_dots(czA, czB, oc[u], u0, z[u], an, d);
+                S(u, 3 + c) = an[c];
+            const float rj[3] = {S(u, 0), S(u, 1), S(u, 2)};
+            float zz[3];  // z_j again from r_j (the form's arithmetic: the same bits)
+            lat_z(czA[cls], czB[cls], cls, rj, zz);
+            fused_row_dots(czA, czB, cls, u0, zz, an, d);
             const uint32_t po = opub[u] != kResNone ? 48u * ((j & 1u) * ra.npub + opub[u]) : kResOob;
             const uint32_t tag = ra.tag0 + j + 1u;
-            st4_sc1(rpub, po, u32x4{__float_as_uint(r[u][0]), __float_as_uint(r[u][1]), __float_as_uint(r[u][2]), tag});
+            st4_sc1(rpub, po, u32x4{__float_as_uint(rj[0]), __float_as_uint(rj[1]), __float_as_uint(rj[2]), tag});
             st4_sc1(rpub, po + 16u, u32x4{__float_as_uint(an[0]), __float_as_uint(an[1]), __float_as_uint(an[2]), tag});
             st4_sc1(rpub, po + 32u, u32x4{__float_as_uint(u0[0]), __float_as_uint(u0[1]), __float_as_uint(u0[2]), tag});
         }
@@ -455,9 +483,9 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
     for (int u = 0; u < NPT; ++u)
     {
-        const uint32_t nb = on[u] != kResNone ? 12u * on[u] : 12u * kLatOob3;
-        const u32x3 vx = {__float_as_uint(x[u][0]), __float_as_uint(x[u][1]), __float_as_uint(x[u][2])},
-                    vr = {__float_as_uint(r[u][0]), __float_as_uint(r[u][1]), __float_as_uint(r[u][2])};
+        const uint32_t nb = on[u] != kResNone ? 12u * on[u] : 12u * kLatOob3, e0 = tid + (uint32_t)u * kResNT;
+        const u32x3 vx = {__float_as_uint(S(u, 6)), __float_as_uint(S(u, 7)), __float_as_uint(S(u, 8))},
+                    vr = {__float_as_uint(S(u, 0)), __float_as_uint(S(u, 1)), __float_as_uint(S(u, 2))};
         __builtin_amdgcn_raw_buffer_store_b96(vx, wx, nb, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b96(vr, wr, nb, 0, 0);
     }
@@ -493,18 +521,24 @@ int res_bpc(const DevSys &s, size_t lds)
     const auto k = s.t.lhex ? (s.t.lsym ? k_pcg_resident<true, LatHex, NPT, NPH> : k_pcg_resident<false, LatHex, NPT, NPH>)
                             : (s.t.lsym ? k_pcg_resident<true, LatKuhn, NPT, NPH>
                                         : k_pcg_resident<false, LatKuhn, NPT, NPH>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k, kResNT, lds) != hipSuccess)
+    // the image is dynamic LDS beside ~100 KB of static arrays: allow the workgroup its size (gfx950: 160 KB)
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k, kResNT, lds) != hipSuccess)
         return 0;
     return bpc;
 }
 }  // namespace
 
 // ---- the resident solve (the kernel above): one launch per PCG solve ------------------------------------------------
-// the instantiation: <= 3 own + 2 halo entries per thread (boxes of <= 1,536 nodes and <= 1,024 ring entries; 234-238
-// VGPRs, no scratch: 2 waves per SIMD, one workgroup per CU). A 4 + 4 form spilled 144-172 B per lane.
+// the instantiations: <= 3 own + 2 halo entries per thread, state in registers (boxes of <= 1,536 nodes and <= 1,024
+// ring entries: C2's 14 x 10 x 10), or <= 4 + 3 with the state in LDS (<= 2,048 nodes, <= 1,536 entries: the C3 / 8
+// slab's 19 x 19 x 5); 2 waves per SIMD, one workgroup per CU, no scratch
 int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds)
 {
-    return npt <= kResNPT && nph <= kResNPH ? res_bpc<kResNPT, kResNPH>(s, lds) : 0;
+    if (npt <= 3 && nph <= 2)
+        return res_bpc<3, 2>(s, lds);
+    return npt <= 4 && nph <= 3 ? res_bpc<4, 3>(s, lds) : 0;
 }
 
 void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
@@ -543,7 +577,10 @@ void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hip
         ra.trace_j = at ? (uint32_t)atoi(at) : 50u;
         (void)hipMemsetAsync(trace, 0, 64ull * rp.G, st);
     }
-    launch_resident_n<kResNPT, kResNPH>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
+    if (rp.npt <= 3 && rp.nph <= 2)
+        launch_resident_n<3, 2>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
+    else
+        launch_resident_n<4, 3>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
     if (tp && trace)
     {
         std::vector<uint64_t> v(8ull * rp.G);
@@ -556,7 +593,7 @@ void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hip
                 for (unsigned b = 0; b < rp.G; ++b)
                 {
                     std::fprintf(f, "%u", b);
-                    for (int i = 0; i < 7; ++i)
+                    for (int i = 0; i < 8; ++i)
                         std::fprintf(f, " %llu", (unsigned long long)v[8ull * b + i]);
                     std::fprintf(f, "\n");
                 }

@@ -23,7 +23,8 @@ def main():
 
     case = scenarios.block_case(nx, ny, nz, h=0.1, tol=1e-30, max_iterations=its)
     rhs = case.static_rhs()
-    for fused in ("resident", "1", "0"):
+    # BLK_SCHEDULES=resident,1,0 (a comma list) limits the schedules (same-box A/B of library builds: CWF_LIB_PATH)
+    for fused in os.environ.get("BLK_SCHEDULES", "resident,1,0").split(","):
         if fused == "resident":
             os.environ.pop("CWF_FUSED", None)
         else:

@@ -29,12 +29,15 @@ def main():
     B = bs[int(sys.argv[2]) if len(sys.argv) > 2 else -1]
     a = np.array(B["rows"], np.int64)
     t = a[:, 1:8].astype(np.float64) * 0.01  # us
+    fold = (a[:, 8] - a[:, 2]).astype(np.float64) * 0.01 if a.shape[1] > 8 else None  # stamp 7: the fold done
     t -= t[:, 0].min()
     names = ["poll", "fold+decide", "form", "rows", "reduce", "shares"]
     print(f"{B['hdr']}: {len(a)} workgroups")
     for i, n in enumerate(names):
         d = t[:, i + 1] - t[:, i]
         print(f"  {n:12s} median {np.median(d):6.2f}  max {d.max():6.2f} us")
+    if fold is not None and np.all(a[:, 8] > 0):
+        print(f"  (fold alone median {np.median(fold):.2f} max {fold.max():.2f} us; decide the rest)")
     print(f"  phase start spread {t[:, 0].max() - t[:, 0].min():.2f} us, release (wait done) spread "
           f"{t[:, 1].max() - t[:, 1].min():.2f} us, last end {t[:, 6].max():.2f} us after the first start, "
           f"compute (release -> end) median {np.median(t[:, 6] - t[:, 1]):.2f} max {np.max(t[:, 6] - t[:, 1]):.2f}")
