@@ -451,7 +451,8 @@ def main():
     D = owned_dofs
     local = np.array([elapsed, D * total_iters, total_iters, D], np.float64)
     # the PCG schedule the ranks agreed on (cwf_hip_system_exchange_schedule): 0 two kernels + two exchange steps,
-    # 1 fused + one exchange step, 2 fused with the exchange inside the launch (PEER)
+    # 1 fused + one exchange step, 2 fused with the exchange inside the launch (PEER), 3 the resident solve (PEER
+    # slab shards: one launch per solve)
     sched = int(L.cwf_hip_system_exchange_schedule(h)) if world > 1 else None
     per_rank = [{"owned_dofs": int(D), "local_tets": int(local_tets), "halo_nodes": int(halo_nodes),
                  "halo_bytes_per_exchange": 12 * int(halo_nodes), "seconds": elapsed, "schedule": sched}]

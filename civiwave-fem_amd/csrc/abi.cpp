@@ -1366,7 +1366,7 @@ int cwf_hip_system_keff_traffic(const cwf_hip_system *h, uint64_t *layout_bytes,
         // hex8: 16-B corner ids + 16-B positions per hex (no material stream for one material)
         // fan groups: 16-B group record (ids, push ranks, tet count, material) instead of the per-tet records
         const uint64_t rec = s.t.hex ? 32 : s.t.geo ? 16 : 56;
-        if (s.t.lat && fast_fused(h) && !h->sharded() && resident_ready(const_cast<cwf_hip_system *>(h)))
+        if (s.t.lat && fast_fused(h) && resident_on(h))
         {  // the resident solve (resident.hip), per iteration: only what crosses a CU -- the halo records read, the
            // box-surface records and the shares written, the G x 5 shares read -- the vectors stay on chip
             *layout_bytes = resident_offchip_bytes(h);
@@ -1416,7 +1416,7 @@ int cwf_hip_system_exchange_schedule(const cwf_hip_system *h)
 {
     if (!h || !h->sharded() || h->fused_agreed < 0)
         return -1;
-    return h->fused_agreed == 0 ? 0 : h->px_agreed == 1 ? 2 : 1;
+    return h->fused_agreed == 0 ? 0 : h->res_agreed == 1 ? 3 : h->px_agreed == 1 ? 2 : 1;
 }
 
 const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
@@ -1434,11 +1434,11 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h)
             return h->ds.iso ? "k_keff_parity_tile<true, false, false, true>" : "k_keff_parity_tile<false, false, false, true>";
         return h->ds.iso ? "k_keff_parity_tile<true, false, true, false>" : "k_keff_parity_tile<false, false, true, false>";
     }
-    if (t.lat && fast_fused(h) && !h->sharded() && resident_ready(const_cast<cwf_hip_system *>(h)))
+    if (t.lat && fast_fused(h) && resident_on(h))
     {  // the resident solve's one launch per solve (resident.hip)
         static thread_local char name[96];
-        snprintf(name, sizeof name, "k_pcg_resident<%s, %s, %u, %u>", t.lsym ? "true" : "false",
-                 t.lhex ? "LatHex" : "LatKuhn", h->res.npt, h->res.nph);
+        snprintf(name, sizeof name, "k_pcg_resident<%s, %s, %u, %u, %s>", t.lsym ? "true" : "false",
+                 t.lhex ? "LatHex" : "LatKuhn", h->res.npt, h->res.nph, h->res.shard ? "true" : "false");
         return name;
     }
     if (t.lat && fast_fused(h) && h->fused_agreed != 0)  // the fused iteration's one launch (lattice_fused.inc)

@@ -71,11 +71,19 @@ int pcg_finish(const std::vector<cwf_hip_system *> &g, cwf_pcg_telemetry *tel)
 
 // the resident solve: fast_fused_init (block inverse, r_0, norms, tolerance), then ONE launch that runs every
 // iteration on chip (resident.hip) and leaves x, r and the control block; hipEvent-timed as a whole when timing is on
-// (the handle's K_eff timing then counts its iterations: avg = the time per iteration)
+// (the handle's K_eff timing then counts its iterations: avg = the time per iteration). A PEER slab shard (one member
+// per process): the sharded prologue instead of fast_fused_init, ghost x from the owners after the solve
 int run_pcg_resident(cwf_hip_system *h, const float *rhs, const cwf_pcg_settings &set, cwf_pcg_telemetry *tel)
 {
     hipStream_t st = h->stream;
-    fast_fused_init(h, rhs, set.relative_tolerance, st, false);
+    const bool shard = h->sharded();
+    if (shard)
+    {
+        if (int e = sharded_resident_init({h}, {rhs}, set.relative_tolerance))
+            return e;
+    }
+    else
+        fast_fused_init(h, rhs, set.relative_tolerance, st, false);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->timing)
     {
@@ -96,6 +104,12 @@ int run_pcg_resident(cwf_hip_system *h, const float *rhs, const cwf_pcg_settings
     HIPTRY(h, hipGetLastError());
     HIPTRY(h, hipMemcpyAsync(h->ctl_host, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st));
     HIPTRY(h, hipStreamSynchronize(st));
+    if (shard && !h->ctl_host->error)  // ghost x <- owners (the stepper's node-wise updates read the ghost rows too)
+    {
+        if (int e = comm_halo({h}, &cwf_hip_system::x))
+            return e;
+        HIPTRY(h, hipStreamSynchronize(st));
+    }
     if (e0 && h->ctl_host->iterations)
     {
         float ms = 0.f;
@@ -147,6 +161,8 @@ int run_pcg_group(const std::vector<cwf_hip_system *> &g, const std::vector<cons
     const bool fused = fast && (sharded ? gf == 1 : fast_fused(h));
     // a block that fits on chip: the whole solve in one launch (resident.hip)
     if (fused && !sharded && set.max_iterations <= (1u << 24) && resident_ready(h))
+        return run_pcg_resident(h, rhs[0], set, tel);
+    if (fused && sharded && g.size() == 1 && h->res_agreed == 1 && set.max_iterations <= (1u << 24))
         return run_pcg_resident(h, rhs[0], set, tel);
     if (fused && sharded)
     {

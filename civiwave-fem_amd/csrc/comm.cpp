@@ -309,11 +309,14 @@ int group_fused(const std::vector<cwf_hip_system *> &g)
     bool mine = true;
     for (cwf_hip_system *h : g)
         mine = mine && fast_fused(h) && h->ds.t.lat;
-    // and the exchange inside the launches (PEER: one member per process)
+    // and the exchange inside the launches (PEER: one member per process); and the resident solve (PEER: every
+    // iteration in one launch, resident.hip), whose tag base every rank then takes from the largest (the ranks'
+    // granules must carry the same tags)
     const bool px = mine && g.size() == 1 && peer_fused_eligible(h0);
+    const bool res = mine && g.size() == 1 && resident_shard_ready(h0);
     for (cwf_hip_system *h : g)
     {
-        const double v[2] = {mine ? 1.0 : 0.0, px ? 1.0 : 0.0};
+        const double v[2] = {mine ? 1.0 : 0.0, (px ? 1.0 : 0.0) + (res ? 2.0 : 0.0) + 4.0 * (double)h->res.tag};
         HIPTRY(h, hipMemcpyAsync(h->g_init + 2 * h->rank, v, sizeof v, hipMemcpyHostToDevice, h->stream));
         HIPTRY(h, hipStreamSynchronize(h->stream));
     }
@@ -324,16 +327,23 @@ int group_fused(const std::vector<cwf_hip_system *> &g)
     std::vector<double> f(2 * (size_t)h0->nranks, 0.0);
     HIPTRY(h0, hipStreamSynchronize(h0->stream));
     HIPTRY(h0, hipMemcpy(f.data(), h0->g_init, f.size() * sizeof(double), hipMemcpyDeviceToHost));
-    bool all = true, all_px = true;
+    bool all = true, all_px = true, all_res = true;
+    uint64_t tag = 0;
     for (int r = 0; r < h0->nranks; ++r)
     {
+        const uint64_t pv = (uint64_t)f[2 * (size_t)r + 1];
         all = all && f[2 * (size_t)r] == 1.0;
-        all_px = all_px && f[2 * (size_t)r + 1] == 1.0;
+        all_px = all_px && (pv & 1u);
+        all_res = all_res && (pv & 2u);
+        tag = std::max<uint64_t>(tag, pv >> 2);
     }
     for (cwf_hip_system *h : g)
     {
         h->fused_agreed = all ? 1 : 0;
         h->px_agreed = all && all_px ? 1 : 0;
+        h->res_agreed = all && all_res ? 1 : 0;
+        if (h->res_agreed)
+            h->res.tag = (uint32_t)tag;
     }
     return all ? 1 : 0;
 }
@@ -361,7 +371,12 @@ int fused_exchange(const std::vector<cwf_hip_system *> &g, unsigned j)
 }
 }  // namespace
 
-int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+namespace
+{
+// the fused and resident schedules' prologue: block inverse, the ghosts' global classes (once), ghost x, r_0 and the
+// gathered norms, the tolerance, r_0's ghost rows (the first launch forms the ghosts' p_0 from them)
+int sharded_fused_prologue(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs,
+                           double rel_tol)
 {
     for (cwf_hip_system *h : g)
         fast_block_inverse(h, h->stream);
@@ -393,7 +408,13 @@ int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector
         return st;
     for (cwf_hip_system *h : g)
         fast_init_scalars_strided(h, h->g_init, h->g_init + 1, (uint32_t)h->nranks, 2u, rel_tol, h->stream);
-    if (int st = comm_halo(g, &cwf_hip_system::r))  // r_0's ghost rows (launch 0 forms ghost p_0 from them)
+    return comm_halo(g, &cwf_hip_system::r);
+}
+}  // namespace
+
+int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+{
+    if (int st = sharded_fused_prologue(g, rhs, rel_tol))
         return st;
     if (g[0]->px_agreed == 1)  // the launches exchange themselves: epochs from here
         if (int st = peer_fused_begin(g[0]))
@@ -401,6 +422,13 @@ int sharded_fused_init(const std::vector<cwf_hip_system *> &g, const std::vector
     for (cwf_hip_system *h : g)
         fast_fused_launch0(h, h->stream);
     return g[0]->px_agreed == 1 ? 0 : fused_exchange(g, 0);
+}
+
+// the resident solve of PEER slab shards (resident.hip): the prologue only; the one launch then runs every
+// iteration, its halo records and rank totals stored into the mailboxes by the kernel itself
+int sharded_resident_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol)
+{
+    return sharded_fused_prologue(g, rhs, rel_tol);
 }
 
 int sharded_fused_iteration(const std::vector<cwf_hip_system *> &g, unsigned it, hipEvent_t e0, hipEvent_t e1)
@@ -806,6 +834,11 @@ int cwf_hip_system_attach(cwf_hip_system *h, cwf_hip_comm *cm, int32_t rank, con
                 break;
             }
     h->pstride = 0;
+    {  // a resident plan made before the attach is the whole block's: re-planned for the shard (its tags go on)
+        const uint32_t tag = h->res.tag;
+        h->res = cwf::ResidentPlan{};
+        h->res.tag = tag;
+    }
     h->comm = cm;
     h->rank = rank;
     h->nranks = n;

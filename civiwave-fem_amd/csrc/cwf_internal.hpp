@@ -301,6 +301,8 @@ struct ResidentPlan
     float *pub = nullptr;
     double *sh = nullptr;
     uint32_t tag = 1;  // the next solve's granule tag base (resident.hip: phase j publishes tag + j + 1)
+    bool shard = false;         // a PEER slab shard: ghost records in the mailbox, rank totals across ranks
+    uint64_t remote_sends = 0;  // a shard: own records stored into the neighbours' mailboxes per phase
 };
 
 struct DevBuf
@@ -337,6 +339,7 @@ struct cwf_hip_system
     bool unusable = false;
     int fused_agreed = -1;    // a shard: every rank runs the fused iteration (1) or none (0); -1: not asked yet
     int px_agreed = 0;        // ... and exchanges inside its launches (PEER, every rank eligible)
+    int res_agreed = 0;       // ... and every rank runs the resident solve (PEER slab shards, every rank eligible)
     int32_t px_send_k[2] = {-1, -1};  // the lattice plane of each neighbour slot's send segment
     uint32_t px_ebase = 0;            // the communicator's epoch before the solve's launch 0
     unsigned fused_grid = 0, fused_items = 0;  // the fused launch's grid and the work items it was sized for
@@ -492,8 +495,13 @@ int group_fused(const std::vector<cwf_hip_system *> &g);  // 1 fused, 0 two-kern
 // = 0 turns it off), the launch (fast_fused_init has run; one launch runs every iteration) and its residency query
 bool resident_ready(cwf_hip_system *h);
 void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
-int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds);
+int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds, bool shard);
 uint64_t resident_offchip_bytes(const cwf_hip_system *h);  // per phase: halo records read, surface records and shares
+// a PEER slab shard's resident solve: planned on the rank's own at the schedule vote (group_fused), run only when every
+// rank planned one (res_agreed); the init is the fused one's without its launch 0 and exchange step (comm.cpp)
+bool resident_shard_ready(cwf_hip_system *h);
+bool resident_on(const cwf_hip_system *h);  // the handle's FAST solves run the resident solve (planned and agreed)
+int sharded_resident_init(const std::vector<cwf_hip_system *> &g, const std::vector<const float *> &rhs, double rel_tol);
 int sharded_fused_end(const std::vector<cwf_hip_system *> &g);  // after the last launch (PEER in-kernel epochs)
 
 unsigned fast_tile_blocks(const DevSys &s);
@@ -559,6 +567,23 @@ void peer_fused_args(const cwf_hip_system *h, unsigned j, FusedPeerArgs &pe, con
 int peer_fused_begin(cwf_hip_system *h);  // before launch 0: the epoch base; the launch ticket cleared
 int peer_fused_end(cwf_hip_system *h);    // after the solve: the communicator's epoch = the last launch that pushed
 unsigned pcg_lattice_resident_count(const DevSys &s);  // resident workgroups of the fused launch
+// the resident solve of a PEER slab shard (resident.hip): where its cross-rank granules go and come from. Each mailbox
+// has a resident area by phase parity: the rank totals ([nranks][5] 16-B granules) and the ghost records ([nghost]
+// 48-B records, the ghosts' local order). Per neighbour slot e (the halo plan's k): the neighbour's record area at my
+// send segment; per rank p: p's rank-total area (my slot included)
+struct ResPeerArgs
+{
+    uint32_t nranks = 1, rank = 0;
+    float *rdst[2][2] = {};          // [e][parity] neighbour e's ghost records of my segment
+    uint32_t rdst_bytes[2] = {};     // 48 x my segment for e
+    const float *grecv[2] = {};      // [parity] my ghost records (written by the neighbours)
+    uint32_t grecv_bytes = 0;
+    uint32_t *tot[kMaxPeers][2] = {};  // [p][parity] rank p's rank-total area (granule (r, q) at 16 (5 r + q))
+    const uint32_t *tot_mine[2] = {};  // [parity] my rank-total area
+};
+size_t peer_resident_bytes(int nranks, uint64_t nghost);  // the resident area, both parities (peer_attach adds it)
+void peer_resident_args(const cwf_hip_system *h, ResPeerArgs &pa);
+int peer_resident_clear(cwf_hip_system *h);  // tags 0 in this rank's resident area (before any resident solve)
 int comm_exchange_vecs(const std::vector<cwf_hip_system *> &g, std::initializer_list<Gather> gathers,
                        const std::vector<std::vector<float *>> &vecs);
 int comm_allgather(const std::vector<cwf_hip_system *> &g, double *cwf_hip_system::*buf, size_t count);

@@ -81,6 +81,10 @@ inline size_t off_gath(int n) { return align256(off_flags() + kFlagLine * (size_
 inline size_t gath_bytes(int n) { return (size_t)kMaxPeerGathers * n * kSlot * sizeof(double); }  // one parity
 inline size_t off_recv(int n) { return align256(off_gath(n) + 2 * gath_bytes(n)); }
 inline size_t recv_bytes(uint64_t nghost) { return kMaxHaloVecs * 3 * nghost * sizeof(float); }  // one parity
+// the resident solve's area after the receive areas (resident.hip): per parity the rank totals, then the ghost records
+inline size_t off_res(int n, uint64_t nghost) { return align256(off_recv(n) + 2 * recv_bytes(nghost)); }
+inline size_t res_tot_bytes(int n) { return align256(80ull * (size_t)n); }
+inline size_t res_par_bytes(int n, uint64_t nghost) { return align256(res_tot_bytes(n) + 48ull * nghost); }
 
 struct PeerStep
 {
@@ -306,7 +310,7 @@ int peer_attach(cwf_hip_system *h)
     cwf_hip_comm *cm = h->comm;
     const int n = cm->nranks;
     const uint64_t nghost = h->ds.N - h->ds.Nown;
-    const size_t bytes = off_recv(n) + 2 * recv_bytes(nghost);
+    const size_t bytes = off_res(n, nghost) + 2 * res_par_bytes(n, nghost);
     if (int st = peer_alloc_mailbox(h, bytes))
         return st;
     cm->mbox_bytes = bytes;
@@ -504,6 +508,52 @@ void peer_fused_args(const cwf_hip_system *h, unsigned j, FusedPeerArgs &pe, con
     pe.rank = (uint32_t)h->rank;
     // gather 0 of the previous epoch: rank p's totals at [kSlot p]
     *gath_prev = reinterpret_cast<const double *>(static_cast<char *>(cm->mbox) + off_gath(n) + prev * gath_bytes(n));
+}
+
+size_t peer_resident_bytes(int nranks, uint64_t nghost) { return 2 * res_par_bytes(nranks, nghost); }
+
+int peer_resident_clear(cwf_hip_system *h)
+{
+    const cwf_hip_comm *cm = h->comm;
+    const uint64_t nghost = h->ds.N - h->ds.Nown;
+    char *base = static_cast<char *>(cm->mbox) + off_res(cm->nranks, nghost);
+    HIPTRY(h, hipMemset(base, 0, peer_resident_bytes(cm->nranks, nghost)));
+    return 0;
+}
+
+void peer_resident_args(const cwf_hip_system *h, ResPeerArgs &pa)
+{
+    const cwf_hip_comm *cm = h->comm;
+    const int n = cm->nranks;
+    pa = ResPeerArgs{};
+    pa.nranks = (uint32_t)n;
+    pa.rank = (uint32_t)h->rank;
+    const uint64_t nghost = h->ds.N - h->ds.Nown;
+    for (size_t k = 0; k < 2 && k < h->nbr.size(); ++k)
+    {
+        const int q = h->nbr[k];
+        const uint64_t qg = cm->peer_nghost[q], qoff = cm->peer_recv_off[q];
+        for (uint32_t par = 0; par < 2; ++par)
+        {
+            char *base = static_cast<char *>(cm->peer_mbox[q]) + off_res(n, qg) + par * res_par_bytes(n, qg) +
+                         res_tot_bytes(n);
+            pa.rdst[k][par] = reinterpret_cast<float *>(base + 48ull * qoff);
+        }
+        pa.rdst_bytes[k] = (uint32_t)(48ull * (h->send_off[k + 1] - h->send_off[k]));
+    }
+    for (uint32_t par = 0; par < 2; ++par)
+    {
+        const char *mine = static_cast<const char *>(cm->mbox) + off_res(n, nghost) + par * res_par_bytes(n, nghost);
+        pa.grecv[par] = reinterpret_cast<const float *>(mine + res_tot_bytes(n));
+        pa.tot_mine[par] = reinterpret_cast<const uint32_t *>(mine);
+        for (int p = 0; p < n; ++p)
+        {
+            const uint64_t pg = p == h->rank ? nghost : cm->peer_nghost[p];
+            char *pb = static_cast<char *>(p == h->rank ? cm->mbox : cm->peer_mbox[p]);
+            pa.tot[p][par] = reinterpret_cast<uint32_t *>(pb + off_res(n, pg) + par * res_par_bytes(n, pg));
+        }
+    }
+    pa.grecv_bytes = (uint32_t)(48ull * nghost);
 }
 
 int peer_fused_begin(cwf_hip_system *h)

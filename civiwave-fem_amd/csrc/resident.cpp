@@ -23,6 +23,7 @@ constexpr unsigned kResThreads = 512, kResOwn = 4 * kResThreads, kResHalo = 3 * 
 // 15-offset Kuhn stencil, 40.5 KB with the 27-offset hex8 one)
 constexpr unsigned kResMaxSlotsKuhn = 3800, kResMaxSlotsHex = 2800;  // (the register-state instantiation has 72 KB more)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kResGhost = 0x80000000u;  // a halo entry's source: a ghost record (resident.hip)
 constexpr unsigned kFusedSharesHost = 5;  // kFusedShares (lattice_common.hpp): one 16-B granule each
 
 void split(unsigned n, unsigned g, unsigned q, unsigned &a, unsigned &b)
@@ -32,33 +33,68 @@ void split(unsigned n, unsigned g, unsigned q, unsigned &a, unsigned &b)
 }
 }  // namespace
 
-bool resident_ready(cwf_hip_system *h)
+namespace
+{
+// the plan over the node planes [k0, k1) of the block (a PEER slab shard: its owned planes; the ghost planes beside
+// them are the halo entries' only other source, read from the mailbox). False: the solve keeps the other schedules
+bool plan_resident(cwf_hip_system *h, bool shard)
 {
     ResidentPlan &rp = h->res;
-    if (rp.state)
-        return rp.state > 0;
-    rp.state = -1;
-    // the default for a FAST structured block that fits; CWF_RESIDENT=0, or an explicit CWF_FUSED schedule (0: two
-    // kernels, 1: the per-launch fused iteration, 2: its persistent walk), keeps the launch-per-iteration schedules
-    const char *kn = knob("CWF_RESIDENT");
-    if ((kn && kn[0] == '0') || knob("CWF_FUSED"))
-        return false;
     const DevTiles &t = h->ds.t;
-    const uint32_t N = h->ds.N;
-    if (h->mode != CWF_MODE_FAST || !t.lat || !t.lcls || !t.lcz || h->sharded() || h->ds.Nown != N ||
-        h->lat_plane.size() != t.lnz || t.lk0 != 0 || t.lk1 != t.lnz)
+    const uint32_t N = h->ds.N, Nown = h->ds.Nown;
+    if (h->mode != CWF_MODE_FAST || !t.lat || !t.lcls || !t.lcz || h->lat_plane.size() != t.lnz)
         return false;
-    const unsigned nx = t.lnx, ny = t.lny, nz = t.lnz;
-    if (nx < 2 || ny < 2 || nz < 2)
+    const unsigned nx = t.lnx, ny = t.lny, per = nx * ny;
+    const unsigned k0 = shard ? t.lk0 : 0, k1 = shard ? t.lk1 : t.lnz, nz = k1 - k0;
+    if (nx < 2 || ny < 2 || nz < 2 || k1 > t.lnz)
         return false;
+    const std::vector<uint32_t> &plane = h->lat_plane;
+    if (!shard && (Nown != N || t.lk0 != 0 || t.lk1 != t.lnz))
+        return false;
+    // a slab shard: its owned nodes are the whole planes [k0, k1), every other plane is ghosts, its send segments
+    // (the halo plan's, <= 2 neighbours) disjoint
+    std::vector<uint32_t> remote;  // per owned node: neighbour slot << 24 | position in my send segment to it
+    if (shard)
+    {
+        if ((uint64_t)nz * per != Nown || h->nbr.size() > 2 || Nown >= N)
+            return false;
+        for (unsigned k = 0; k < t.lnz; ++k)
+        {
+            const bool own = k >= k0 && k < k1;
+            if (own ? (uint64_t)plane[k] + per > Nown : plane[k] < Nown || (uint64_t)plane[k] + per > N)
+                return false;
+        }
+        const uint64_t nsend = h->send_off.empty() ? 0 : h->send_off.back();
+        std::vector<uint32_t> idx(nsend);
+        if (nsend && hipMemcpy(idx.data(), h->send_idx, nsend * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return false;
+        remote.assign(Nown, kNone);
+        for (size_t k = 0; k < h->nbr.size(); ++k)
+            for (uint64_t i = h->send_off[k]; i < h->send_off[k + 1]; ++i)
+            {
+                const uint64_t pos = i - h->send_off[k];
+                if (idx[i] >= Nown || remote[idx[i]] != kNone || pos >= (1u << 24))
+                    return false;
+                remote[idx[i]] = (uint32_t)k << 24 | (uint32_t)pos;
+            }
+    }
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         return false;
-    if ((uint64_t)N > (uint64_t)cus * kResOwn)
+    // ranks sharing this device (a 1-GPU rehearsal) split its CUs: every rank's grid is resident at once
+    unsigned same = 1;
+    if (shard)
+        for (int p = 0; p < h->comm->nranks; ++p)
+            same += p != h->rank && h->comm->peer_same_device[p] != 0 ? 1u : 0u;
+    const unsigned G0 = (unsigned)cus / same;
+    if (!G0 || (uint64_t)Nown > (uint64_t)G0 * kResOwn)
         return false;  // more nodes than the grid's registers hold
+    // the node classes: the boundary type orders each box's own list (the type-stencil rows first)
+    std::vector<uint8_t> cls(N);
+    if (hipMemcpy(cls.data(), t.lcls, N, hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
     // the box grid
-    const unsigned G0 = (unsigned)cus;
     const unsigned kResMaxSlots = t.lhex ? kResMaxSlotsHex : kResMaxSlotsKuhn;
     double best = 1e300;
     unsigned bg[3] = {0, 0, 0};
@@ -82,9 +118,8 @@ bool resident_ready(cwf_hip_system *h)
     const unsigned G = bg[0] * bg[1] * bg[2];
     const int(*off)[3] = t.lhex ? kLatHexOff : kLatOff;
     const int noff = t.lhex ? kLatHexOffsets : kLatOffsets;
-    const std::vector<uint32_t> &plane = h->lat_plane;
     const auto node = [&](unsigned i, unsigned j, unsigned k) { return plane[k] + j * nx + i; };
-    // owner box of every node, and which nodes another box reads
+    // owner box of every own node, and which nodes another box reads (a ghost has no owner box)
     std::vector<uint32_t> owner(N, kNone);
     std::vector<unsigned> B(6 * (size_t)G);
     for (unsigned b = 0; b < G; ++b)
@@ -94,13 +129,17 @@ bool resident_ready(cwf_hip_system *h)
         split(nx, bg[0], bx, q[0], q[1]);
         split(ny, bg[1], by, q[2], q[3]);
         split(nz, bg[2], bz, q[4], q[5]);
+        q[4] += k0, q[5] += k0;
         for (unsigned k = q[4]; k < q[5]; ++k)
             for (unsigned j = q[2]; j < q[3]; ++j)
                 for (unsigned i = q[0]; i < q[1]; ++i)
                     owner[node(i, j, k)] = b;
     }
+    const auto inside = [&](long ii, long jj, long kk) {
+        return ii >= 0 && jj >= 0 && kk >= 0 && ii < (long)nx && jj < (long)ny && kk < (long)t.lnz;
+    };
     std::vector<uint8_t> needed(N, 0);
-    for (unsigned k = 0; k < nz; ++k)
+    for (unsigned k = k0; k < k1; ++k)
         for (unsigned j = 0; j < ny; ++j)
             for (unsigned i = 0; i < nx; ++i)
             {
@@ -108,22 +147,23 @@ bool resident_ready(cwf_hip_system *h)
                 for (int o = 1; o < noff; ++o)
                 {
                     const long ii = (long)i + off[o][0], jj = (long)j + off[o][1], kk = (long)k + off[o][2];
-                    if (ii < 0 || jj < 0 || kk < 0 || ii >= (long)nx || jj >= (long)ny || kk >= (long)nz)
+                    if (!inside(ii, jj, kk))
                         continue;
                     const uint32_t m = node((unsigned)ii, (unsigned)jj, (unsigned)kk);
-                    if (owner[m] != owner[n])
+                    if (owner[m] != kNone && owner[m] != owner[n])
                         needed[m] = 1;
                 }
             }
     // own lists (block-surface nodes first: their type-stencil rows; then the interior's brick rows), publication indices
     // in that order box after box, then the halo lists (sorted by publication index: consecutive lanes, consecutive
-    // records)
+    // records; a shard's ghost entries last, by ghost index)
     std::vector<uint32_t> pubidx(N, kNone);
     std::vector<std::vector<uint4>> ownl(G), halol(G);
     std::vector<uint4> hdr(G);
     uint32_t npub = 0;
     unsigned max_own = 0, max_halo = 0;
     size_t max_slots = 0;
+    uint64_t remote_sends = 0;
     for (unsigned b = 0; b < G; ++b)
     {
         const unsigned *q = &B[6 * (size_t)b];
@@ -135,14 +175,16 @@ bool resident_ready(cwf_hip_system *h)
                 for (unsigned j = q[2]; j < q[3]; ++j)
                     for (unsigned i = q[0]; i < q[1]; ++i)
                     {
-                        const bool shell = i == 0 || j == 0 || k == 0 || i + 1 == nx || j + 1 == ny || k + 1 == nz;
-                        if (shell != (pass == 0))  // the surface first: its slower rows land in the first
-                            continue;              // wave-slots, one wave per SIMD in turn, not in the last waves
                         const uint32_t n = node(i, j, k);
+                        const bool surface = (cls[n] >> 3) != 13u;
+                        if (surface != (pass == 0))  // the surface first: its slower rows land in the first
+                            continue;                // wave-slots, one wave per SIMD in turn, not in the last waves
                         const unsigned slot = (k - q[4] + 1) * PXY + (j - q[2] + 1) * PX + (i - q[0] + 1);
                         if (needed[n])
                             pubidx[n] = npub++;
-                        ownl[b].push_back(uint4{n, slot, pubidx[n], 0u});
+                        const uint32_t rw = shard ? remote[n] : kNone;
+                        remote_sends += rw != kNone ? 1u : 0u;
+                        ownl[b].push_back(uint4{n, slot, pubidx[n], rw});
                     }
         max_own = std::max<unsigned>(max_own, (unsigned)ownl[b].size());
     }
@@ -158,7 +200,7 @@ bool resident_ready(cwf_hip_system *h)
                     for (int o = 1; o < noff; ++o)
                     {
                         const long ii = (long)i + off[o][0], jj = (long)j + off[o][1], kk = (long)k + off[o][2];
-                        if (ii < 0 || jj < 0 || kk < 0 || ii >= (long)nx || jj >= (long)ny || kk >= (long)nz)
+                        if (!inside(ii, jj, kk))
                             continue;
                         const uint32_t m = node((unsigned)ii, (unsigned)jj, (unsigned)kk);
                         if (owner[m] == b || seen[m] == b)
@@ -166,22 +208,24 @@ bool resident_ready(cwf_hip_system *h)
                         seen[m] = b;
                         const unsigned slot = (unsigned)((kk - (long)q[4] + 1) * PXY + (jj - (long)q[2] + 1) * PX +
                                                          (ii - (long)q[0] + 1));
-                        halol[b].push_back(uint4{m, slot, pubidx[m], 0u});
+                        // a ghost (m >= Nown): its record in the mailbox, at its ghost index
+                        const uint32_t src = m >= Nown ? kResGhost | (m - Nown) : pubidx[m];
+                        halol[b].push_back(uint4{m, slot, src, 0u});
                     }
         std::sort(halol[b].begin(), halol[b].end(), [](const uint4 &a, const uint4 &c) { return a.z < c.z; });
         max_halo = std::max<unsigned>(max_halo, (unsigned)halol[b].size());
         halo_total += halol[b].size();
     }
     const unsigned npt = (max_own + kResThreads - 1) / kResThreads, nph = (max_halo + kResThreads - 1) / kResThreads;
-    if (max_own > kResOwn || max_halo > kResHalo || max_slots > kResMaxSlots)
+    if (max_own > kResOwn || max_halo > kResHalo || max_slots > kResMaxSlots || N - Nown >= kResGhost)
         return false;
     const bool small = npt <= 3 && nph <= 2;
     const unsigned own_stride = (small ? 3u : 4u) * kResThreads, halo_stride = (small ? 2u : 3u) * kResThreads;
     const size_t lds = max_slots * 16;
     // one workgroup per CU at least (the grid waits for all of them every phase)
-    if (resident_blocks_per_cu(h->ds, npt, nph, lds) < 1)
+    if (resident_blocks_per_cu(h->ds, npt, nph, lds, shard) < 1)
         return false;
-    std::vector<uint4> own((size_t)G * own_stride, uint4{kNone, 0u, kNone, 0u}),
+    std::vector<uint4> own((size_t)G * own_stride, uint4{kNone, 0u, kNone, kNone}),
         halo((size_t)G * halo_stride, uint4{kNone, 0u, kNone, 0u});
     for (unsigned b = 0; b < G; ++b)
     {
@@ -239,9 +283,13 @@ bool resident_ready(cwf_hip_system *h)
     if (hipMemset(dsh, 0, 2ull * 2 * kFusedSharesHost * G * sizeof(double)) != hipSuccess ||
         hipMemset(dpub, 0, 2ull * 12 * std::max<uint32_t>(npub, 1u) * sizeof(float)) != hipSuccess)
         return false;
+    // a shard's mailbox area (the peers store into it only in a resident solve, after the collective vote that
+    // follows this)
+    if (shard && peer_resident_clear(h))
+        return false;
     rp.G = G;
-    rp.npt = npt <= 3 && nph <= 2 ? 3 : 4;  // the instantiation (resident.hip)
-    rp.nph = npt <= 3 && nph <= 2 ? 2 : 3;
+    rp.npt = small ? 3 : 4;  // the instantiation (resident.hip)
+    rp.nph = small ? 2 : 3;
     rp.own_stride = own_stride;
     rp.halo_stride = halo_stride;
     rp.npub = std::max<uint32_t>(npub, 1u);
@@ -256,14 +304,58 @@ bool resident_ready(cwf_hip_system *h)
     rp.halo = dha;
     rp.pub = dpub;
     rp.sh = dsh;
+    rp.shard = shard;
+    rp.remote_sends = remote_sends;
     rp.state = 1;
     return true;
+}
+
+// CWF_RESIDENT=0, or an explicit CWF_FUSED schedule (0: two kernels, 1: the per-launch fused iteration, 2: its
+// persistent walk), keeps the launch-per-iteration schedules
+bool resident_off()
+{
+    const char *kn = knob("CWF_RESIDENT");
+    return (kn && kn[0] == '0') || knob("CWF_FUSED");
+}
+}  // namespace
+
+bool resident_ready(cwf_hip_system *h)
+{
+    ResidentPlan &rp = h->res;
+    if (rp.state)
+        return rp.state > 0 && !rp.shard;
+    if (h->sharded())
+        return false;  // a shard plans at the schedule vote (resident_shard_ready)
+    rp.state = -1;
+    return !resident_off() && plan_resident(h, false);
+}
+
+bool resident_shard_ready(cwf_hip_system *h)
+{
+    ResidentPlan &rp = h->res;
+    if (rp.state)
+        return rp.state > 0 && rp.shard;
+    rp.state = -1;
+    // PEER only: the kernel stores its surface records into the neighbours' mailboxes itself
+    if (resident_off() || !h->sharded() || !h->comm || h->comm->kind != 2 || h->nranks > kMaxPeers)
+        return false;
+    return plan_resident(h, true);
+}
+
+bool resident_on(const cwf_hip_system *h)
+{
+    if (h->sharded())
+        return h->res_agreed == 1 && h->res.state > 0 && h->res.shard;
+    return resident_ready(const_cast<cwf_hip_system *>(h));
 }
 
 uint64_t resident_offchip_bytes(const cwf_hip_system *h)
 {
     const ResidentPlan &rp = h->res;
-    return 48ull * (rp.halo_total + rp.npub) + 80ull * rp.G * (1ull + rp.G);
+    uint64_t b = 48ull * (rp.halo_total + rp.npub + rp.remote_sends) + 80ull * rp.G * (1ull + rp.G);
+    if (rp.shard)  // the rank totals: one rank's stores to every rank, every workgroup's poll of all of them
+        b += 80ull * h->nranks * (1ull + rp.G);
+    return b;
 }
 
 }  // namespace cwf

@@ -42,6 +42,7 @@ constexpr int kResNT = 512;
 constexpr uint32_t kResMaxRounds = 4000000u;  // poll rounds before a phase gives up (>= 4 s: a round is >= 1 us)
 constexpr uint32_t kResNone = 0xFFFFFFFFu;
 constexpr uint32_t kResOob = 0xFFFFFF00u;  // a byte offset past every range-checked buffer here, +32 included (no wrap)
+constexpr uint32_t kResGhost = 0x80000000u;  // a halo entry's source: a shard's ghost record (resident.cpp)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct ResArgs
@@ -61,6 +62,9 @@ struct ResArgs
     uint32_t max_it;
     uint64_t *trace;    // diagnostic (CWF_RESIDENT_TRACE): per workgroup 8 s_memrealtime stamps of phase trace_j
     uint32_t trace_j;
+    // a PEER slab shard (nranks > 1): own records of the send planes also stored into the neighbours' mailboxes, the
+    // ghosts' records read from this rank's, the rank totals stored to every rank and polled from this rank's
+    ResPeerArgs pa;
 };
 
 __device__ __forceinline__ void st4_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off, u32x4 w)
@@ -74,6 +78,15 @@ __device__ __forceinline__ u32x4 pk4(float a, float b, float c, float d)
 __device__ __forceinline__ u32x4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, uint32_t off)
 {
     return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);  // sc1: served past L1
+}
+// the PEER mailboxes (uncached IPC memory, written by other devices over xGMI): system scope both ways
+__device__ __forceinline__ void st4_sys(__amdgpu_buffer_rsrc_t rs, uint32_t off, u32x4 w)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, off, 0, 17);  // sc0 sc1
+}
+__device__ __forceinline__ u32x4 ld4_sys(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 17);
 }
 
 // a workgroup barrier that orders LDS only: no vmcnt wait, so the write-through stores and the polls in flight stay in
@@ -109,7 +122,7 @@ __device__ __forceinline__ void block_sum_lds(double v[K], double *red)
     }
 }
 
-template <bool SYM, class E, int NPT, int NPH>
+template <bool SYM, class E, int NPT, int NPH, bool MR>
 __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pcg_resident(DevSys s, ResArgs ra, const float *__restrict__ coef)
 {
     extern __shared__ float4 pl[];  // the box + one-node halo image of p_j (out-of-block entries stay 0)
@@ -118,6 +131,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     __shared__ float2 czB[kLatClasses];
     __shared__ float4 tcf[27 * E::nOff * 3];  // the boundary types' stencils (type 13, the interior, unused)
     __shared__ int vote[3];  // the poll rounds' workgroup vote, by round mod 3
+    __shared__ double rt[MR ? kFusedShares * kMaxPeers : 1];  // a shard: the ranks' totals, folded in rank order
     // the own entries' r, Ap, x and p: in registers for boxes of <= 3 nodes per thread (C2's 14 x 10 x 10), else
     // (LST) r, Ap, x in LDS (lane-linear: conflict-free) and p in the image (each slot formed by one thread), so 4
     // nodes per thread fit without spilling (the C3 / 8 slab's 19 x 19 x 5; LDS state cost C2 0.9 us per phase)
@@ -152,6 +166,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         czB[tid] = float2{zB.x, zB.y};
     }
     const uint32_t vbytes = 12u * s.N;
+    constexpr bool multi = MR;  // a PEER slab shard (its own instantiation: the one-block kernel stays as it was)
     const __amdgpu_buffer_rsrc_t rx = sized_rsrc(ra.x, vbytes), rr = sized_rsrc(ra.r, vbytes),
                                  rcls = sized_rsrc(T.lcls, s.N), rmass = sized_rsrc(s.mass, 4u * s.N),
                                  rpub = sized_rsrc(ra.pub, 96u * ra.npub), rsh = sized_rsrc(ra.sh, 160u * G);
@@ -195,6 +210,23 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
     for (int o = 0; o < E::nOff; ++o)
         soff[o] = E::off[o][0] + E::off[o][1] * PX + E::off[o][2] * PXY;
+    // halo entry h's record of the phase of parity par: another box's (pub), or a ghost's in the mailbox (a shard;
+    // the out-of-range load of the other source returns 0, so the two combine by OR)
+    const auto request = [&](int h, uint32_t par, u32x4 &a, u32x4 &c, u32x4 &e) {
+        const bool gh = (hpub[h] & kResGhost) != 0u, v = hn[h] != kResNone;
+        const uint32_t po = v && !gh ? 48u * (par * ra.npub + hpub[h]) : kResOob;
+        a = ld4_sc1(rpub, po);
+        c = ld4_sc1(rpub, po + 16u);
+        e = ld4_sc1(rpub, po + 32u);
+        if constexpr (multi)
+        {
+            const __amdgpu_buffer_rsrc_t rg = sized_rsrc(par ? ra.pa.grecv[1] : ra.pa.grecv[0], ra.pa.grecv_bytes);
+            const uint32_t pg = v && gh ? 48u * (hpub[h] & ~kResGhost) : kResOob;
+            a |= ld4_sys(rg, pg);
+            c |= ld4_sys(rg, pg + 16u);
+            e |= ld4_sys(rg, pg + 32u);
+        }
+    };
     __syncthreads();
     const float sK = (float)s.sK, sM = (float)s.sM;
     bool go = pre.active != 0;
@@ -268,18 +300,55 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
 #pragma unroll
             for (int h = 0; h < NPH; ++h)
-            {
-                const uint32_t po = hn[h] != kResNone ? 48u * (par * ra.npub + hpub[h]) : kResOob;
-                w0[h] = ld4_sc1(rpub, po);
-                w1[h] = ld4_sc1(rpub, po + 16u);
-                w2[h] = ld4_sc1(rpub, po + 32u);
-            }
+                request(h, par, w0[h], w1[h], w2[h]);
             stamp(j, 1);
             double v[kFusedShares];
 #pragma unroll
             for (int q = 0; q < kFusedShares; ++q)
                 v[q] = tid < G ? __hiloint2double((int)g[q].y, (int)g[q].x) : 0.0;
             block_sum_lds<kResNT, kFusedShares>(v, red);  // fixed order: every workgroup the same totals
+            if constexpr (multi)  // the rank's totals to every rank (workgroup 0), then every rank's, folded in rank order
+            {
+                const uint32_t nr = ra.pa.nranks, jp = j & 1u;
+                if (b == 0 && tid < (uint32_t)kFusedShares)
+                {
+                    double t = v[0];
+#pragma unroll
+                    for (int q = 1; q < kFusedShares; ++q)
+                        t = tid == (uint32_t)q ? v[q] : t;
+                    const u32x4 w = {(uint32_t)__double2loint(t), (uint32_t)__double2hiint(t), want, 0u};
+#pragma unroll
+                    for (int p = 0; p < kMaxPeers; ++p)
+                        if ((uint32_t)p < nr)
+                            st4_sys(sized_rsrc(jp ? ra.pa.tot[p][1] : ra.pa.tot[p][0], 80u * nr),
+                                    16u * (kFusedShares * ra.pa.rank + tid), w);
+                }
+                const __amdgpu_buffer_rsrc_t rtm = sized_rsrc(jp ? ra.pa.tot_mine[1] : ra.pa.tot_mine[0], 80u * nr);
+                u32x4 gt;
+                for (;; ++round)
+                {
+                    gt = ld4_sys(rtm, tid < kFusedShares * nr ? 16u * tid : kResOob);
+                    if (all_ok(tid >= kFusedShares * nr || gt.z == want))
+                        break;
+                    if (round >= kResMaxRounds)
+                    {
+                        give_up();
+                        return;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (tid < kFusedShares * nr)
+                    rt[tid] = __hiloint2double((int)gt.y, (int)gt.x);
+                lds_sync();
+#pragma unroll
+                for (int q = 0; q < kFusedShares; ++q)
+                {
+                    double t = 0.0;
+                    for (uint32_t p = 0; p < nr; ++p)
+                        t += rt[kFusedShares * p + q];
+                    v[q] = t;
+                }
+            }
             stamp(j, 7);
             go = fused_decide(ra.ctl, ra.hist, j, pre, v, &alpha, &beta);
             if (go && j - 1u == ra.max_it)  // max_iterations updates made (the host loop's last launch)
@@ -303,7 +372,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             __builtin_amdgcn_sched_barrier(0);  // one node's working set at a time (no cross-node hoisting)
             if (on[u] == kResNone)
                 continue;
-            const uint32_t e0 = tid + (uint32_t)u * kResNT, slot = osc[u] & 0xFFFFu;
+            const uint32_t slot = osc[u] & 0xFFFFu;
             // p_(j-1): this thread formed it last phase (0 at phase 0)
             const float4 po = LST ? pl[slot] : float4{S(u, 9), S(u, 10), S(u, 11), 0.f};
             const float rr0[3] = {S(u, 0), S(u, 1), S(u, 2)}, aa0[3] = {S(u, 3), S(u, 4), S(u, 5)},
@@ -363,12 +432,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             }
 #pragma unroll
             for (int h = 0; h < NPH; ++h)
-            {
-                const uint32_t po = hn[h] != kResNone ? 48u * (par * ra.npub + hpub[h]) : kResOob;
-                w0[h] = ld4_sc1(rpub, po);
-                w1[h] = ld4_sc1(rpub, po + 16u);
-                w2[h] = ld4_sc1(rpub, po + 32u);
-            }
+                request(h, par, w0[h], w1[h], w2[h]);
         }
         stamp(j, 3);
         // rows: Ap_j = K_eff p_j, the dots of the row, the box-surface records for the neighbours' next phase
@@ -382,6 +446,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             asm volatile("" : "+v"(c0));  // opaque per phase: the rows' image addresses are not hoisted out of the phase
                                           // loop (56 loop-invariant addresses would pin as many VGPRs)
             const uint32_t e0 = tid + (uint32_t)u * kResNT;
+            const uint32_t rw = multi ? ra.own[(size_t)b * ra.own_stride + e0].w : kResNone;  // a shard's send position
             const float4 q0 = LST ? pl[c0] : float4{S(u, 9), S(u, 10), S(u, 11), 0.f};
             const float u0[3] = {q0.x, q0.y, q0.z};
             float acc[3];
@@ -460,9 +525,25 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             fused_row_dots(czA, czB, cls, u0, zz, an, d);
             const uint32_t po = opub[u] != kResNone ? 48u * ((j & 1u) * ra.npub + opub[u]) : kResOob;
             const uint32_t tag = ra.tag0 + j + 1u;
-            st4_sc1(rpub, po, u32x4{__float_as_uint(rj[0]), __float_as_uint(rj[1]), __float_as_uint(rj[2]), tag});
-            st4_sc1(rpub, po + 16u, u32x4{__float_as_uint(an[0]), __float_as_uint(an[1]), __float_as_uint(an[2]), tag});
-            st4_sc1(rpub, po + 32u, u32x4{__float_as_uint(u0[0]), __float_as_uint(u0[1]), __float_as_uint(u0[2]), tag});
+            const u32x4 g0 = {__float_as_uint(rj[0]), __float_as_uint(rj[1]), __float_as_uint(rj[2]), tag},
+                        g1 = {__float_as_uint(an[0]), __float_as_uint(an[1]), __float_as_uint(an[2]), tag},
+                        g2 = {__float_as_uint(u0[0]), __float_as_uint(u0[1]), __float_as_uint(u0[2]), tag};
+            st4_sc1(rpub, po, g0);
+            st4_sc1(rpub, po + 16u, g1);
+            st4_sc1(rpub, po + 32u, g2);
+            if constexpr (multi)  // a send-plane node: the same record into the neighbour's mailbox, at its ghost position
+            {
+                const uint32_t jp = j & 1u, e = rw >> 24, pos = 48u * (rw & 0xFFFFFFu);
+                const __amdgpu_buffer_rsrc_t d0 = sized_rsrc(jp ? ra.pa.rdst[0][1] : ra.pa.rdst[0][0], ra.pa.rdst_bytes[0]),
+                                             d1 = sized_rsrc(jp ? ra.pa.rdst[1][1] : ra.pa.rdst[1][0], ra.pa.rdst_bytes[1]);
+                const uint32_t o0 = rw != kResNone && e == 0u ? pos : kResOob, o1 = rw != kResNone && e == 1u ? pos : kResOob;
+                st4_sys(d0, o0, g0);
+                st4_sys(d0, o0 + 16u, g1);
+                st4_sys(d0, o0 + 32u, g2);
+                st4_sys(d1, o1, g0);
+                st4_sys(d1, o1 + 16u, g1);
+                st4_sys(d1, o1 + 32u, g2);
+            }
         }
         stamp(j, 4);
         block_sum_lds<kResNT, kFusedShares>(d, red);
@@ -483,7 +564,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
     for (int u = 0; u < NPT; ++u)
     {
-        const uint32_t nb = on[u] != kResNone ? 12u * on[u] : 12u * kLatOob3, e0 = tid + (uint32_t)u * kResNT;
+        const uint32_t nb = on[u] != kResNone ? 12u * on[u] : 12u * kLatOob3;
         const u32x3 vx = {__float_as_uint(S(u, 6)), __float_as_uint(S(u, 7)), __float_as_uint(S(u, 8))},
                     vr = {__float_as_uint(S(u, 0)), __float_as_uint(S(u, 1)), __float_as_uint(S(u, 2))};
         __builtin_amdgcn_raw_buffer_store_b96(vx, wx, nb, 0, 0);
@@ -491,36 +572,37 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
 }
 
-template <bool SYM, class E, int NPT, int NPH>
+template <bool SYM, class E, int NPT, int NPH, bool MR>
 void launch_resident_e(const DevSys &s, const ResArgs &ra, unsigned G, size_t lds, hipStream_t st, hipEvent_t e0,
                        hipEvent_t e1)
 {
-    const auto k = k_pcg_resident<SYM, E, NPT, NPH>;
+    const auto k = k_pcg_resident<SYM, E, NPT, NPH, MR>;
     if (e0 && e1)
         hipExtLaunchKernelGGL(k, dim3(G), dim3(kResNT), lds, st, e0, e1, 0, s, ra, s.t.lcoef);
     else
         k<<<G, kResNT, lds, st>>>(s, ra, s.t.lcoef);
 }
 
-template <int NPT, int NPH>
+template <int NPT, int NPH, bool MR>
 void launch_resident_n(const DevSys &s, const ResArgs &ra, unsigned G, size_t lds, hipStream_t st, hipEvent_t e0,
                        hipEvent_t e1)
 {
     if (s.t.lhex)
-        s.t.lsym ? launch_resident_e<true, LatHex, NPT, NPH>(s, ra, G, lds, st, e0, e1)
-                 : launch_resident_e<false, LatHex, NPT, NPH>(s, ra, G, lds, st, e0, e1);
+        s.t.lsym ? launch_resident_e<true, LatHex, NPT, NPH, MR>(s, ra, G, lds, st, e0, e1)
+                 : launch_resident_e<false, LatHex, NPT, NPH, MR>(s, ra, G, lds, st, e0, e1);
     else
-        s.t.lsym ? launch_resident_e<true, LatKuhn, NPT, NPH>(s, ra, G, lds, st, e0, e1)
-                 : launch_resident_e<false, LatKuhn, NPT, NPH>(s, ra, G, lds, st, e0, e1);
+        s.t.lsym ? launch_resident_e<true, LatKuhn, NPT, NPH, MR>(s, ra, G, lds, st, e0, e1)
+                 : launch_resident_e<false, LatKuhn, NPT, NPH, MR>(s, ra, G, lds, st, e0, e1);
 }
 
-template <int NPT, int NPH>
+template <int NPT, int NPH, bool MR>
 int res_bpc(const DevSys &s, size_t lds)
 {
     int bpc = 0;
-    const auto k = s.t.lhex ? (s.t.lsym ? k_pcg_resident<true, LatHex, NPT, NPH> : k_pcg_resident<false, LatHex, NPT, NPH>)
-                            : (s.t.lsym ? k_pcg_resident<true, LatKuhn, NPT, NPH>
-                                        : k_pcg_resident<false, LatKuhn, NPT, NPH>);
+    const auto k = s.t.lhex ? (s.t.lsym ? k_pcg_resident<true, LatHex, NPT, NPH, MR>
+                                        : k_pcg_resident<false, LatHex, NPT, NPH, MR>)
+                            : (s.t.lsym ? k_pcg_resident<true, LatKuhn, NPT, NPH, MR>
+                                        : k_pcg_resident<false, LatKuhn, NPT, NPH, MR>);
     // the image is dynamic LDS beside ~100 KB of static arrays: allow the workgroup its size (gfx950: 160 KB)
     if (hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess ||
@@ -534,11 +616,13 @@ int res_bpc(const DevSys &s, size_t lds)
 // the instantiations: <= 3 own + 2 halo entries per thread, state in registers (boxes of <= 1,536 nodes and <= 1,024
 // ring entries: C2's 14 x 10 x 10), or <= 4 + 3 with the state in LDS (<= 2,048 nodes, <= 1,536 entries: the C3 / 8
 // slab's 19 x 19 x 5); 2 waves per SIMD, one workgroup per CU, no scratch
-int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds)
+int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds, bool shard)
 {
     if (npt <= 3 && nph <= 2)
-        return res_bpc<3, 2>(s, lds);
-    return npt <= 4 && nph <= 3 ? res_bpc<4, 3>(s, lds) : 0;
+        return shard ? res_bpc<3, 2, true>(s, lds) : res_bpc<3, 2, false>(s, lds);
+    if (npt <= 4 && nph <= 3)
+        return shard ? res_bpc<4, 3, true>(s, lds) : res_bpc<4, 3, false>(s, lds);
+    return 0;
 }
 
 void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hipEvent_t e0, hipEvent_t e1)
@@ -560,6 +644,10 @@ void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hip
     ra.x = h->x;
     ra.r = h->r;
     ra.max_it = max_it;
+    if (rp.shard)
+        peer_resident_args(h, ra.pa);
+    else
+        ra.pa = ResPeerArgs{};
     static uint64_t *trace = nullptr;  // diagnostic: CWF_RESIDENT_TRACE=path appends phase CWF_FUSED_TRACE_IT's stamps
     static unsigned trace_n = 0;
     const char *tp = knob("CWF_RESIDENT_TRACE");
@@ -578,9 +666,11 @@ void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hip
         (void)hipMemsetAsync(trace, 0, 64ull * rp.G, st);
     }
     if (rp.npt <= 3 && rp.nph <= 2)
-        launch_resident_n<3, 2>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
+        rp.shard ? launch_resident_n<3, 2, true>(h->ds, ra, rp.G, rp.lds, st, e0, e1)
+                 : launch_resident_n<3, 2, false>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
     else
-        launch_resident_n<4, 3>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
+        rp.shard ? launch_resident_n<4, 3, true>(h->ds, ra, rp.G, rp.lds, st, e0, e1)
+                 : launch_resident_n<4, 3, false>(h->ds, ra, rp.G, rp.lds, st, e0, e1);
     if (tp && trace)
     {
         std::vector<uint64_t> v(8ull * rp.G);

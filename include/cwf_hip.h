@@ -150,7 +150,9 @@ const char *cwf_hip_system_keff_kernel(const cwf_hip_system *h);
 /* Diagnostic: the PCG schedule a sharded handle's FAST solves run, decided collectively at its first solve:
  * -1 not decided yet (or not sharded), 0 the two-kernel iteration (two exchange steps per iteration), 1 the fused
  * lattice iteration with one exchange step per iteration, 2 the fused iteration exchanging inside its launches
- * (PEER: the Ap send rows, rank totals and epoch flags pushed by the launch itself, no exchange launch). */
+ * (PEER: the Ap send rows, rank totals and epoch flags pushed by the launch itself, no exchange launch), 3 the
+ * resident solve (PEER slab shards: every iteration in one launch per solve, its surface records and rank totals
+ * stored into the peers' mailboxes by the kernel). */
 int cwf_hip_system_exchange_schedule(const cwf_hip_system *h);
 /* 16 hex digits: a hash of the source files and build flags of the translation unit that holds that kernel
  * (csrc/Makefile FAST_SRC / PARITY_SRC), so a committed PMC profile can be matched to the code that ran */

@@ -153,7 +153,7 @@ def test_c3_fast_newmark_step_matches_parity(c3):
 # ------------------------------------------------------------------------------------------------ C2 FAST (the bench)
 # the benchmarked path (the default: the resident one-launch solve, one 512-thread workgroup per 14 x 10 x 10 box) and
 # the launch-per-iteration fused schedule it replaced (CWF_FUSED=1: its one-round grid of 436 workgroups)
-C2_SCHEDULES = {"resident": (None, "k_pcg_resident<true, LatKuhn, 3, 2>"),
+C2_SCHEDULES = {"resident": (None, "k_pcg_resident<true, LatKuhn, 3, 2, false>"),
                 "fused": ("1", "k_pcg_lattice<true, LatKuhn, true, true, false, false>")}
 
 

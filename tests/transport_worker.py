@@ -168,6 +168,8 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
                 with open(os.path.join(rdv, "done"), "w") as fh:
                     fh.write("1")
                 queue.put((rank, "ok", dict(dead=False, mailbox_kind=mkind, seconds=el,
+                                            kernel_after=(_lib.load().cwf_hip_system_keff_kernel(s.handle())
+                                                          or b"").decode(),
                                             error=None if res.has_value() else res.error().message,
                                             trial_error=us_err)))
             s.close()
@@ -180,6 +182,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
             return
         t = res.value()
         sched = _lib.load().cwf_hip_system_exchange_schedule(s.handle())
+        kern_after = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()  # the agreed schedule's
         # a second solve on the same communicator (the in-kernel exchange's epochs continue across solves)
         x2 = np.zeros(3 * sh.local_nodes, np.float32)
         t0 = time.perf_counter()
@@ -197,6 +200,7 @@ def run_rank_peer(rank, nranks, rdv, spec, queue):
         s.mode = _lib.MODE_FAST
         own = 3 * sh.owned_nodes
         queue.put((rank, "ok", dict(telemetry=(t.iterations, t.converged, t.residual_norm), kernel=kern,
+                                    kernel_after=kern_after,
                                     nodes=sh.node_global[: sh.owned_nodes].astype(np.int64), x=x[:own].copy(),
                                     exchange_us=us, parity_error=perr, mailbox_kind=mkind, schedule=sched,
                                     telemetry2=(t2.iterations, t2.converged, t2.residual_norm),
