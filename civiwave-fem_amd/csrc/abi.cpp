@@ -816,8 +816,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                         else if (std::memcmp(&tmass[ty], &d->lumped_mass[n], sizeof(float)) != 0)
                             uniform = false;
                     }
-            const char *lm = knob("CWF_LAT_MASS");
-            if (uniform && tseen[13] && !(lm && lm[0] == '0'))  // type 13: inside along x, y and z (the bricks' nodes)
+            if (uniform && tseen[13])  // type 13: inside along x, y and z (the bricks' nodes)
             {
                 t.lmu = 1;
                 t.lmass = tmass[13];

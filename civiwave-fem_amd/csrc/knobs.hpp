@@ -29,12 +29,8 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_HEX_NT", "128|256: lanes of the hex8 tiles (tests/test_hex8.py)"},
     {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
     {"CWF_LATTICE", "0: no structured-block stencil (lattice.cpp); structured Kuhn (hex8) blocks then run the fan groups (hex tiles)"},
-    {"CWF_LAT_MASS", "0: the lattice bricks read the per-node mass even when the strict interior's is uniform"},
     {"CWF_LAT_ZR", "0|1: the lattice update pass stores z / the K_eff pass forms z from r and the node class "
                    "(default: the latter from 2M nodes)"},
-    {"CWF_LAT_SHELL_LAST", "0|1|2: the lattice shell workgroups lead / follow the bricks / each k-chunk's perimeter "
-                           "workgroups follow its bricks (default: follow when the grid fits one round of resident "
-                           "workgroups, else interleaved)"},
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     {"CWF_PARITY_TILES", "strip: PARITY node tiles of 256 consecutive nodes also on a single handle (default there: "
                          "compact breadth-first tiles and a separate p.Ap partials pass; shards always use strips)"},

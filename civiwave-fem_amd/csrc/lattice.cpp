@@ -464,14 +464,12 @@ void lattice_plan(DevTiles &t)
     // the shell workgroups lead the bricks when the grid takes several rounds of resident workgroups (C3: 2.8
     // rounds, shell last -2.6%) and follow them when it fits in one (C2: 436 workgroups, shell last +6.2%, keff 14.2
     // -> 12.9 us; same box, two passes)
-    const char *sl = knob("CWF_LAT_SHELL_LAST");
     // several rounds of many k-chunks: each chunk's perimeter workgroups right after its bricks (C3 +0.5-1.4%, C3
     // hex8 +1.5% over the shell first, same box: the perimeter gathers find the chunk's lines in the XCD's L2;
     // profiles/r04w_*). Not with few chunks: each XCD takes a contiguous share of the items, so C5's one chunk put
     // its 1,250 whole-column bricks on three XCDs and the end planes on the rest (K_eff 241 -> 476 us, r04z)
     const uint64_t nchunks = (planes + L - 1) / L;
-    t.lshl = sl ? (sl[0] == '2' ? 2 : sl[0] == '1' ? 1 : 0)
-                : (t.lnwork <= kLatTargetItems ? 1 : nchunks >= 16 ? 2 : 0);
+    t.lshl = t.lnwork <= kLatTargetItems ? 1 : nchunks >= 16 ? 2 : 0;
     t.lnsc = 0;
     if (t.lshl == 2)  // interleaved: per k-chunk its bricks, then the perimeters of its planes; the end planes last
     {

@@ -19,7 +19,8 @@
 // rank totals are pushed by the launch, the flags raised by its last workgroup, and the next launch's prologue waits.
 //
 // Workgroups wait for peers, not for each other, and the grid is small (<= 64 workgroups of 1024 threads, resident
-// together), so every workgroup reaches its ticket. The ticket is a relaxed agent-scope add: what it orders are the
+// together), so every workgroup reaches its ticket. The ticket is an agent-scope add (acq_rel in k_peer_step, relaxed in
+// the fused launch, where the release's L2 write-back cost 14 us per launch): what it orders are the
 // workgroups' write-through (system-scope) stores, each already acknowledged (every storing wave waits vmcnt(0)
 // behind a workgroup barrier before its lane takes the ticket), so the last arriver's system-scope release fence and
 // flag store come after every workgroup's stores have reached the receiver's memory. Round 4's first form was three launches (push, wait, unpack)
@@ -193,14 +194,17 @@ __global__ __launch_bounds__(kPeerThreads) void k_peer_step(PeerStep a)
     // hand-off of the MI355X guide's measured-forms table, row 1 (sc0 sc1 stores, each wave's vmcnt(0), a barrier,
     // one agent-scope add per workgroup, the last adder told by the returned value); the last arriver then orders
     // the whole launch's stores before its flag stores with a system-scope release, and the consumer side keeps
-    // its acquire. Relaxed on the ticket itself: the ordering it needs is the waits before it, not the atomic's
+    // its acquire. The ticket is acq_rel as well (the release formally orders the workgroup's
+    // stores before its add, the acquire the last arriver's flag stores after every add): measured free here (8.3-9.0
+    // us per step relaxed, 8.3-9.4 acq_rel, same round; profiles/r06s_ticket_acq_rel.txt), unlike the fused launch's
+    // ticket (lattice_fused.inc fused_peer_publish: +14 us per launch, kept relaxed)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
     {
         // one workgroup (the scalar-only p.Ap step) is its own last arriver: no ticket round trip
         const uint32_t old = gridDim.x == 1 ? 0u
-                                            : __hip_atomic_fetch_add(a.cnt_ticket, 1u, __ATOMIC_RELAXED,
+                                            : __hip_atomic_fetch_add(a.cnt_ticket, 1u, __ATOMIC_ACQ_REL,
                                                                      __HIP_MEMORY_SCOPE_AGENT);
         if (old + 1 == gridDim.x)
         {

@@ -88,13 +88,11 @@ def test_lattice_off_runs_the_fan_groups(case, monkeypatch):
     assert _apply_err(case, s) <= 2e-5
 
 
-@pytest.mark.parametrize("shell", ["lead", "follow"])
 @pytest.mark.parametrize("L", ["2", "3", "64"])
-def test_lattice_work_item_lengths(L, shell, monkeypatch):
-    """Planes per work item (CWF_LAT_L): chunk boundaries inside the block and one chunk over all planes; the shell
-    workgroups before or after the bricks (CWF_LAT_SHELL_LAST)."""
+def test_lattice_work_item_lengths(L, monkeypatch):
+    """Planes per work item (CWF_LAT_L): chunk boundaries inside the block and one chunk over all planes (the shell
+    workgroups' place in the grid follows the grid's size: lattice.cpp lattice_plan)."""
     monkeypatch.setenv("CWF_LAT_L", L)
-    monkeypatch.setenv("CWF_LAT_SHELL_LAST", "1" if shell == "follow" else "0")
     case = scenarios.block_case(40, 17, 9, h=0.1, tol=1e-6)
     assert _apply_err(case, _system(case), seed=11) <= 2e-5
 
@@ -131,14 +129,18 @@ def test_lattice_pcg_variants_solve(variant, monkeypatch):
     """The PCG-loop bricks in their three forms solve to the oracle's solution (bricks cut by the faces in x, y and
     k): the strict interior's one lumped mass as a kernel argument with z = M^-1 r formed from r and the node
     class in the K_eff pass and no z stored by the update pass (CWF_LAT_ZR=1, the default from 2M nodes), or with z
-    stored by the update pass (CWF_LAT_ZR=0, the default below), and the per-node mass through LDS
-    (CWF_LAT_MASS=0, which also stores z)."""
+    stored by the update pass (CWF_LAT_ZR=0, the default below), and the per-node mass through LDS (a block whose
+    strict interior's lumped masses are not one value: a few perturbed, the oracle given the same masses; z stored)."""
     monkeypatch.setenv("CWF_FUSED", "0")  # the two-kernel iteration's brick variants
     monkeypatch.setenv("CWF_LAT_ZR", "1" if variant == "z-from-r" else "0")
-    if variant == "per-node-mass":
-        monkeypatch.setenv("CWF_LAT_MASS", "0")
     monkeypatch.setenv("CWF_LAT_L", "3")
     case = scenarios.block_case(40, 19, 9, h=0.1, tol=1e-6, max_iterations=1500)
+    if variant == "per-node-mass":  # interior nodes (i, j, k) = (20, 9, 4) and (7, 3, 2) x 1.5 and x 0.75
+        P = case.packing
+        for (i, j, k), f in (((20, 9, 4), 1.5), ((7, 3, 2), 0.75)):
+            n = (k * 20 + j) * 41 + i
+            P.lumped_mass64[n] *= f
+            P.lumped_mass[n] = np.float32(P.lumped_mass64[n])
     s = _system(case)
     # <..., mass uniform, z from r, plane bases (0 read, 1 affine, 2 affine + deep prefetch)>
     want = {"z-from-r": ["true", "true"], "z-stored": ["true", "false"], "per-node-mass": ["false", "false"]}[variant]

@@ -15,7 +15,6 @@ from helpers import oracle_system  # noqa: E402
 
 VARIANTS = {"fused": {"CWF_FUSED": "1"}, "two-kernel": {"CWF_FUSED": "0"},
             "two-kernel-zr": {"CWF_FUSED": "0", "CWF_LAT_ZR": "1"},
-            "fused-mass": {"CWF_FUSED": "1", "CWF_LAT_MASS": "0"}, "two-kernel-mass": {"CWF_FUSED": "0", "CWF_LAT_MASS": "0"},
             "tiles": {"CWF_LATTICE": "0"}, "tiles256": {"CWF_LATTICE": "0", "CWF_HEX_NT": "256"}}
 
 
@@ -74,7 +73,7 @@ def main():
         for name, env in VARIANTS.items():
             if element == "tet4" and "256" in name:
                 continue
-            for k in ("CWF_FUSED", "CWF_LAT_ZR", "CWF_LATTICE", "CWF_HEX_NT", "CWF_LAT_MASS"):
+            for k in ("CWF_FUSED", "CWF_LAT_ZR", "CWF_LATTICE", "CWF_HEX_NT"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             s = pcg.MatrixFreeSystem.from_packing(P, case.materials, sK, sM, mode=_lib.MODE_FAST)
