@@ -41,6 +41,19 @@ def main():
     print(f"  phase start spread {t[:, 0].max() - t[:, 0].min():.2f} us, release (wait done) spread "
           f"{t[:, 1].max() - t[:, 1].min():.2f} us, last end {t[:, 6].max():.2f} us after the first start, "
           f"compute (release -> end) median {np.median(t[:, 6] - t[:, 1]):.2f} max {np.max(t[:, 6] - t[:, 1]):.2f}")
+    # per box: the form + rows span by the number of block faces the box touches (box b = (bx, by, bz), x fastest)
+    hdr = B["hdr"].split("boxes ")
+    if len(hdr) > 1:
+        gx, gy, gz = (int(v) for v in hdr[1].split("x"))
+        b = a[:, 0]
+        pos = np.stack([b % gx, (b // gx) % gy, b // (gx * gy)], 1)
+        faces = ((pos == 0) | (pos == np.array([gx, gy, gz]) - 1)).sum(1)
+        work = t[:, 4] - t[:, 2]
+        for f in sorted(set(faces.tolist())):
+            w = work[faces == f]
+            print(f"  boxes on {f} block faces: {len(w):3d}, form + rows median {np.median(w):5.2f} max {w.max():5.2f} us")
+        for ax, n in zip("xyz", (gx, gy, gz)):
+            print(f"  along {ax}: " + " ".join(f"{np.median(work[pos[:, 'xyz'.index(ax)] == q]):.2f}" for q in range(n)))
 
 
 if __name__ == "__main__":
