@@ -527,8 +527,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
             // contiguous id range (whole-line owner p / partial stores, coalesced owned gathers). The groups
             // and tiles are built from coordinates and tet order only, so the rebuild after this renumbering
             // gives the same partition.
-            const char *ot = knob("CWF_OWNER_ORDER");
-            if (!(ot && ot[0] == '0') && (hex || (d->material_count <= 16 && groups_enabled() && geo_ok)))
+            if (hex || (d->material_count <= 16 && groups_enabled() && geo_ok))
             {
                 cwf_system_desc md = *d;
                 md.element_connectivity = r_conn.data();
@@ -787,8 +786,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         t.E = (uint32_t)E;
         t.geo = 1;
         t.total_tile_nodes = (uint32_t)N;
-        const char *wt = knob("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
-        t.wt_part = wt ? (wt[0] == '1') : 0;
+        t.wt_part = 0;
         // per-class preconditioner (the update pass reads one byte per node instead of the 16-B record and the
         // partial-run bounds) when the lumped mass is a function of the boundary type
         {
@@ -871,8 +869,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         {
             t.hex = 1;
             t.hex_nt = (int)hex_tile_lanes(E);
-            const char *wt = knob("CWF_TILES_WT");  // 0|1: write-through hex partials (diagnostic)
-            t.wt_part = wt && wt[0] == '1';
+            t.wt_part = 0;
             t.push = 1;
         }
         else
@@ -947,10 +944,7 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
                     t.push = 1;
                     t.pipe = 1;
                     t.pipe_nt = (int)gnt;
-                    {
-                        const char *wt = knob("CWF_TILES_WT");  // 0|1 overrides (diagnostic)
-                        t.wt_part = wt ? (wt[0] == '1') : (E < 4000000ull);
-                    }
+                    t.wt_part = E < 4000000ull ? 1 : 0;  // write-through tile partials below 4M tets
                     t.ntiles = gt.ntiles;
                     t.ngroups = gt.ngroups;
                     t.max_tile_nodes = gt.max_tile_nodes;
@@ -965,12 +959,11 @@ int cwf_hip_system_create(const cwf_system_desc *d, int device, cwf_hip_system *
         {
         try
         {
-            // pipelined tiles: 256-thread workgroups over 512-element tiles, or 128 over 256 (CWF_PIPE_NT, or
-            // automatically for meshes whose 512-element tiles would give each resident workgroup < 8 tiles)
+            // pipelined tiles: 256-thread workgroups over 512-element tiles, or 128 over 256 (128 below 4M
+            // tets: the meshes whose 512-element tiles would give each resident workgroup < 8 tiles)
             if (t.pipe)
             {
-                const char *pn = knob("CWF_PIPE_NT");
-                t.pipe_nt = pn ? (atoi(pn) == 128 ? 128 : 256) : (E < 4000000ull ? 128 : 256);
+                t.pipe_nt = E < 4000000ull ? 128 : 256;
                 t.push = 1;  // the pipelined kernel folds pushed forces (epos), not local-CSR entries
             }
             if (hex)

@@ -358,16 +358,11 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
     // leaves aimed at the full lane count with a +-n/32 layer-gap window: C3 14.3k tiles at 90% lane fill
     // against 15.9k at 81% for the per-tet tiles' 15/16 target and +-n/16 window, same T/N (K_eff 111.4 ->
     // 105.6 us, +3.7% PCG it/s); C2 2.9k tiles against 3.2k (T/N 1.73 -> 1.76, +1.2%) (same-box A/B).
-    // CWF_GROUP_RCB="tdiv,wdiv" overrides (diagnostic)
-    int tdiv = 0, wdiv = 32;
-    if (const char *rv = knob("CWF_GROUP_RCB"))
-        sscanf(rv, "%d,%d", &tdiv, &wdiv);
+    const int tdiv = 0, wdiv = 32;  // the RCB leaf target and layer-gap window (measured best, rounds 2-3)
     rcb_partition(cen, gext, order, nt, leaf_end, tdiv, wdiv);
 
-    // lanes of a tile ordered against LDS bank conflicts (order_lanes_by_bank; CWF_GROUP_LANES=0 keeps the
-    // RCB order, diagnostic)
-    const char *gl = knob("CWF_GROUP_LANES");
-    const bool lanes_by_bank = order_lanes && !(gl && gl[0] == '0');
+    // lanes of a tile ordered against LDS bank conflicts (order_lanes_by_bank)
+    const bool lanes_by_bank = order_lanes;
     // tiles: each RCB leaf, split greedily while its node list would exceed max_nodes
     std::vector<uint32_t> stamp(N, ~0u), local(N, 0), tcnt(N, 0), placed;
     std::vector<uint32_t> nodes, cnt, cur;

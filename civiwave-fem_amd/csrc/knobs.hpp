@@ -17,17 +17,12 @@ struct Knob
 inline constexpr Knob kKnobs[] = {
     // node order and tiling of a FAST handle (abi.cpp, groups.cpp, tiles.cpp)
     {"CWF_RENUMBER", "0: keep the caller's node order (no Morton / owner-tile renumbering)"},
-    {"CWF_OWNER_ORDER", "0: Morton renumbering only, not (owner tile, Morton)"},
     {"CWF_GEO", "0: the 48-B gradient records instead of recomputing geometry from tile-node coordinates"},
     {"CWF_GROUPS", "0: per-tet tiles (k_keff_tiles_pipe) instead of the fan groups"},
     {"CWF_GROUP_NT", "128: 128-lane fan-group tiles (default 256; tests/test_gpu_parity.py)"},
-    {"CWF_GROUP_RCB", "\"tdiv,wdiv\": RCB leaf target and layer-gap window of the fan-group tiling"},
-    {"CWF_GROUP_LANES", "0: keep the RCB order of a tile's groups (no bank-aware lane order)"},
     {"CWF_TILE_ORDER", "morton|rcb: per-tet / hex8 tile order"},
     {"CWF_TILE_PIPE", "0: the one-tile-per-workgroup per-tet kernel (k_keff_tiles)"},
-    {"CWF_PIPE_NT", "128|256: lanes of the per-tet pipelined tiles"},
     {"CWF_HEX_NT", "128|256: lanes of the hex8 tiles (tests/test_hex8.py)"},
-    {"CWF_TILES_WT", "0|1: write-through tile partials (default: fan groups below 4M tets)"},
     {"CWF_LATTICE", "0: no structured-block stencil (lattice.cpp); structured Kuhn (hex8) blocks then run the fan groups (hex tiles)"},
     {"CWF_LAT_ZR", "0|1: the lattice update pass stores z / the K_eff pass forms z from r and the node class "
                    "(default: the latter from 2M nodes)"},
@@ -47,7 +42,6 @@ inline constexpr Knob kKnobs[] = {
                            "appended (tools/resident_trace.py)"},
     {"CWF_FUSED_TRACE_IT", "n: the iteration whose launch CWF_FUSED_TRACE records (default 50)"},
     {"CWF_FUSED_MAXWG", "n: cap on the fused launch's grid (default 1024 workgroups; a grid below the work items walks them persistently)"},
-    {"CWF_UPD_CAP", "n: at most n update-pass workgroups (their r.r / r.z shares are what the next K_eff refolds)"},
     {"CWF_XLAG", "1..4: iterations per lazy x update (tests/test_gpu_parity.py compares 4 with 1)"},
     // multi-GPU (comm.cpp)
     {"CWF_RCCL_LIB", "path: load this NCCL-API library instead of librccl (tests/transport: the host-staged "

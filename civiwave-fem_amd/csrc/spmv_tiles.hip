@@ -1854,10 +1854,7 @@ unsigned update_resident()
 unsigned fast_update_blocks(const DevSys &s, bool flush)
 {
     static const unsigned resident[2] = {update_resident<1, false>(), update_resident<1, true>()};
-    static const unsigned cap = [] {
-        const char *e = knob("CWF_UPD_CAP");
-        return e && atoi(e) > 0 ? (unsigned)atoi(e) : kMaxUpdateBlocks;
-    }();
+    constexpr unsigned cap = kMaxUpdateBlocks;
     const unsigned res = std::min(resident[flush ? 1 : 0], cap);
     const unsigned g = grid_for(s.N, kUpdThreads);
     return g < res ? (g ? g : 1u) : res;
