@@ -4,7 +4,7 @@ per PCG iteration, without its exchange): fixed iterations (tol 1e-30), the seco
 read-backs included): the resident one-launch solve (the default where the block fits on chip, resident.hip), the fused
 launch-per-iteration schedule (CWF_FUSED=1) and the two-kernel loop (CWF_FUSED=0).
 
-usage: python tools/block_iter_time.py NX NY NZ [ITERATIONS]"""
+usage: python tools/block_iter_time.py NX NY NZ [ITERATIONS]   (BLK_ELEMENT=hex8: the block as native hex8 cells)"""
 import os
 import sys
 import time
@@ -21,7 +21,8 @@ def main():
 
     from cwf import _lib, pcg, scenarios
 
-    case = scenarios.block_case(nx, ny, nz, h=0.1, tol=1e-30, max_iterations=its)
+    element = os.environ.get("BLK_ELEMENT", "tet4")
+    case = scenarios.block_case(nx, ny, nz, h=0.1, tol=1e-30, max_iterations=its, element=element)
     rhs = case.static_rhs()
     # BLK_SCHEDULES=resident,1,0 (a comma list) limits the schedules (same-box A/B of library builds: CWF_LIB_PATH)
     for fused in os.environ.get("BLK_SCHEDULES", "resident,1,0").split(","):
@@ -36,7 +37,7 @@ def main():
             t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(its, 1e-30), pcg.PcgVectors(x, None)).value()
             el = time.perf_counter() - t0
         kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
-        print(f"{nx}x{ny}x{nz} ({3 * nx * ny * nz / 1e6:.2f}M DOF) { {'resident': 'resident', '1': 'fused'}.get(fused, 'two kernels')}: "
+        print(f"{nx}x{ny}x{nz} {element} ({3 * nx * ny * nz / 1e6:.2f}M DOF) { {'resident': 'resident', '1': 'fused'}.get(fused, 'two kernels')}: "
               f"{t.iterations} iterations, {el / max(t.iterations, 1) * 1e6:.2f} us per iteration ({kern})", flush=True)
         s.close()
 
