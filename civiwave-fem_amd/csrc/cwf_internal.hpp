@@ -297,7 +297,7 @@ struct ResidentPlan
     unsigned max_own = 0, max_halo = 0;
     uint64_t halo_total = 0;            // halo entries over every box (records read per phase)
     const uint4 *hdr = nullptr, *own = nullptr, *halo = nullptr;
-    const float4 *tcoef = nullptr;  // [27][nOff][3] the boundary types' stencils
+    const float4 *tcoef = nullptr;  // [G][12][nOff][3] each box's boundary types' stencils
     float *pub = nullptr;
     double *sh = nullptr;
     uint32_t tag = 1;  // the next solve's granule tag base (resident.hip: phase j publishes tag + j + 1)
@@ -496,6 +496,7 @@ int group_fused(const std::vector<cwf_hip_system *> &g);  // 1 fused, 0 two-kern
 bool resident_ready(cwf_hip_system *h);
 void launch_pcg_resident(cwf_hip_system *h, uint32_t max_it, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
 int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds, bool shard);
+size_t resident_static_lds(const DevSys &s, bool small, bool shard);  // the instantiation's static LDS bytes
 uint64_t resident_offchip_bytes(const cwf_hip_system *h);  // per phase: halo records read, surface records and shares
 // a PEER slab shard's resident solve: planned on the rank's own at the schedule vote (group_fused), run only when every
 // rank planned one (res_agreed); the init is the fused one's without its launch 0 and exchange step (comm.cpp)

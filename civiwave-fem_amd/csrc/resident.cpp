@@ -18,10 +18,10 @@ namespace cwf
 namespace
 {
 constexpr unsigned kResThreads = 512, kResOwn = 4 * kResThreads, kResHalo = 3 * kResThreads;  // resident.hip
-// the box image's float4 slots within the 160 KB of LDS a gfx950 workgroup may hold, beside the kernel's static
-// arrays (the own entries' r, Ap, x: 72 KB; the class table and the boundary types' stencils: 25 KB with the
-// 15-offset Kuhn stencil, 40.5 KB with the 27-offset hex8 one)
-constexpr unsigned kResMaxSlotsKuhn = 3800, kResMaxSlotsHex = 2800;  // (the register-state instantiation has 72 KB more)
+// the box image's float4 slots fill the LDS a gfx950 workgroup may hold beside the kernel's static arrays (the own
+// entries' r, Ap, x in the 4-node instantiation: 72 KB; the class table; the box's boundary types' stencils, at
+// most kResTypesHost of the 27: 8.6 KB with the 15-offset Kuhn stencil, 15.6 KB with the 27-offset hex8 one)
+constexpr unsigned kResTypesHost = 12;  // resident.hip kResTypes
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kResGhost = 0x80000000u;  // a halo entry's source: a ghost record (resident.hip)
 constexpr unsigned kFusedSharesHost = 5;  // kFusedShares (lattice_common.hpp): one 16-B granule each
@@ -94,8 +94,18 @@ bool plan_resident(cwf_hip_system *h, bool shard)
     std::vector<uint8_t> cls(N);
     if (hipMemcpy(cls.data(), t.lcls, N, hipMemcpyDeviceToHost) != hipSuccess)
         return false;
-    // the box grid
-    const unsigned kResMaxSlots = t.lhex ? kResMaxSlotsHex : kResMaxSlotsKuhn;
+    // the box grid; the image's cap from the LDS the instantiation leaves (the 3-node one for boxes it takes)
+    int lds_max = 0;
+    if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || lds_max <= 0)
+        return false;
+    const size_t st_small = resident_static_lds(h->ds, true, shard), st_lst = resident_static_lds(h->ds, false, shard);
+    if (!st_small || !st_lst || st_small >= (size_t)lds_max || st_lst >= (size_t)lds_max)
+        return false;
+    const unsigned cap_small = (unsigned)(((size_t)lds_max - st_small) / 16),
+                   cap_lst = (unsigned)(((size_t)lds_max - st_lst) / 16);
+    const auto slot_cap = [&](uint64_t own, uint64_t halo) {
+        return own <= 3ull * kResThreads && halo <= 2ull * kResThreads ? cap_small : cap_lst;
+    };
     double best = 1e300;
     unsigned bg[3] = {0, 0, 0};
     for (unsigned gx = 1; gx <= std::min(nx, G0); ++gx)
@@ -104,7 +114,7 @@ bool plan_resident(cwf_hip_system *h, bool shard)
             {
                 const uint64_t sx = (nx + gx - 1) / gx, sy = (ny + gy - 1) / gy, sz = (nz + gz - 1) / gz;
                 const uint64_t own = sx * sy * sz, slots = (sx + 2) * (sy + 2) * (sz + 2), halo = slots - own;
-                if (own > kResOwn || halo > kResHalo || slots > kResMaxSlots)
+                if (own > kResOwn || halo > kResHalo || slots > slot_cap(own, halo))
                     continue;
                 const double cost = (double)own + 1.5 * (double)halo + 2.0 * (double)(gx * gy * gz);
                 if (cost < best)
@@ -216,8 +226,32 @@ bool plan_resident(cwf_hip_system *h, bool shard)
         max_halo = std::max<unsigned>(max_halo, (unsigned)halol[b].size());
         halo_total += halol[b].size();
     }
+    // each box's boundary types (its block-surface nodes'), in ascending order; the own entry carries the node's
+    // index among them in y >> 24 (the kernel's stencil table holds only the box's types)
+    std::vector<uint8_t> btypes((size_t)G * kResTypesHost, 0);
+    for (unsigned b = 0; b < G; ++b)
+    {
+        int idx[27];
+        std::fill(idx, idx + 27, -1);
+        unsigned nt = 0;
+        for (const uint4 &e : ownl[b])
+            idx[cls[e.x] >> 3] = 0;
+        for (unsigned ty = 0; ty < 27; ++ty)
+            if (idx[ty] == 0 && ty != 13)
+            {
+                if (nt == kResTypesHost)
+                    return false;
+                btypes[(size_t)b * kResTypesHost + nt] = (uint8_t)ty;
+                idx[ty] = (int)nt++;
+            }
+        for (uint4 &e : ownl[b])
+        {
+            const unsigned ty = cls[e.x] >> 3;
+            e.y |= (ty == 13 ? 0u : (uint32_t)idx[ty]) << 24;
+        }
+    }
     const unsigned npt = (max_own + kResThreads - 1) / kResThreads, nph = (max_halo + kResThreads - 1) / kResThreads;
-    if (max_own > kResOwn || max_halo > kResHalo || max_slots > kResMaxSlots || N - Nown >= kResGhost)
+    if (max_own > kResOwn || max_halo > kResHalo || max_slots > slot_cap(max_own, max_halo) || N - Nown >= kResGhost)
         return false;
     const bool small = npt <= 3 && nph <= 2;
     const unsigned own_stride = (small ? 3u : 4u) * kResThreads, halo_stride = (small ? 2u : 3u) * kResThreads;
@@ -269,8 +303,14 @@ bool plan_resident(cwf_hip_system *h, bool shard)
             q[2] = float4{(float)S[8], 0.f, 0.f, 0.f};
         }
     }
+    std::vector<float4> btco((size_t)G * kResTypesHost * noff * 3, float4{0.f, 0.f, 0.f, 0.f});
+    for (unsigned b = 0; b < G; ++b)
+        for (unsigned k = 0; k < kResTypesHost; ++k)
+            std::copy(tco.begin() + (size_t)3 * noff * btypes[(size_t)b * kResTypesHost + k],
+                      tco.begin() + (size_t)3 * noff * (btypes[(size_t)b * kResTypesHost + k] + 1),
+                      btco.begin() + ((size_t)b * kResTypesHost + k) * 3 * noff);
     float4 *dtc;
-    if (upload(h, &dtc, tco.data(), tco.size()))
+    if (upload(h, &dtc, btco.data(), btco.size()))
         return false;
     uint4 *dh, *dow, *dha;
     float *dpub;

@@ -43,6 +43,7 @@ constexpr uint32_t kResMaxRounds = 4000000u;  // poll rounds before a phase give
 constexpr uint32_t kResNone = 0xFFFFFFFFu;
 constexpr uint32_t kResOob = 0xFFFFFF00u;  // a byte offset past every range-checked buffer here, +32 included (no wrap)
 constexpr uint32_t kResGhost = 0x80000000u;  // a halo entry's source: a shard's ghost record (resident.cpp)
+constexpr int kResTypes = 12;  // boundary types one box's own nodes touch, at most (resident.cpp kResTypesHost)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct ResArgs
@@ -52,7 +53,8 @@ struct ResArgs
     const uint4 *hdr;   // [G] {LDS slots, -, PX, PXY}: the box's (sx + 2)(sy + 2)(sz + 2) image and its strides
     const uint4 *own;   // [G][own_stride] {node, image slot, publication index or kResNone, -}
     const uint4 *halo;  // [G][halo_stride] {node, slot, publication index of its owner's record, -}
-    const float4 *tcoef;  // [27][nOff][3] the stencil of each boundary type (the block-surface rows), padded blocks
+    const float4 *tcoef;  // [G][kResTypes][nOff][3] per box, the stencil of each boundary type its nodes have (the
+                          // block-surface rows; the own entry's y >> 16 is the node's index here), padded blocks
     uint32_t own_stride, halo_stride;
     float *pub;         // [2][npub][12] by phase parity: granules {r.xyz, tag} {Ap.xyz, tag} {p.xyz, tag}
     uint32_t npub;
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     __shared__ double red[kFusedShares * (kResNT / 64)];
     __shared__ float4 czA[kLatClasses];
     __shared__ float2 czB[kLatClasses];
-    __shared__ float4 tcf[27 * E::nOff * 3];  // the boundary types' stencils (type 13, the interior, unused)
+    __shared__ float4 tcf[kResTypes * E::nOff * 3];  // the box's boundary types' stencils (not the interior's)
     __shared__ int vote[3];  // the poll rounds' workgroup vote, by round mod 3
     __shared__ double rt[MR ? kFusedShares * kMaxPeers : 1];  // a shard: the ranks' totals, folded in rank order
     // the own entries' r, Ap, x and p: in registers for boxes of <= 3 nodes per thread (C2's 14 x 10 x 10), else
@@ -156,8 +158,8 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     };
     for (uint32_t i = tid; i < hd.x; i += kResNT)
         pl[i] = float4{0.f, 0.f, 0.f, 0.f};
-    for (uint32_t i = tid; i < 27u * E::nOff * 3u; i += kResNT)
-        tcf[i] = ra.tcoef[i];
+    for (uint32_t i = tid; i < (uint32_t)(kResTypes * E::nOff * 3); i += kResNT)
+        tcf[i] = ra.tcoef[(size_t)b * (kResTypes * E::nOff * 3) + i];
 
     if (tid < kLatClasses)
     {
@@ -190,7 +192,9 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         S(u, 6) = __uint_as_float(wx.x), S(u, 7) = __uint_as_float(wx.y), S(u, 8) = __uint_as_float(wx.z);
         if constexpr (!LST)
             sreg[u][9] = sreg[u][10] = sreg[u][11] = 0.f;
-        osc[u] = (e.y & 0xFFFFu) | (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rcls, v ? e.x : kResNone, 0, 0) << 16;
+        // image slot | class << 16 | the box's index of the node's boundary type << 24
+        osc[u] = (e.y & 0xFF00FFFFu) |
+                 (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rcls, v ? e.x : kResNone, 0, 0) << 16;
         m[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmass, v ? 4u * e.x : 4u * kLatOob1, 0, 0));
     }
     // halo entries: their owners' records
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const float rr0[3] = {S(u, 0), S(u, 1), S(u, 2)}, aa0[3] = {S(u, 3), S(u, 4), S(u, 5)},
                         pp0[3] = {po.x, po.y, po.z};
             float rn[3], zz[3], pn[3];
-            fused_form(czA, czB, osc[u] >> 16, alpha, beta, rr0, aa0, pp0, rn, zz, pn);
+            fused_form(czA, czB, (osc[u] >> 16) & 0xFFu, alpha, beta, rr0, aa0, pp0, rn, zz, pn);
 #pragma unroll
             for (int c = 0; c < 3; ++c)
             {
@@ -450,10 +454,10 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const float4 q0 = LST ? pl[c0] : float4{S(u, 9), S(u, 10), S(u, 11), 0.f};
             const float u0[3] = {q0.x, q0.y, q0.z};
             float acc[3];
-            const uint32_t cls = osc[u] >> 16, ty = cls >> 3;  // boundary type (lo / inside / hi along x, y, z)
+            const uint32_t cls = (osc[u] >> 16) & 0xFFu, ty = cls >> 3;  // boundary type (lo / inside / hi: x, y, z)
             if (ty != 13u)  // a block-surface node: its type's stencil (the cell form's pair blocks of the cells that
             {               // exist, summed per offset at plan time), every offset on its own
-                const float4 *tb = tcf + ty * (uint32_t)(E::nOff * 3);
+                const float4 *tb = tcf + (osc[u] >> 24) * (uint32_t)(E::nOff * 3);
                 f2 acc01 = {0.f, 0.f};
                 float acc2 = 0.f;
                 const f2 u0xy = {u0[0], u0[1]};
@@ -596,6 +600,17 @@ void launch_resident_n(const DevSys &s, const ResArgs &ra, unsigned G, size_t ld
 }
 
 template <int NPT, int NPH, bool MR>
+size_t res_static_lds(const DevSys &s)
+{
+    const auto k = s.t.lhex ? (s.t.lsym ? k_pcg_resident<true, LatHex, NPT, NPH, MR>
+                                        : k_pcg_resident<false, LatHex, NPT, NPH, MR>)
+                            : (s.t.lsym ? k_pcg_resident<true, LatKuhn, NPT, NPH, MR>
+                                        : k_pcg_resident<false, LatKuhn, NPT, NPH, MR>);
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k)) == hipSuccess ? a.sharedSizeBytes : 0;
+}
+
+template <int NPT, int NPH, bool MR>
 int res_bpc(const DevSys &s, size_t lds)
 {
     int bpc = 0;
@@ -616,6 +631,13 @@ int res_bpc(const DevSys &s, size_t lds)
 // the instantiations: <= 3 own + 2 halo entries per thread, state in registers (boxes of <= 1,536 nodes and <= 1,024
 // ring entries: C2's 14 x 10 x 10), or <= 4 + 3 with the state in LDS (<= 2,048 nodes, <= 1,536 entries: the C3 / 8
 // slab's 19 x 19 x 5); 2 waves per SIMD, one workgroup per CU, no scratch
+size_t resident_static_lds(const DevSys &s, bool small, bool shard)
+{
+    if (small)
+        return shard ? res_static_lds<3, 2, true>(s) : res_static_lds<3, 2, false>(s);
+    return shard ? res_static_lds<4, 3, true>(s) : res_static_lds<4, 3, false>(s);
+}
+
 int resident_blocks_per_cu(const DevSys &s, unsigned npt, unsigned nph, size_t lds, bool shard)
 {
     if (npt <= 3 && nph <= 2)

@@ -146,3 +146,23 @@ def test_resident_stepper_steps(monkeypatch):
     for what in (Stepper.DISPLACEMENT, Stepper.VELOCITY):
         ur, uf = ref.get_state(what), fast.get_state(what)
         assert np.linalg.norm(uf - ur) <= 1e-4 * np.linalg.norm(ur)
+
+
+@pytest.mark.parametrize("element", ["tet4", "hex8"])
+def test_resident_c3_slab_block_follows_two_kernels(element, monkeypatch):
+    """The C3/8 slab's size (149 x 149 x 19 cells, 427k nodes): the 4-node instantiation with r, Ap, x in LDS and the
+    box's own boundary-type stencils only (hex8: the 27-offset table of the box's types is what lets its image fit
+    the LDS). After 3 and 20 fixed iterations x within 1e-5 of the two-kernel schedule's (CWF_FUSED=0)."""
+    case = scenarios.block_case(149, 149, 19, h=0.1, element=element, tol=1e-30, max_iterations=20)
+    rhs = case.static_rhs()
+    sr = _system(case, monkeypatch)
+    e = "LatHex" if element == "hex8" else "LatKuhn"
+    assert _kernel(sr) == f"k_pcg_resident<true, {e}, 4, 3, false>", _kernel(sr)
+    sk = _system(case, monkeypatch, fused="0")
+    assert _kernel(sk).startswith("k_keff_lattice"), _kernel(sk)
+    for its in (3, 20):
+        tr, xr, _ = _solve(sr, rhs, its, 1e-30)
+        tk, xk, _ = _solve(sk, rhs, its, 1e-30)
+        assert tr.iterations == tk.iterations == its
+        d = np.linalg.norm(xr.astype(np.float64) - xk) / np.linalg.norm(xk.astype(np.float64))
+        assert d <= 1e-5, (its, d)
