@@ -226,10 +226,12 @@ bool plan_resident(cwf_hip_system *h, bool shard)
         max_halo = std::max<unsigned>(max_halo, (unsigned)halol[b].size());
         halo_total += halol[b].size();
     }
-    // each box's boundary types (its block-surface nodes'), in ascending order; the own entry carries the node's
-    // index among them in y >> 24 (the kernel's stencil table holds only the box's types)
+    // the 4-node instantiation (LDS state): each box's boundary types (its block-surface nodes'), in ascending
+    // order; the own entry carries the node's index among them in y >> 24 (the kernel's stencil table holds only the
+    // box's types: the LDS the image needs). The 3-node one keeps all 27.
+    const bool small0 = (max_own + kResThreads - 1) / kResThreads <= 3 && (max_halo + kResThreads - 1) / kResThreads <= 2;
     std::vector<uint8_t> btypes((size_t)G * kResTypesHost, 0);
-    for (unsigned b = 0; b < G; ++b)
+    for (unsigned b = 0; b < G && !small0; ++b)
     {
         int idx[27];
         std::fill(idx, idx + 27, -1);
@@ -303,14 +305,14 @@ bool plan_resident(cwf_hip_system *h, bool shard)
             q[2] = float4{(float)S[8], 0.f, 0.f, 0.f};
         }
     }
-    std::vector<float4> btco((size_t)G * kResTypesHost * noff * 3, float4{0.f, 0.f, 0.f, 0.f});
-    for (unsigned b = 0; b < G; ++b)
+    std::vector<float4> btco(small ? 0 : (size_t)G * kResTypesHost * noff * 3, float4{0.f, 0.f, 0.f, 0.f});
+    for (unsigned b = 0; b < G && !small; ++b)
         for (unsigned k = 0; k < kResTypesHost; ++k)
             std::copy(tco.begin() + (size_t)3 * noff * btypes[(size_t)b * kResTypesHost + k],
                       tco.begin() + (size_t)3 * noff * (btypes[(size_t)b * kResTypesHost + k] + 1),
                       btco.begin() + ((size_t)b * kResTypesHost + k) * 3 * noff);
     float4 *dtc;
-    if (upload(h, &dtc, btco.data(), btco.size()))
+    if (small ? upload(h, &dtc, tco.data(), tco.size()) : upload(h, &dtc, btco.data(), btco.size()))
         return false;
     uint4 *dh, *dow, *dha;
     float *dpub;

@@ -53,8 +53,9 @@ struct ResArgs
     const uint4 *hdr;   // [G] {LDS slots, -, PX, PXY}: the box's (sx + 2)(sy + 2)(sz + 2) image and its strides
     const uint4 *own;   // [G][own_stride] {node, image slot, publication index or kResNone, -}
     const uint4 *halo;  // [G][halo_stride] {node, slot, publication index of its owner's record, -}
-    const float4 *tcoef;  // [G][kResTypes][nOff][3] per box, the stencil of each boundary type its nodes have (the
-                          // block-surface rows; the own entry's y >> 16 is the node's index here), padded blocks
+    const float4 *tcoef;  // the stencil of each boundary type (the block-surface rows), padded blocks: [27][nOff][3]
+                          // for the register-state instantiation; for the LDS-state one [G][kResTypes][nOff][3], per
+                          // box only the types its nodes have (the own entry's y >> 24 is the node's index there)
     uint32_t own_stride, halo_stride;
     float *pub;         // [2][npub][12] by phase parity: granules {r.xyz, tag} {Ap.xyz, tag} {p.xyz, tag}
     uint32_t npub;
@@ -131,13 +132,14 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     __shared__ double red[kFusedShares * (kResNT / 64)];
     __shared__ float4 czA[kLatClasses];
     __shared__ float2 czB[kLatClasses];
-    __shared__ float4 tcf[kResTypes * E::nOff * 3];  // the box's boundary types' stencils (not the interior's)
+    constexpr bool LST = NPT > 3;
+    constexpr int kTT = LST ? kResTypes : 27;  // the box's boundary types (LST: the LDS the image needs) or all 27
+    __shared__ float4 tcf[kTT * E::nOff * 3];  // the boundary types' stencils (not the interior's)
     __shared__ int vote[3];  // the poll rounds' workgroup vote, by round mod 3
     __shared__ double rt[MR ? kFusedShares * kMaxPeers : 1];  // a shard: the ranks' totals, folded in rank order
     // the own entries' r, Ap, x and p: in registers for boxes of <= 3 nodes per thread (C2's 14 x 10 x 10), else
     // (LST) r, Ap, x in LDS (lane-linear: conflict-free) and p in the image (each slot formed by one thread), so 4
     // nodes per thread fit without spilling (the C3 / 8 slab's 19 x 19 x 5; LDS state cost C2 0.9 us per phase)
-    constexpr bool LST = NPT > 3;
     __shared__ float st[LST ? 9 : 1][LST ? NPT * kResNT : 1];
     float sreg[LST ? 1 : NPT][LST ? 1 : 12];  // r, Ap, x, p
     const auto S = [&](int u, int q) -> float & {  // q: 0-2 r, 3-5 Ap, 6-8 x (9-11 p: registers only)
@@ -158,8 +160,8 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     };
     for (uint32_t i = tid; i < hd.x; i += kResNT)
         pl[i] = float4{0.f, 0.f, 0.f, 0.f};
-    for (uint32_t i = tid; i < (uint32_t)(kResTypes * E::nOff * 3); i += kResNT)
-        tcf[i] = ra.tcoef[(size_t)b * (kResTypes * E::nOff * 3) + i];
+    for (uint32_t i = tid; i < (uint32_t)(kTT * E::nOff * 3); i += kResNT)
+        tcf[i] = ra.tcoef[(LST ? (size_t)b * (kTT * E::nOff * 3) : 0) + i];
 
     if (tid < kLatClasses)
     {
@@ -192,8 +194,8 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         S(u, 6) = __uint_as_float(wx.x), S(u, 7) = __uint_as_float(wx.y), S(u, 8) = __uint_as_float(wx.z);
         if constexpr (!LST)
             sreg[u][9] = sreg[u][10] = sreg[u][11] = 0.f;
-        // image slot | class << 16 | the box's index of the node's boundary type << 24
-        osc[u] = (e.y & 0xFF00FFFFu) |
+        // image slot | class << 16 (| LST: the box's index of the node's boundary type << 24)
+        osc[u] = (e.y & (LST ? 0xFF00FFFFu : 0xFFFFu)) |
                  (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rcls, v ? e.x : kResNone, 0, 0) << 16;
         m[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmass, v ? 4u * e.x : 4u * kLatOob1, 0, 0));
     }
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const float rr0[3] = {S(u, 0), S(u, 1), S(u, 2)}, aa0[3] = {S(u, 3), S(u, 4), S(u, 5)},
                         pp0[3] = {po.x, po.y, po.z};
             float rn[3], zz[3], pn[3];
-            fused_form(czA, czB, (osc[u] >> 16) & 0xFFu, alpha, beta, rr0, aa0, pp0, rn, zz, pn);
+            fused_form(czA, czB, LST ? (osc[u] >> 16) & 0xFFu : osc[u] >> 16, alpha, beta, rr0, aa0, pp0, rn, zz, pn);
 #pragma unroll
             for (int c = 0; c < 3; ++c)
             {
@@ -454,10 +456,10 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const float4 q0 = LST ? pl[c0] : float4{S(u, 9), S(u, 10), S(u, 11), 0.f};
             const float u0[3] = {q0.x, q0.y, q0.z};
             float acc[3];
-            const uint32_t cls = (osc[u] >> 16) & 0xFFu, ty = cls >> 3;  // boundary type (lo / inside / hi: x, y, z)
+            const uint32_t cls = LST ? (osc[u] >> 16) & 0xFFu : osc[u] >> 16, ty = cls >> 3;  // boundary type
             if (ty != 13u)  // a block-surface node: its type's stencil (the cell form's pair blocks of the cells that
             {               // exist, summed per offset at plan time), every offset on its own
-                const float4 *tb = tcf + (osc[u] >> 24) * (uint32_t)(E::nOff * 3);
+                const float4 *tb = tcf + (LST ? osc[u] >> 24 : ty) * (uint32_t)(E::nOff * 3);
                 f2 acc01 = {0.f, 0.f};
                 float acc2 = 0.f;
                 const f2 u0xy = {u0[0], u0[1]};

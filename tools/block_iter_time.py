@@ -31,11 +31,14 @@ def main():
         else:
             os.environ["CWF_FUSED"] = fused
         s = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, *case.scalars(), mode=_lib.MODE_FAST)
-        for _ in range(2):
+        reps = int(os.environ.get("BLK_REPEAT", "1"))  # timed solves after the first (each printed when > 1)
+        for k in range(1 + reps):
             x = np.zeros_like(rhs)
             t0 = time.perf_counter()
             t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(its, 1e-30), pcg.PcgVectors(x, None)).value()
             el = time.perf_counter() - t0
+            if reps > 1 and k:
+                print(f"  solve {k}: {el / max(t.iterations, 1) * 1e6:.2f} us per iteration", flush=True)
         kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
         print(f"{nx}x{ny}x{nz} {element} ({3 * nx * ny * nz / 1e6:.2f}M DOF) { {'resident': 'resident', '1': 'fused'}.get(fused, 'two kernels')}: "
               f"{t.iterations} iterations, {el / max(t.iterations, 1) * 1e6:.2f} us per iteration ({kern})", flush=True)
