@@ -31,17 +31,27 @@ def main():
         else:
             os.environ["CWF_FUSED"] = fused
         s = pcg.MatrixFreeSystem.from_packing(case.packing, case.materials, *case.scalars(), mode=_lib.MODE_FAST)
+        import ctypes as C
+
+        L = _lib.load()
         reps = int(os.environ.get("BLK_REPEAT", "1"))  # timed solves after the first (each printed when > 1)
         for k in range(1 + reps):
             x = np.zeros_like(rhs)
+            L.cwf_hip_system_set_timing(s.handle(), 1)  # the resident solve: its one launch, hipEvent-timed
             t0 = time.perf_counter()
             t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(its, 1e-30), pcg.PcgVectors(x, None)).value()
             el = time.perf_counter() - t0
+            ms, n = C.c_double(), C.c_uint64()
+            L.cwf_hip_system_timing(s.handle(), C.byref(ms), C.byref(n))
+            L.cwf_hip_system_set_timing(s.handle(), 0)
+            kin = ms.value * 1e3 / max(n.value, 1)
             if reps > 1 and k:
-                print(f"  solve {k}: {el / max(t.iterations, 1) * 1e6:.2f} us per iteration", flush=True)
+                print(f"  solve {k}: {el / max(t.iterations, 1) * 1e6:.2f} us per iteration (in-kernel {kin:.2f})",
+                      flush=True)
         kern = (_lib.load().cwf_hip_system_keff_kernel(s.handle()) or b"").decode()
         print(f"{nx}x{ny}x{nz} {element} ({3 * nx * ny * nz / 1e6:.2f}M DOF) { {'resident': 'resident', '1': 'fused'}.get(fused, 'two kernels')}: "
-              f"{t.iterations} iterations, {el / max(t.iterations, 1) * 1e6:.2f} us per iteration ({kern})", flush=True)
+              f"{t.iterations} iterations, {el / max(t.iterations, 1) * 1e6:.2f} us per iteration, in-kernel {kin:.2f} "
+              f"({kern})", flush=True)
         s.close()
 
 
