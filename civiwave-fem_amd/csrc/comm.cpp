@@ -306,9 +306,12 @@ int group_fused(const std::vector<cwf_hip_system *> &g)
     cwf_hip_system *h0 = g[0];
     if (h0->fused_agreed >= 0)
         return h0->fused_agreed == 1;
+    // a shard owning a single node plane keeps the two kernels: the fused launch's ghost-plane forms assume owned
+    // planes on both sides of a brick's first and last plane (slabs one cell thick did not converge fused, LOCAL and
+    // PEER alike; tests/test_gpu_lattice.py::test_thin_slab_shards_take_two_kernels)
     bool mine = true;
     for (cwf_hip_system *h : g)
-        mine = mine && fast_fused(h) && h->ds.t.lat;
+        mine = mine && fast_fused(h) && h->ds.t.lat && h->ds.t.lk1 >= h->ds.t.lk0 + 2;
     // and the exchange inside the launches (PEER: one member per process); and the resident solve (PEER: every
     // iteration in one launch, resident.hip), whose tag base every rank then takes from the largest (the ranks'
     // granules must carry the same tags)

@@ -302,7 +302,8 @@ struct ResidentPlan
     double *sh = nullptr;
     uint32_t tag = 1;  // the next solve's granule tag base (resident.hip: phase j publishes tag + j + 1)
     bool shard = false;         // a PEER slab shard: ghost records in the mailbox, rank totals across ranks
-    uint64_t remote_sends = 0;  // a shard: own records stored into the neighbours' mailboxes per phase
+    uint64_t remote_sends = 0;  // a shard: Ap granules stored into the neighbours' mailboxes per phase
+    uint64_t ghost_total = 0;   // a shard: ghost halo entries over every box (one Ap granule read each per phase)
 };
 
 struct DevBuf
@@ -569,15 +570,15 @@ int peer_fused_begin(cwf_hip_system *h);  // before launch 0: the epoch base; th
 int peer_fused_end(cwf_hip_system *h);    // after the solve: the communicator's epoch = the last launch that pushed
 unsigned pcg_lattice_resident_count(const DevSys &s);  // resident workgroups of the fused launch
 // the resident solve of a PEER slab shard (resident.hip): where its cross-rank granules go and come from. Each mailbox
-// has a resident area by phase parity: the rank totals ([nranks][5] 16-B granules) and the ghost records ([nghost]
-// 48-B records, the ghosts' local order). Per neighbour slot e (the halo plan's k): the neighbour's record area at my
-// send segment; per rank p: p's rank-total area (my slot included)
+// has a resident area by phase parity: the rank totals ([nranks][5] 16-B granules) and the ghosts' Ap granules
+// ([nghost] 16 B, the ghosts' local order). Per neighbour slot e (the halo plan's k): the neighbour's granule area at
+// my send segment; per rank p: p's rank-total area (my slot included)
 struct ResPeerArgs
 {
     uint32_t nranks = 1, rank = 0;
-    float *rdst[2][2] = {};          // [e][parity] neighbour e's ghost records of my segment
-    uint32_t rdst_bytes[2] = {};     // 48 x my segment for e
-    const float *grecv[2] = {};      // [parity] my ghost records (written by the neighbours)
+    float *rdst[2][2] = {};          // [e][parity] neighbour e's ghost granules of my segment
+    uint32_t rdst_bytes[2] = {};     // 16 x my segment for e
+    const float *grecv[2] = {};      // [parity] my ghosts' granules (written by the neighbours)
     uint32_t grecv_bytes = 0;
     uint32_t *tot[kMaxPeers][2] = {};  // [p][parity] rank p's rank-total area (granule (r, q) at 16 (5 r + q))
     const uint32_t *tot_mine[2] = {};  // [parity] my rank-total area

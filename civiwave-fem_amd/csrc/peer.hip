@@ -82,10 +82,11 @@ inline size_t off_gath(int n) { return align256(off_flags() + kFlagLine * (size_
 inline size_t gath_bytes(int n) { return (size_t)kMaxPeerGathers * n * kSlot * sizeof(double); }  // one parity
 inline size_t off_recv(int n) { return align256(off_gath(n) + 2 * gath_bytes(n)); }
 inline size_t recv_bytes(uint64_t nghost) { return kMaxHaloVecs * 3 * nghost * sizeof(float); }  // one parity
-// the resident solve's area after the receive areas (resident.hip): per parity the rank totals, then the ghost records
+// the resident solve's area after the receive areas (resident.hip): per parity the rank totals, then the ghosts' Ap
+// granules
 inline size_t off_res(int n, uint64_t nghost) { return align256(off_recv(n) + 2 * recv_bytes(nghost)); }
 inline size_t res_tot_bytes(int n) { return align256(80ull * (size_t)n); }
-inline size_t res_par_bytes(int n, uint64_t nghost) { return align256(res_tot_bytes(n) + 48ull * nghost); }
+inline size_t res_par_bytes(int n, uint64_t nghost) { return align256(res_tot_bytes(n) + 16ull * nghost); }
 
 struct PeerStep
 {
@@ -541,9 +542,9 @@ void peer_resident_args(const cwf_hip_system *h, ResPeerArgs &pa)
         {
             char *base = static_cast<char *>(cm->peer_mbox[q]) + off_res(n, qg) + par * res_par_bytes(n, qg) +
                          res_tot_bytes(n);
-            pa.rdst[k][par] = reinterpret_cast<float *>(base + 48ull * qoff);
+            pa.rdst[k][par] = reinterpret_cast<float *>(base + 16ull * qoff);
         }
-        pa.rdst_bytes[k] = (uint32_t)(48ull * (h->send_off[k + 1] - h->send_off[k]));
+        pa.rdst_bytes[k] = (uint32_t)(16ull * (h->send_off[k + 1] - h->send_off[k]));
     }
     for (uint32_t par = 0; par < 2; ++par)
     {
@@ -557,7 +558,7 @@ void peer_resident_args(const cwf_hip_system *h, ResPeerArgs &pa)
             pa.tot[p][par] = reinterpret_cast<uint32_t *>(pb + off_res(n, pg) + par * res_par_bytes(n, pg));
         }
     }
-    pa.grecv_bytes = (uint32_t)(48ull * nghost);
+    pa.grecv_bytes = (uint32_t)(16ull * nghost);
 }
 
 int peer_fused_begin(cwf_hip_system *h)

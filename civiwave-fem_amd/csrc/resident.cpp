@@ -22,6 +22,7 @@ constexpr unsigned kResThreads = 512, kResOwn = 4 * kResThreads, kResHalo = 3 * 
 // entries' r, Ap, x in the 4-node instantiation: 72 KB; the class table; the box's boundary types' stencils, at
 // most kResTypesHost of the 27: 8.6 KB with the 15-offset Kuhn stencil, 15.6 KB with the 27-offset hex8 one)
 constexpr unsigned kResTypesHost = 12;  // resident.hip kResTypes
+constexpr unsigned kResGhostHost = 512;  // resident.hip kResGhostMax: a shard box's ghost halo entries (their r, p in LDS)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kResGhost = 0x80000000u;  // a halo entry's source: a ghost record (resident.hip)
 constexpr unsigned kFusedSharesHost = 5;  // kFusedShares (lattice_common.hpp): one 16-B granule each
@@ -198,7 +199,7 @@ bool plan_resident(cwf_hip_system *h, bool shard)
                     }
         max_own = std::max<unsigned>(max_own, (unsigned)ownl[b].size());
     }
-    uint64_t halo_total = 0;
+    uint64_t halo_total = 0, ghost_total = 0;
     std::vector<uint32_t> seen(N, kNone);
     for (unsigned b = 0; b < G; ++b)
     {
@@ -225,6 +226,13 @@ bool plan_resident(cwf_hip_system *h, bool shard)
         std::sort(halol[b].begin(), halol[b].end(), [](const uint4 &a, const uint4 &c) { return a.z < c.z; });
         max_halo = std::max<unsigned>(max_halo, (unsigned)halol[b].size());
         halo_total += halol[b].size();
+        // the ghost entries are the list's tail: the first one's position (the kernel's index into its ghost state)
+        const auto g0 = std::find_if(halol[b].begin(), halol[b].end(), [](const uint4 &e) { return (e.z & kResGhost) != 0; });
+        const uint64_t ng = (uint64_t)(halol[b].end() - g0);
+        if (ng > kResGhostHost)
+            return false;
+        hdr[b].y = (uint32_t)(g0 - halol[b].begin());
+        ghost_total += ng;
     }
     // the 4-node instantiation (LDS state): each box's boundary types (its block-surface nodes'), in ascending
     // order; the own entry carries the node's index among them in y >> 24 (the kernel's stencil table holds only the
@@ -348,6 +356,7 @@ bool plan_resident(cwf_hip_system *h, bool shard)
     rp.sh = dsh;
     rp.shard = shard;
     rp.remote_sends = remote_sends;
+    rp.ghost_total = ghost_total;
     rp.state = 1;
     return true;
 }
@@ -394,7 +403,10 @@ bool resident_on(const cwf_hip_system *h)
 uint64_t resident_offchip_bytes(const cwf_hip_system *h)
 {
     const ResidentPlan &rp = h->res;
-    uint64_t b = 48ull * (rp.halo_total + rp.npub + rp.remote_sends) + 80ull * rp.G * (1ull + rp.G);
+    // 48-B records on chip (read by the ring entries, written by the published nodes); a shard's ghost entries read,
+    // and its send-plane nodes write, one 16-B Ap granule
+    uint64_t b = 48ull * (rp.halo_total - rp.ghost_total + rp.npub) + 16ull * (rp.ghost_total + rp.remote_sends) +
+                 80ull * rp.G * (1ull + rp.G);
     if (rp.shard)  // the rank totals: one rank's stores to every rank, every workgroup's poll of all of them
         b += 80ull * h->nranks * (1ull + rp.G);
     return b;

@@ -44,13 +44,15 @@ constexpr uint32_t kResNone = 0xFFFFFFFFu;
 constexpr uint32_t kResOob = 0xFFFFFF00u;  // a byte offset past every range-checked buffer here, +32 included (no wrap)
 constexpr uint32_t kResGhost = 0x80000000u;  // a halo entry's source: a shard's ghost record (resident.cpp)
 constexpr int kResTypes = 12;  // boundary types one box's own nodes touch, at most (resident.cpp kResTypesHost)
+constexpr int kResGhostMax = 512;  // a shard box's ghost halo entries, at most (resident.cpp kResGhostHost)
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct ResArgs
 {
     Ctl *ctl;
     double *hist;
-    const uint4 *hdr;   // [G] {LDS slots, -, PX, PXY}: the box's (sx + 2)(sy + 2)(sz + 2) image and its strides
+    const uint4 *hdr;   // [G] {LDS slots, first ghost halo entry (a shard), PX, PXY}: the box's (sx + 2)(sy + 2)(sz + 2)
+                        // image and its strides
     const uint4 *own;   // [G][own_stride] {node, image slot, publication index or kResNone, -}
     const uint4 *halo;  // [G][halo_stride] {node, slot, publication index of its owner's record, -}
     const float4 *tcoef;  // the stencil of each boundary type (the block-surface rows), padded blocks: [27][nOff][3]
@@ -65,8 +67,9 @@ struct ResArgs
     uint32_t max_it;
     uint64_t *trace;    // diagnostic (CWF_RESIDENT_TRACE): per workgroup 8 s_memrealtime stamps of phase trace_j
     uint32_t trace_j;
-    // a PEER slab shard (nranks > 1): own records of the send planes also stored into the neighbours' mailboxes, the
-    // ghosts' records read from this rank's, the rank totals stored to every rank and polled from this rank's
+    // a PEER slab shard (nranks > 1): the send planes' Ap_(j-1) granules stored into the neighbours' mailboxes (a ghost's
+    // r and p the receiving box forms itself and keeps, exactly as the owner does), the ghosts' granules read from this
+    // rank's, the rank totals stored to every rank and polled from this rank's
     ResPeerArgs pa;
 };
 
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     __shared__ float4 tcf[kTT * E::nOff * 3];  // the boundary types' stencils (not the interior's)
     __shared__ int vote[3];  // the poll rounds' workgroup vote, by round mod 3
     __shared__ double rt[MR ? kFusedShares * kMaxPeers : 1];  // a shard: the ranks' totals, folded in rank order
+    __shared__ float4 gst[MR ? 2 * kResGhostMax : 1];  // a shard: each ghost entry's r_j, p_j ({r, -} {p, -})
     // the own entries' r, Ap, x and p: in registers for boxes of <= 3 nodes per thread (C2's 14 x 10 x 10), else
     // (LST) r, Ap, x in LDS (lane-linear: conflict-free) and p in the image (each slot formed by one thread), so 4
     // nodes per thread fit without spilling (the C3 / 8 slab's 19 x 19 x 5; LDS state cost C2 0.9 us per phase)
@@ -224,13 +228,10 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         a = ld4_sc1(rpub, po);
         c = ld4_sc1(rpub, po + 16u);
         e = ld4_sc1(rpub, po + 32u);
-        if constexpr (multi)
+        if constexpr (multi)  // a ghost: its owner's Ap_(j-1) granule only
         {
             const __amdgpu_buffer_rsrc_t rg = sized_rsrc(par ? ra.pa.grecv[1] : ra.pa.grecv[0], ra.pa.grecv_bytes);
-            const uint32_t pg = v && gh ? 48u * (hpub[h] & ~kResGhost) : kResOob;
-            a |= ld4_sys(rg, pg);
-            c |= ld4_sys(rg, pg + 16u);
-            e |= ld4_sys(rg, pg + 32u);
+            c |= ld4_sys(rg, v && gh ? 16u * (hpub[h] & ~kResGhost) : kResOob);
         }
     };
     __syncthreads();
@@ -396,6 +397,20 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             pl[slot] = float4{pn[0], pn[1], pn[2], 0.f};
             fused_entry_dots(rn, zz, d);
         }
+        // a shard's ghost entries: their r_(j-1), p_(j-1) as this box formed them last phase (the registers stay as
+        // loaded through the re-reads below, so a ghost formed twice stores the same r_j, p_j)
+        const auto ghost = [&](int h) { return multi && (hpub[h] & kResGhost) != 0u; };
+        const auto gslot = [&](int h) { return 2u * (tid + (uint32_t)h * kResNT - hd.y); };
+        if constexpr (multi)
+            if (j > 0)
+#pragma unroll
+                for (int h = 0; h < NPH; ++h)
+                    if (hn[h] != kResNone && ghost(h))
+                    {
+                        const float4 gr = gst[gslot(h)], gp = gst[gslot(h) + 1u];
+                        hr[h][0] = gr.x, hr[h][1] = gr.y, hr[h][2] = gr.z;
+                        hp[h][0] = gp.x, hp[h][1] = gp.y, hp[h][2] = gp.z;
+                    }
         // the halo's p_j: phase 0 from fast_fused_init's r; later phases from the records requested above, each
         // granule checked for its tag (a record that had not landed is read again: a bounded, voted re-read)
         for (;; ++round)
@@ -408,21 +423,30 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     continue;
                 if (j > 0)
                 {
-                    if (w0[h].w != want || w1[h].w != want || w2[h].w != want)
+                    const bool gh = ghost(h);
+                    if (w1[h].w != want || (!gh && (w0[h].w != want || w2[h].w != want)))
                     {
                         hok = false;
                         continue;
                     }
-                    hr[h][0] = __uint_as_float(w0[h].x), hr[h][1] = __uint_as_float(w0[h].y);
-                    hr[h][2] = __uint_as_float(w0[h].z);
+                    if (!gh)
+                    {
+                        hr[h][0] = __uint_as_float(w0[h].x), hr[h][1] = __uint_as_float(w0[h].y);
+                        hr[h][2] = __uint_as_float(w0[h].z);
+                        hp[h][0] = __uint_as_float(w2[h].x), hp[h][1] = __uint_as_float(w2[h].y);
+                        hp[h][2] = __uint_as_float(w2[h].z);
+                    }
                     ha[h][0] = __uint_as_float(w1[h].x), ha[h][1] = __uint_as_float(w1[h].y);
                     ha[h][2] = __uint_as_float(w1[h].z);
-                    hp[h][0] = __uint_as_float(w2[h].x), hp[h][1] = __uint_as_float(w2[h].y);
-                    hp[h][2] = __uint_as_float(w2[h].z);
                 }
                 float rn[3], zz[3], pn[3];
                 fused_form(czA, czB, hsc[h] >> 16, alpha, beta, hr[h], ha[h], hp[h], rn, zz, pn);
                 pl[hsc[h] & 0xFFFFu] = float4{pn[0], pn[1], pn[2], 0.f};
+                if (ghost(h))
+                {
+                    gst[gslot(h)] = float4{rn[0], rn[1], rn[2], 0.f};
+                    gst[gslot(h) + 1u] = float4{pn[0], pn[1], pn[2], 0.f};
+                }
             }
             if (j == 0)
             {
@@ -537,18 +561,14 @@ __global__ __launch_bounds__(kResNT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             st4_sc1(rpub, po, g0);
             st4_sc1(rpub, po + 16u, g1);
             st4_sc1(rpub, po + 32u, g2);
-            if constexpr (multi)  // a send-plane node: the same record into the neighbour's mailbox, at its ghost position
+            if constexpr (multi)  // a send-plane node: its Ap_j granule into the neighbour's mailbox, at its ghost position
             {
-                const uint32_t jp = j & 1u, e = rw >> 24, pos = 48u * (rw & 0xFFFFFFu);
+                const uint32_t jp = j & 1u, e = rw >> 24, pos = 16u * (rw & 0xFFFFFFu);
                 const __amdgpu_buffer_rsrc_t d0 = sized_rsrc(jp ? ra.pa.rdst[0][1] : ra.pa.rdst[0][0], ra.pa.rdst_bytes[0]),
                                              d1 = sized_rsrc(jp ? ra.pa.rdst[1][1] : ra.pa.rdst[1][0], ra.pa.rdst_bytes[1]);
                 const uint32_t o0 = rw != kResNone && e == 0u ? pos : kResOob, o1 = rw != kResNone && e == 1u ? pos : kResOob;
-                st4_sys(d0, o0, g0);
-                st4_sys(d0, o0 + 16u, g1);
-                st4_sys(d0, o0 + 32u, g2);
-                st4_sys(d1, o1, g0);
-                st4_sys(d1, o1 + 16u, g1);
-                st4_sys(d1, o1 + 32u, g2);
+                st4_sys(d0, o0, g1);
+                st4_sys(d1, o1, g1);
             }
         }
         stamp(j, 4);

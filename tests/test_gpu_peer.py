@@ -214,14 +214,15 @@ def test_peer_resident_slabs(nranks, element):
 
 
 def test_peer_resident_needs_every_rank():
-    """Slabs one cell thick: the ranks owning a single node plane cannot plan a resident solve (a box needs two
-    planes), the last rank (two planes) can; the schedule vote is collective, so every rank runs the fused launch
-    with its in-kernel exchange (schedule 2) and equals the LOCAL solve bit for bit, never a mixed schedule."""
+    """Slabs one cell thick: the ranks owning a single node plane can plan neither a resident solve (a box needs
+    two planes) nor the fused launch, the last rank (two planes) could; the schedule vote is collective, so every
+    rank runs the two kernels (schedule 0) and equals the LOCAL solve bit for bit, never a mixed schedule."""
     shape = (13, 9, 1)
     out = _run(dict(slab=shape, tol=1e-6, max_iterations=800, timing_steps=50), 3)
     glob, tl, xl = _local_slab(shape, 3, 1e-6, 800)
+    assert tl.converged
     for d in out.values():
-        assert d["kernel_after"].startswith("k_pcg_lattice"), d["kernel_after"]
-        assert d["schedule"] == 2, d["schedule"]
+        assert d["kernel_after"].startswith("k_keff_lattice"), d["kernel_after"]
+        assert d["schedule"] == 0, d["schedule"]
         assert d["telemetry"] == (tl.iterations, tl.converged, tl.residual_norm)
     assert_bitwise(_assemble(out, glob.packing.node_count), xl, "PEER one-cell slabs x vs LOCAL")
