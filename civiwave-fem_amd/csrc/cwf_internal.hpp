@@ -31,7 +31,14 @@ uint32_t hex_tile_lanes(uint64_t hexes);
 // fan-group tiles of NT = 256 lanes (group_lanes(), abi.cpp; 128 on request): <= NT groups (one per lane), <= 2 NT nodes
 // (two per lane; 9-bit local ids), <= kGroupSlotsPerLane NT pushed-force slots (padded runs, LDS) and <= 16
 // pushes per tile node (4-bit ranks in the record)
-constexpr uint32_t kGroupSlotsPerLane = 12;
+#ifndef CWF_GROUP_SLOTS
+#define CWF_GROUP_SLOTS 12
+#endif
+#ifndef CWF_GROUP_WAVES
+#define CWF_GROUP_WAVES 1
+#endif
+constexpr uint32_t kGroupSlotsPerLane = CWF_GROUP_SLOTS;
+constexpr int kGroupWavesPerSimd = CWF_GROUP_WAVES;  // k_keff_groups_pipe's minimum waves per SIMD (VGPR cap)
 constexpr uint32_t kGroupMaxRun = 16;
 
 struct DevTiles
@@ -354,6 +361,10 @@ struct cwf_hip_system
     bool inv_fast = false;
     double inv_sK = 0.0, inv_sM = 0.0;
     double *part0 = nullptr, *part1 = nullptr, *part2 = nullptr;  // chunk / block partials
+    // PARITY streamed scalar folds (kernels_parity.hip, single handle, 256-DOF chunks): tagged 16-B chunk-partial
+    // granules [2 chunks] (null: the separate fold kernels) and the tag of the last streamed launch
+    double *fgran = nullptr;
+    uint32_t fgran_tag = 0;
     uint64_t part_cap = 0;
     // FAST-mode internal node renumbering (Morton order of the coordinates): perm[i] = caller's node of
     // internal node i; every vector crossing the ABI is gathered / scattered through it (pbuf: 13N staging)

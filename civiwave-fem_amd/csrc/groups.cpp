@@ -380,10 +380,11 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
         const uint64_t stop = leaf < leaf_end.size() ? leaf_end[leaf] : G;
         nodes.clear();
         const uint64_t p0 = p;
+        uint32_t pslots = 0;  // the tile's slots with runs padded to even lengths (the layout below without spread)
         while (p < stop && p - p0 < nt)
         {
             const Fan &F = fans[order[p]];
-            uint32_t add = 0;
+            uint32_t add = 0, dslots = 0;
             bool long_run = false;
             for (int s = 0; s < slots_used(F); ++s)
             {
@@ -395,9 +396,11 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
                     ++add;
                     nodes.push_back(n);
                 }
+                dslots += (tcnt[n] & 1u) ? 0u : 2u;  // an even run grows by a padded pair
                 long_run |= ++tcnt[n] > kGroupMaxRun;
             }
-            if (nodes.size() > max_nodes || long_run)
+            // a slot budget below 10 per lane (the 4-wave LDS layout) closes the tile at the budget too
+            if (nodes.size() > max_nodes || long_run || pslots + dslots > slot_budget)
             {
                 // undo this group's pushes and new nodes and close the tile before it
                 for (int s = 0; s < slots_used(F); ++s)
@@ -409,6 +412,7 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
                 }
                 break;
             }
+            pslots += dslots;
             ++p;
         }
         if (p == p0)
@@ -443,7 +447,7 @@ int build_group_tiles(const cwf_system_desc *d, GroupTiles &out, uint32_t nt, ui
                 break;
         }
         if (out.max_tile_slots > slot_budget)
-            return -3;  // cannot happen for slot_budget >= 10 nt: <= 8 pushes per group + 1 pad per node
+            return -3;  // cannot happen: the tile closed at the budget (padded without spread)
         cur.assign(start.begin(), start.end());
         if (lanes_by_bank)
         {

@@ -9,6 +9,7 @@
 //    round-to-nearest sum that starts at +0.0 is never -0.0, so adding a +-0 term is a no-op;
 //  * this TU is compiled with -ffp-contract=off (no FMA contraction), IEEE fp64 div/sqrt.
 #include "cwf_internal.hpp"
+#include "knobs.hpp"
 
 #include <algorithm>
 #include <type_traits>
@@ -229,6 +230,23 @@ __device__ __forceinline__ void stage_dtab(const DevSys &s, double *dtab)
 // are the critical path: staging the fp32 operands and forming the products in the chains measured 22 us for
 // the C2 update pass against 14 us without the partials). DOFs of nodes at or past `nlim` (the owned nodes of
 // a shard, or N) are staged as +0.0, an exact no-op in a fold from +0.0. NV = 2: two dots per DOF, {ab, ac}.
+// Streamed scalar folds (the single-handle PCG loop, 256-DOF chunks; kernels below): a producing pass stores each
+// chunk partial as a tagged 16-B granule {partial lo, hi, tag, 0} in ONE write-through (sc1) store, and its
+// workgroup 0 polls them (sc1 loads, served past L1 and the per-XCD L2) and folds them in chunk order while the other
+// workgroups still produce: each granule carries its own tag, so no counter and no ordering between granules is
+// needed (the hand-off form of resident.hip / MI355X_MICROARCH.md). Granule of chunk k, operand c: NC k + c.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gran_rsrc(const double *g)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(g), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ void gran_store(__amdgpu_buffer_rsrc_t rs, uint32_t idx, double v, uint32_t tag)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const u32x4 w = {(uint32_t)b, (uint32_t)(b >> 32), tag, 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, 16u * idx, 0, 16);  // sc1: write-through
+}
+
 constexpr int kChunkRow = 257;
 template <int NV>
 using ChunkTerm = std::conditional_t<NV == 2, double2, double>;
@@ -240,7 +258,7 @@ __device__ __forceinline__ uint32_t chunk_slot(uint32_t d)  // LDS index of the 
 
 template <int NV>
 __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint32_t chunks, double *pab, double *pac,
-                                                  uint32_t blk)
+                                                  uint32_t blk, const double *gran = nullptr, uint32_t tag = 0)
 {
     if (threadIdx.x >= 3u)
         return;
@@ -260,6 +278,14 @@ __device__ __forceinline__ void wg_chunk_partials(const ChunkTerm<NV> *st, uint3
         }
         else
             s0 += row[i];
+    }
+    if (gran)  // streamed: the granules the folding workgroup polls
+    {
+        const __amdgpu_buffer_rsrc_t rs = gran_rsrc(gran);
+        gran_store(rs, NV * k, s0, tag);
+        if constexpr (NV == 2)
+            gran_store(rs, NV * k + 1u, s1, tag);
+        return;
     }
     pab[k] = s0;
     if constexpr (NV == 2)
@@ -664,17 +690,15 @@ __global__ __launch_bounds__(kBlock) void k_dot_chunks_generic(const float *__re
 constexpr int kDotChunksPerBlock = 32;
 constexpr int kDotRow = 257;
 template <int NV>
-__global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
-                                                       const float *__restrict__ c, uint32_t D, uint32_t chunks,
-                                                       double *__restrict__ pab, double *__restrict__ pac,
-                                                       const Ctl *__restrict__ ctl)
+__device__ __forceinline__ void dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
+                                              const float *__restrict__ c, uint32_t D, uint32_t chunks,
+                                              double *__restrict__ pab, double *__restrict__ pac, uint32_t bx,
+                                              const double *gran, uint32_t tag)
 {
     __shared__ float sa[kDotChunksPerBlock * kDotRow];
     __shared__ float sb[kDotChunksPerBlock * kDotRow];
     __shared__ float sc[NV == 2 ? kDotChunksPerBlock * kDotRow : 1];
-    if (ctl && !ctl->active)
-        return;
-    const uint64_t base = (uint64_t)blockIdx.x * kDotChunksPerBlock * 256u;
+    const uint64_t base = (uint64_t)bx * kDotChunksPerBlock * 256u;
     // 16-B loads (4 DOFs per lane and step) when the operands are 16-B aligned (a caller's device pointer need
     // not be); a block's range starts 32 KB into the vector, the tail past D goes scalar
     const bool al = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
@@ -708,7 +732,7 @@ __global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__
     __syncthreads();
     if (threadIdx.x >= kDotChunksPerBlock)
         return;
-    const uint32_t k = blockIdx.x * kDotChunksPerBlock + threadIdx.x;
+    const uint32_t k = bx * kDotChunksPerBlock + threadIdx.x;
     if (k >= chunks)
         return;
     const float *ra = sa + threadIdx.x * kDotRow, *rb = sb + threadIdx.x * kDotRow;
@@ -722,27 +746,84 @@ __global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__
         if constexpr (NV == 2)
             s1 += av * (double)rc[i];
     }
+    if (gran)
+    {
+        const __amdgpu_buffer_rsrc_t rs = gran_rsrc(gran);
+        gran_store(rs, NV * k, s0, tag);
+        if constexpr (NV == 2)
+            gran_store(rs, NV * k + 1u, s1, tag);
+        return;
+    }
     pab[k] = s0;
     if constexpr (NV == 2)
         pac[k] = s1;
 }
 
-// Ordered sequential fold over chunk partials: total += partial[c] in chunk order (pcg.cpp:200). The chain of
-// fp64 adds is inherently serial (each rounding depends on the running sum), so thread 0 of a 256-thread
-// workgroup runs it, from LDS: waves 1-3 stage the next block of partials (coalesced) while thread 0 folds the
-// current one, so the fold runs at the add latency instead of one global load round trip per 8 partials (C2:
-// 117-127 us per scalar kernel with a single thread, r03c profile). t0 / t1 are valid in thread 0.
+template <int NV>
+__global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
+                                                       const float *__restrict__ c, uint32_t D, uint32_t chunks,
+                                                       double *__restrict__ pab, double *__restrict__ pac,
+                                                       const Ctl *__restrict__ ctl)
+{
+    if (ctl && !ctl->active)
+        return;
+    dot_chunks256<NV>(a, b, c, D, chunks, pab, pac, blockIdx.x, nullptr, 0u);
+}
+
+// The ordered chain over one block of NB partials in LDS, fully unrolled with scheduling barriers. A loop of two
+// alternating register sets is rotated by LLVM so that both sets load at the top of each trip: every 32 adds then
+// wait a full LDS round trip (C2's 4,020-partial folds took 28-30 us in the streamed kernels, ~6 ns per add). Here
+// the next set's eight 16-B reads are pinned in front of the current set's 16 dependent adds.
+template <uint32_t NB>
+__device__ __forceinline__ void fold_block(const double2 *v, double &acc)
+{
+    constexpr uint32_t H = 8;  // double2 per set
+    double2 A[H], B[H];
+#pragma unroll
+    for (uint32_t u = 0; u < H; ++u)
+        A[u] = v[u];
+#pragma unroll
+    for (uint32_t i = 0; i < NB / 2u; i += 2u * H)
+    {
+#pragma unroll
+        for (uint32_t u = 0; u < H; ++u)
+            B[u] = v[i + H + u];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (uint32_t u = 0; u < H; ++u)
+        {
+            acc += A[u].x;
+            acc += A[u].y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 2u * H < NB / 2u)
+        {
+#pragma unroll
+            for (uint32_t u = 0; u < H; ++u)
+                A[u] = v[i + 2u * H + u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (uint32_t u = 0; u < H; ++u)
+        {
+            acc += B[u].x;
+            acc += B[u].y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 constexpr int kFoldThreads = 256;
 constexpr uint32_t kFoldBlock = 4096;  // partials per staged block and operand (one block: C2's 4,030 chunks)
+constexpr uint32_t kFoldSub = 256;     // partials per fold_block (a staged block is padded with +0.0 to a multiple)
 template <int NC>
 __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict__ p1, uint32_t count, double &t0,
                          double &t1)
 {
-    // W partials per register set, two sets alternating (ping-pong); a staged block is padded with +0.0 to a
-    // multiple of 2W (a sequential sum from +0.0 is never -0.0, so adding +0.0 is exact) plus W readable slots
-    // for the last set's (unused) prefetch, so the chain runs branch-free. Two operands (NC = 2) are two
-    // independent chains, run by thread 0 (operand 0) and thread 64 (operand 1) in different waves: interleaved
-    // in one thread they measured no faster than back to back (C2 beta 39 us; a ping-pong of both 42-45).
+    // a staged block is padded with +0.0 to a multiple of kFoldSub (a sequential sum from +0.0 is never -0.0, so
+    // adding +0.0 is exact) and folded by fold_block, branch-free. Two operands (NC = 2) are two independent chains,
+    // run by thread 0 (operand 0) and thread 64 (operand 1) in different waves: interleaved in one thread they
+    // measured no faster than back to back (C2 beta 39 us; a ping-pong of both 42-45).
     constexpr uint32_t W = 16, kRow = kFoldBlock + W;
     constexpr uint32_t kStage = NC == 2 ? 128u : 64u;  // the first thread of the staging waves
     __shared__ double2 buf[2][NC][kRow / 2];
@@ -750,7 +831,7 @@ __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict
     const uint32_t nb = (count + kFoldBlock - 1u) / kFoldBlock;
     const auto stage = [&](uint32_t blk, uint32_t first, uint32_t step) {
         const uint32_t b0 = blk * kFoldBlock, n = min(kFoldBlock, count - b0);
-        const uint32_t npad = (n + 2u * W - 1u) / (2u * W) * (2u * W);
+        const uint32_t npad = (n + kFoldSub - 1u) / kFoldSub * kFoldSub;
         double *d0 = reinterpret_cast<double *>(buf[blk & 1u][0]);
         double *d1 = reinterpret_cast<double *>(buf[blk & 1u][NC - 1]);
         for (uint32_t i = first; i < npad; i += step)
@@ -760,36 +841,10 @@ __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict
                 d1[i] = i < n ? p1[b0 + i] : 0.0;
         }
     };
-    // one chain over a padded block: the next set's 16-B LDS reads issue before the current set's dependent adds
-    // (tools/fold_chain_bench.hip: 4.2 ns per add; one set of reads then its adds 4.5, the operands in registers
-    // 2.8 (the v_add_f64 latency), readlane / global-load chains 2-4x slower)
+    // whole kFoldSub-partial sub-blocks through fold_block (its next reads pinned ahead of the adds)
     const auto chain = [](const double2 *v, uint32_t npad, double &acc) {
-        constexpr uint32_t H = W / 2;
-        double2 A[H], B[H];
-#pragma unroll
-        for (uint32_t u = 0; u < H; ++u)
-            A[u] = v[u];
-        for (uint32_t i = 0; i < npad; i += 2u * W)
-        {
-#pragma unroll
-            for (uint32_t u = 0; u < H; ++u)
-                B[u] = v[(i + W) / 2u + u];
-#pragma unroll
-            for (uint32_t u = 0; u < H; ++u)
-            {
-                acc += A[u].x;
-                acc += A[u].y;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < H; ++u)
-                A[u] = v[(i + 2u * W) / 2u + u];  // the block's tail reads the W spare slots past npad (unused)
-#pragma unroll
-            for (uint32_t u = 0; u < H; ++u)
-            {
-                acc += B[u].x;
-                acc += B[u].y;
-            }
-        }
+        for (uint32_t i = 0; i < npad; i += kFoldSub)
+            fold_block<kFoldSub>(v + i / 2u, acc);
     };
     double acc = 0.0;
     if (nb)
@@ -798,7 +853,7 @@ __device__ void fold_seq(const double *__restrict__ p0, const double *__restrict
     for (uint32_t blk = 0; blk < nb; ++blk)
     {
         const uint32_t n = min(kFoldBlock, count - blk * kFoldBlock);
-        const uint32_t npad = (n + 2u * W - 1u) / (2u * W) * (2u * W);
+        const uint32_t npad = (n + kFoldSub - 1u) / kFoldSub * kFoldSub;
         if (threadIdx.x >= kStage)  // the staging waves; the folding threads' waves do nothing else
         {
             if (blk + 1u < nb)
@@ -872,14 +927,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_pcg_init_rho(Ctl *ctl, const d
     }
 }
 
-__global__ __launch_bounds__(kFoldThreads) void k_pcg_alpha(Ctl *ctl, const double *__restrict__ p_pAp, uint32_t count)
+// alpha from the folded p . Ap (pcg.cpp:840-853), thread 0
+__device__ __forceinline__ void alpha_decide(Ctl *ctl, double denom)
 {
-    if (!ctl->active)
-        return;
-    double denom, unused;
-    fold_seq<1>(p_pAp, nullptr, count, denom, unused);
-    if (threadIdx.x)
-        return;
     ctl->denom = denom;
     if (fabs(denom) < 1.0e-18)
     {
@@ -893,16 +943,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_pcg_alpha(Ctl *ctl, const doub
     ctl->alpha_last = alpha;
 }
 
-__global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const double *__restrict__ p_rr,
-                                                           const double *__restrict__ p_rz, uint32_t count,
-                                                           double *__restrict__ hist)
+// residual, convergence and beta from the folded r . r and r . z (pcg.cpp:862-895), thread 0
+__device__ __forceinline__ void beta_decide(Ctl *ctl, double rr, double rz, double *__restrict__ hist)
 {
-    if (!ctl->active)
-        return;
-    double rr, rz;
-    fold_seq<2>(p_rr, p_rz, count, rr, rz);
-    if (threadIdx.x)
-        return;
     const double res = sqrt(rr);
     const unsigned long long it = ctl->iterations;
     ctl->res = res;
@@ -925,6 +968,166 @@ __global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const doubl
     ctl->beta = beta;
     ctl->beta_last = beta;
     ctl->rho = rz;
+}
+
+__global__ __launch_bounds__(kFoldThreads) void k_pcg_alpha(Ctl *ctl, const double *__restrict__ p_pAp, uint32_t count)
+{
+    if (!ctl->active)
+        return;
+    double denom, unused;
+    fold_seq<1>(p_pAp, nullptr, count, denom, unused);
+    if (threadIdx.x == 0)
+        alpha_decide(ctl, denom);
+}
+
+__global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const double *__restrict__ p_rr,
+                                                           const double *__restrict__ p_rz, uint32_t count,
+                                                           double *__restrict__ hist)
+{
+    if (!ctl->active)
+        return;
+    double rr, rz;
+    fold_seq<2>(p_rr, p_rz, count, rr, rz);
+    if (threadIdx.x == 0)
+        beta_decide(ctl, rr, rz, hist);
+}
+
+// The streamed form of fold_seq, run by workgroup 0 of the producing pass. Wave 0 folds: lane c chains operand c
+// (NC <= 2 lanes of one wave: both chains in one instruction stream). Waves 1-3 stage: wave w polls the granules of
+// blocks w - 1, w + 2, ... (kStreamBlock chunks each, every lane its NC kStreamBlock / 64 granules at once, re-polling
+// only those that do not carry the launch's tag yet) into a ring of kStreamRing LDS slots, and publishes each block
+// with an LDS flag; the folding lanes wait on the flag and free the slot when done. So three blocks' polls are in
+// flight while the chain runs, decoupled by LDS flags instead of workgroup barriers. The chain is fold_block, in
+// chunk order: bitwise fold_seq over the partial arrays. Bounded: a granule that never arrives ends the poll (the
+// block is published anyway, the fold returns false and the solve fails).
+constexpr uint32_t kStreamBlock = 256;           // chunks per block (C2: 4,020 chunks in 16 blocks)
+constexpr uint32_t kStreamRing = 6;              // LDS slots
+constexpr uint32_t kStreamRow = kStreamBlock + 16u;  // + the chain's W spare slots
+constexpr uint32_t kStreamMaxRounds = 4000000u;  // poll rounds per block before giving up (>= 4 s)
+template <int NC>
+constexpr uint32_t fold_stream_lds()  // double2 entries of the caller's staging buffer
+{
+    return kStreamRing * NC * (kStreamRow / 2u);
+}
+// bufp: fold_stream_lds<NC>() double2 of LDS (the caller's, so a producing workgroup reuses it for its own staging);
+// t0 (operand 0) and t1 (operand 1) are valid in thread 0
+template <int NC>
+__device__ bool fold_stream(const double *gran, uint32_t count, uint32_t tag, double2 *bufp, double &t0, double &t1)
+{
+    constexpr uint32_t W = 16, kRow = kStreamRow, kStagers = kFoldThreads / 64 - 1;
+    constexpr uint32_t P = kStreamBlock * NC / 64u;  // granules per staging lane and block
+    static_assert(P <= 32u && kStreamBlock % (2u * W) == 0u, "stream block");
+    double *buf = reinterpret_cast<double *>(bufp);  // slot s, operand c: buf + (s NC + c) kRow
+    __shared__ uint32_t ready[kStreamRing], consumed, fail;
+    __shared__ double other;
+    const __amdgpu_buffer_rsrc_t rs = gran_rsrc(gran);
+    const uint32_t nb = (count + kStreamBlock - 1u) / kStreamBlock, wave = threadIdx.x / 64u, lane = threadIdx.x % 64u;
+    if (threadIdx.x < kStreamRing)
+        ready[threadIdx.x] = 0u;
+    if (threadIdx.x == 0)
+    {
+        consumed = 0u;
+        fail = 0u;
+    }
+    __syncthreads();
+    // the producing workgroups' waves share these SIMDs: the chain's dependent adds (and the polls feeding it) issue
+    // first
+    if (wave == 0)
+        __builtin_amdgcn_s_setprio(3);
+    else
+        __builtin_amdgcn_s_setprio(2);
+    if (wave > 0)
+    {
+        for (uint32_t blk = wave - 1u; blk < nb; blk += kStagers)
+        {
+            const uint32_t b0 = blk * kStreamBlock, n = min(kStreamBlock, count - b0), slot = blk % kStreamRing;
+            uint32_t pending = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < P; ++u)
+                pending |= (lane + 64u * u) / NC < n ? 1u << u : 0u;
+            u32x4 g[P];
+            for (uint32_t round = 0; pending; ++round)
+            {
+#pragma unroll
+                for (uint32_t u = 0; u < P; ++u)
+                    if ((pending >> u) & 1u)
+                        g[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (NC * b0 + lane + 64u * u), 0, 16);
+#pragma unroll
+                for (uint32_t u = 0; u < P; ++u)
+                    if (((pending >> u) & 1u) && g[u].z == tag)
+                        pending &= ~(1u << u);
+                if (!pending)
+                    break;
+                if (round >= kStreamMaxRounds)
+                {
+                    __hip_atomic_store(&fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            // the slot is free once the chain has folded block blk - kStreamRing
+            while (blk >= kStreamRing &&
+                   __hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + kStreamRing <= blk)
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (uint32_t u = 0; u < P; ++u)
+            {
+                const uint32_t q = lane + 64u * u, i = q / NC, c = q % NC;
+                buf[(slot * NC + c) * kRow + i] = i < n ? __hiloint2double((int)g[u].y, (int)g[u].x) : 0.0;  // +0.0 pads
+                // (a partial block is padded to the whole block: the chain always folds kStreamBlock terms)
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0)
+                __hip_atomic_store(&ready[slot], blk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    else if (lane < (uint32_t)NC)
+    {
+        double acc = 0.0;
+        for (uint32_t blk = 0; blk < nb; ++blk)
+        {
+            const uint32_t slot = blk % kStreamRing;
+            while (__hip_atomic_load(&ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != blk + 1u)
+                __builtin_amdgcn_s_sleep(1);
+            fold_block<kStreamBlock>(reinterpret_cast<const double2 *>(buf + (slot * NC + lane) * kRow), acc);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0)
+                __hip_atomic_store(&consumed, blk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (lane == 1)
+            other = acc;
+        t0 = acc;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __syncthreads();
+    t1 = NC == 2 ? other : 0.0;
+    return fail == 0u;
+}
+
+__device__ __forceinline__ void stream_fail(Ctl *ctl)
+{
+    ctl->error = CWF_ERR_HIP;
+    ctl->error_iter = (int)ctl->iterations;
+    ctl->active = 0;
+}
+
+// the p . Ap chunk partials (k_dot_chunks256, workgroups 1..) streamed into alpha (k_pcg_alpha, workgroup 0)
+__global__ __launch_bounds__(256) void k_dot_alpha_stream(const float *__restrict__ p, const float *__restrict__ Ap,
+                                                          uint32_t D, uint32_t chunks, Ctl *ctl,
+                                                          const double *gran, uint32_t tag)
+{
+    if (!ctl->active)
+        return;
+    if (blockIdx.x == 0)
+    {
+        __shared__ double2 fbuf[fold_stream_lds<1>()];
+        double denom = 0.0, unused;
+        const bool ok = fold_stream<1>(gran, chunks, tag, fbuf, denom, unused);
+        if (threadIdx.x == 0)
+            ok ? alpha_decide(ctl, denom) : stream_fail(ctl);
+        return;
+    }
+    dot_chunks256<1>(p, Ap, nullptr, D, chunks, nullptr, nullptr, blockIdx.x - 1u, gran, tag);
 }
 
 // ---- node-wise vector phases ----
@@ -1002,17 +1205,32 @@ __global__ __launch_bounds__(kBlock) void k_p_init(DevSys s, const float *__rest
 
 // x += f32(alpha p); r -= f32(alpha Ap); enforce; z = M^-1 r  (pcg.cpp:854-860, 877), and the chunk partials of
 // r . r and r . z (pcg.cpp:862, 883) from the workgroup's own DOFs (wg_chunk_partials)
+// STREAM: workgroup 0 folds the r . r and r . z granules of workgroups 1.. (their nodes: blockIdx - 1) into the
+// residual check and beta (k_pcg_beta's work, fold_stream), gran / tag / hist its arguments
+template <bool STREAM>
 __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__restrict__ rhs,
                                                    const float *__restrict__ inv, const float *__restrict__ p,
                                                    const float *__restrict__ Ap, float *__restrict__ x,
                                                    float *__restrict__ r, float *__restrict__ z,
-                                                   const Ctl *__restrict__ ctl, double *__restrict__ prr,
-                                                   double *__restrict__ prz, uint32_t nlim, uint32_t chunks)
+                                                   Ctl *__restrict__ ctl, double *__restrict__ prr,
+                                                   double *__restrict__ prz, uint32_t nlim, uint32_t chunks,
+                                                   const double *gran, uint32_t tag, double *__restrict__ hist)
 {
-    __shared__ double2 srz[3 * kChunkRow];
+    constexpr uint32_t kSh = STREAM ? std::max<uint32_t>(3u * kChunkRow, fold_stream_lds<2>()) : 3u * kChunkRow;
+    __shared__ double2 srz[kSh];
     if (!ctl->active)
         return;
-    const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+    if constexpr (STREAM)
+        if (blockIdx.x == 0)
+        {
+            double rr = 0.0, rz;
+            const bool ok = fold_stream<2>(gran, chunks, tag, srz, rr, rz);
+            if (threadIdx.x == 0)
+                ok ? beta_decide(ctl, rr, rz, hist) : stream_fail(ctl);
+            return;
+        }
+    const uint32_t bx = STREAM ? blockIdx.x - 1u : blockIdx.x;
+    const uint32_t n = bx * kBlock + threadIdx.x;
     float rv[3] = {0.f, 0.f, 0.f}, zv[3] = {0.f, 0.f, 0.f};
     if (n < s.N)
     {
@@ -1048,7 +1266,7 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
         srz[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
     }
     __syncthreads();
-    wg_chunk_partials<2>(srz, chunks, prr, prz, blockIdx.x);
+    wg_chunk_partials<2>(srz, chunks, prr, prz, bx, STREAM ? gran : nullptr, tag);
 }
 
 // p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
@@ -1072,6 +1290,12 @@ __global__ __launch_bounds__(kBlock) void k_p_update(DevSys s, const float *__re
 }
 
 inline unsigned grid_for(uint32_t n, uint32_t b) { return (n + b - 1) / b; }
+
+inline bool knob_off(const char *name)
+{
+    const char *v = knob(name);
+    return v && v[0] == '0';
+}
 
 }  // namespace
 
@@ -1202,6 +1426,20 @@ void parity_pcg_init(cwf_hip_system *h, const float *rhs, double rel_tol, hipStr
 {
     const DevSys &s = h->ds;
     const uint32_t chunks = parity_chunk_count(h);
+    if (!h->fgran && h->reduction_block == 256 && !knob_off("CWF_PARITY_STREAM"))
+    {
+        // the streamed folds' granules: 2 per chunk, tag 0 (the first streamed launch's tag is 1)
+        void *q = nullptr;
+        const size_t bytes = 32ull * chunks + 64u;
+        if (hipMalloc(&q, bytes) == hipSuccess)
+        {
+            h->owned.push_back(q);
+            h->bytes += bytes;
+            h->fgran = static_cast<double *>(q);
+            h->fgran_tag = 0;
+            (void)hipMemsetAsync(q, 0, bytes, st);
+        }
+    }
     parity_block_jacobi(h, h->inv, st);
     h->inv_fast = false;  // inv now holds the PARITY inverse (not symmetrised, no inv6)
     parity_keff(h, h->x, h->Ap, true, nullptr, st);
@@ -1237,8 +1475,9 @@ void parity_update(cwf_hip_system *h, const float *rhs, double *prr, double *prz
 {
     const uint32_t nlim = h->ds.Nown;
     const bool fused = h->reduction_block == 256;
-    k_update<<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z, h->ctl,
-                                                           fused ? prr : nullptr, prz, nlim, grid_for(3u * nlim, 256u));
+    k_update<false><<<grid_for(h->ds.N, kBlock), kBlock, 0, st>>>(h->ds, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z,
+                                                                  h->ctl, fused ? prr : nullptr, prz, nlim,
+                                                                  grid_for(3u * nlim, 256u), nullptr, 0u, nullptr);
     if (!fused)
         parity_dot_partials_n(3u * nlim, (uint32_t)h->reduction_block, h->r, h->r, h->z, prr, prz, h->ctl, st);
 }
@@ -1258,6 +1497,24 @@ void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, h
 {
     const DevSys &s = h->ds;
     const uint32_t chunks = parity_chunk_count(h);
+    if (h->fgran && h->reduction_block == 256 && s.ptile_nodes && s.Nown == s.N)
+    {
+        // streamed folds: alpha folded by the p . Ap pass's workgroup 0, beta by the update pass's (the same
+        // partials in the same order as below: bitwise the same scalars), two launches fewer per iteration
+        if (e0)
+            (void)hipEventRecord(e0, st);
+        parity_keff_ds(s, h->p, h->Ap, false, h->ctl, st);
+        if (e1)
+            (void)hipEventRecord(e1, st);
+        const uint32_t t1 = ++h->fgran_tag, t2 = ++h->fgran_tag;
+        k_dot_alpha_stream<<<1u + grid_for(chunks, kDotChunksPerBlock), 256, 0, st>>>(h->p, h->Ap, 3u * s.N, chunks,
+                                                                                      h->ctl, h->fgran, t1);
+        k_update<true><<<1u + grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z,
+                                                                      h->ctl, h->part0, h->part1, s.N, chunks,
+                                                                      h->fgran, t2, h->hist);
+        k_p_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
+        return;
+    }
     if (e0)
         (void)hipEventRecord(e0, st);
     parity_keff_dot(h, h->p, h->Ap, h->ctl, h->part0, st);  // + the p . Ap chunk partials

@@ -29,6 +29,8 @@ inline constexpr Knob kKnobs[] = {
     {"CWF_LAT_L", "n: planes per lattice brick (default: about 1024 bricks of 256 threads, at least 4 planes)"},
     {"CWF_PARITY_TILES", "strip: PARITY node tiles of 256 consecutive nodes also on a single handle (default there: "
                          "compact breadth-first tiles and a separate p.Ap partials pass; shards always use strips)"},
+    {"CWF_PARITY_STREAM", "0: the PARITY loop folds alpha / beta in their own kernels (k_pcg_alpha / k_pcg_beta) instead "
+                          "of in workgroup 0 of the pass producing the chunk partials (kernels_parity.hip fold_stream)"},
     // PCG schedule (spmv_tiles.hip, resident.hip)
     {"CWF_RESIDENT", "0: a structured block that fits on chip runs the launch-per-iteration schedules instead of the "
                      "resident one-launch solve (resident.hip; also off whenever CWF_FUSED is set)"},

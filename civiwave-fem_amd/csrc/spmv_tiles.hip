@@ -1122,7 +1122,7 @@ __device__ __forceinline__ void group_forces(uint4 g, const float4 *sxp, const f
 // MONO: one material, D from the kernel arguments (SGPR operands); otherwise the group's material selects
 // a row of the LDS table (<= 16 materials, abi.cpp)
 template <bool ISO, bool SANITIZE, int MODE, int NT, bool MONO>
-__global__ __launch_bounds__(NT) void k_keff_groups_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
+__global__ __launch_bounds__(NT, kGroupWavesPerSimd) void k_keff_groups_pipe(DevSys s, const float *__restrict__ x, PcgArgs pa,
                                                          const uint4 *__restrict__ hdr)
 {
     constexpr int kTab = ISO ? 12 : 36;

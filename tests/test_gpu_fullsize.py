@@ -73,6 +73,28 @@ def test_c2_parity_pcg_25_iterations_bitwise(c2):
     s.close()
 
 
+def test_c2_parity_streamed_folds_match_fold_kernels(c2, monkeypatch):
+    """The default single-handle PARITY loop folds alpha and beta in workgroup 0 of the passes that produce the chunk
+    partials (tagged granules polled while the other workgroups produce: kernels_parity.hip fold_stream); the
+    CWF_PARITY_STREAM=0 loop runs the separate fold kernels. Both must give the same bits over a whole solve to
+    convergence (the 25-iteration test above pins the default against the oracle): x, r, history, telemetry."""
+    rhs = c2.static_rhs()
+    out = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("CWF_PARITY_STREAM", env)
+        s = _system(c2, _lib.MODE_PARITY)
+        x, r = np.zeros_like(rhs), np.zeros_like(rhs)
+        t = pcg.solve_pcg(s, rhs, pcg.PcgSettings(3000, 1e-6), pcg.PcgVectors(x, r)).value()
+        out.append((t, x, r, pcg.residual_history(s)))
+        s.close()
+    (ta, xa, ra, ha), (tb, xb, rb, hb) = out
+    assert ta.converged and (ta.iterations, ta.residual_norm, ta.alpha_last, ta.beta_last) == (
+        tb.iterations, tb.residual_norm, tb.alpha_last, tb.beta_last)
+    assert_bitwise(xa, xb, "C2 x streamed vs fold kernels")
+    assert_bitwise(ra, rb, "C2 r streamed vs fold kernels")
+    assert np.array_equal(ha, hb)
+
+
 @pytest.mark.timeout(900)
 def test_c3_parity_pcg_8_iterations_bitwise(c3):
     """C3's 39,551 reduction chunks span ten 4,096-partial blocks of the ordered scalar folds (C2's 4,020 fit in
