@@ -992,14 +992,15 @@ __global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const doubl
         beta_decide(ctl, rr, rz, hist);
 }
 
-// The streamed form of fold_seq, run by workgroup 0 of the producing pass. Wave 0 folds: lane c chains operand c
-// (NC <= 2 lanes of one wave: both chains in one instruction stream). Waves 1-3 stage: wave w polls the granules of
-// blocks w - 1, w + 2, ... (kStreamBlock chunks each, every lane its NC kStreamBlock / 64 granules at once, re-polling
-// only those that do not carry the launch's tag yet) into a ring of kStreamRing LDS slots, and publishes each block
-// with an LDS flag; the folding lanes wait on the flag and free the slot when done. So three blocks' polls are in
-// flight while the chain runs, decoupled by LDS flags instead of workgroup barriers. The chain is fold_block, in
-// chunk order: bitwise fold_seq over the partial arrays. Bounded: a granule that never arrives ends the poll (the
-// block is published anyway, the fold returns false and the solve fails).
+// The streamed form of fold_seq, run by workgroup 0 of the producing pass. Wave c < NC folds operand c (its lane 0,
+// wave-uniform LDS addresses). The S = 4 - NC other waves stage: staging wave w polls the granules of blocks w,
+// w + S, ... (kStreamBlock chunks each; a block's slot is claimed first, then every lane polls its NC kStreamBlock / 64
+// granules at once, re-polling only those that do not carry the launch's tag yet, and stores each landed value to
+// LDS) into a ring of kStreamRing LDS slots, and publishes the block with an LDS flag; the folding waves wait on the
+// flag and count the block folded when done. So S blocks' polls are in flight while the chains run, decoupled by
+// LDS flags instead of workgroup barriers. The chain is fold_block, in chunk order: bitwise fold_seq over the
+// partial arrays. Bounded: a granule that never arrives ends the poll (the block is published anyway, the fold
+// returns false and the solve fails).
 constexpr uint32_t kStreamBlock = 256;           // chunks per block (C2: 4,020 chunks in 16 blocks)
 constexpr uint32_t kStreamRing = 6;              // LDS slots
 constexpr uint32_t kStreamRow = kStreamBlock + 16u;  // + the chain's W spare slots
@@ -1014,40 +1015,57 @@ constexpr uint32_t fold_stream_lds()  // double2 entries of the caller's staging
 template <int NC>
 __device__ bool fold_stream(const double *gran, uint32_t count, uint32_t tag, double2 *bufp, double &t0, double &t1)
 {
-    constexpr uint32_t W = 16, kRow = kStreamRow, kStagers = kFoldThreads / 64 - 1;
+    constexpr uint32_t W = 16, kRow = kStreamRow, kStagers = kFoldThreads / 64 - NC;
     constexpr uint32_t P = kStreamBlock * NC / 64u;  // granules per staging lane and block
     static_assert(P <= 32u && kStreamBlock % (2u * W) == 0u, "stream block");
     double *buf = reinterpret_cast<double *>(bufp);  // slot s, operand c: buf + (s NC + c) kRow
-    __shared__ uint32_t ready[kStreamRing], consumed, fail;
+    __shared__ uint32_t ready[kStreamRing], consumed[NC], fail;
     __shared__ double other;
     const __amdgpu_buffer_rsrc_t rs = gran_rsrc(gran);
-    const uint32_t nb = (count + kStreamBlock - 1u) / kStreamBlock, wave = threadIdx.x / 64u, lane = threadIdx.x % 64u;
+    const uint32_t nb = (count + kStreamBlock - 1u) / kStreamBlock, lane = threadIdx.x % 64u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64u);  // wave-uniform (scalar LDS addresses)
     if (threadIdx.x < kStreamRing)
         ready[threadIdx.x] = 0u;
+    if (threadIdx.x < (uint32_t)NC)
+        consumed[threadIdx.x] = 0u;
     if (threadIdx.x == 0)
-    {
-        consumed = 0u;
         fail = 0u;
-    }
     __syncthreads();
     // the producing workgroups' waves share these SIMDs: the chain's dependent adds (and the polls feeding it) issue
     // first
-    if (wave == 0)
+    if (wave < (uint32_t)NC)
         __builtin_amdgcn_s_setprio(3);
     else
         __builtin_amdgcn_s_setprio(2);
-    if (wave > 0)
+    if (wave >= (uint32_t)NC)
     {
-        for (uint32_t blk = wave - 1u; blk < nb; blk += kStagers)
+        for (uint32_t blk = wave - NC; blk < nb; blk += kStagers)
         {
             const uint32_t b0 = blk * kStreamBlock, n = min(kStreamBlock, count - b0), slot = blk % kStreamRing;
+            // the slot is free once the chain has folded block blk - kStreamRing (the polls of the next slots are
+            // still ahead of the chain: kStreamRing / kStagers blocks per staging wave)
+            const auto folded = [&]() {  // blocks both chains have folded
+                uint32_t c = __hip_atomic_load(&consumed[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if constexpr (NC == 2)
+                    c = min(c, __hip_atomic_load(&consumed[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                return c;
+            };
+            while (blk >= kStreamRing && folded() + kStreamRing <= blk)
+                __builtin_amdgcn_s_sleep(1);
+            double *row = buf + slot * NC * kRow;
             uint32_t pending = 0;
 #pragma unroll
             for (uint32_t u = 0; u < P; ++u)
-                pending |= (lane + 64u * u) / NC < n ? 1u << u : 0u;
-            u32x4 g[P];
+            {
+                const uint32_t q = lane + 64u * u;
+                if (q / NC < n)
+                    pending |= 1u << u;
+                else
+                    row[(q % NC) * kRow + q / NC] = 0.0;  // +0.0 pads: the chain always folds kStreamBlock terms
+            }
             for (uint32_t round = 0; pending; ++round)
             {
+                u32x4 g[P];
 #pragma unroll
                 for (uint32_t u = 0; u < P; ++u)
                     if ((pending >> u) & 1u)
@@ -1055,7 +1073,11 @@ __device__ bool fold_stream(const double *gran, uint32_t count, uint32_t tag, do
 #pragma unroll
                 for (uint32_t u = 0; u < P; ++u)
                     if (((pending >> u) & 1u) && g[u].z == tag)
+                    {
+                        const uint32_t q = lane + 64u * u;
+                        row[(q % NC) * kRow + q / NC] = __hiloint2double((int)g[u].y, (int)g[u].x);
                         pending &= ~(1u << u);
+                    }
                 if (!pending)
                     break;
                 if (round >= kStreamMaxRounds)
@@ -1065,23 +1087,12 @@ __device__ bool fold_stream(const double *gran, uint32_t count, uint32_t tag, do
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            // the slot is free once the chain has folded block blk - kStreamRing
-            while (blk >= kStreamRing &&
-                   __hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + kStreamRing <= blk)
-                __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (uint32_t u = 0; u < P; ++u)
-            {
-                const uint32_t q = lane + 64u * u, i = q / NC, c = q % NC;
-                buf[(slot * NC + c) * kRow + i] = i < n ? __hiloint2double((int)g[u].y, (int)g[u].x) : 0.0;  // +0.0 pads
-                // (a partial block is padded to the whole block: the chain always folds kStreamBlock terms)
-            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0)
                 __hip_atomic_store(&ready[slot], blk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
-    else if (lane < (uint32_t)NC)
+    else if (lane == 0)
     {
         double acc = 0.0;
         for (uint32_t blk = 0; blk < nb; ++blk)
@@ -1089,12 +1100,11 @@ __device__ bool fold_stream(const double *gran, uint32_t count, uint32_t tag, do
             const uint32_t slot = blk % kStreamRing;
             while (__hip_atomic_load(&ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != blk + 1u)
                 __builtin_amdgcn_s_sleep(1);
-            fold_block<kStreamBlock>(reinterpret_cast<const double2 *>(buf + (slot * NC + lane) * kRow), acc);
+            fold_block<kStreamBlock>(reinterpret_cast<const double2 *>(buf + (slot * NC + wave) * kRow), acc);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0)
-                __hip_atomic_store(&consumed, blk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&consumed[wave], blk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (lane == 1)
+        if (wave == 1)
             other = acc;
         t0 = acc;
     }
