@@ -774,10 +774,9 @@ __global__ __launch_bounds__(256) void k_dot_chunks256(const float *__restrict__
 // alternating register sets is rotated by LLVM so that both sets load at the top of each trip: every 32 adds then
 // wait a full LDS round trip (C2's 4,020-partial folds took 28-30 us in the streamed kernels, ~6 ns per add). Here
 // the next set's eight 16-B reads are pinned in front of the current set's 16 dependent adds.
-template <uint32_t NB>
+template <uint32_t NB, uint32_t H = 8>  // H: double2 per register set (2 sets: 4 H VGPRs)
 __device__ __forceinline__ void fold_block(const double2 *v, double &acc)
 {
-    constexpr uint32_t H = 8;  // double2 per set
     double2 A[H], B[H];
 #pragma unroll
     for (uint32_t u = 0; u < H; ++u)
@@ -1001,6 +1000,10 @@ __global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const doubl
 // LDS flags instead of workgroup barriers. The chain is fold_block, in chunk order: bitwise fold_seq over the
 // partial arrays. Bounded: a granule that never arrives ends the poll (the block is published anyway, the fold
 // returns false and the solve fails).
+#ifndef CWF_ALPHA_FOLD_H
+#define CWF_ALPHA_FOLD_H 16
+#endif
+constexpr uint32_t kAlphaFoldH = CWF_ALPHA_FOLD_H;  // (a build macro for the same-box A/B of the register sets)
 constexpr uint32_t kStreamBlock = 256;           // chunks per block (C2: 4,020 chunks in 16 blocks)
 constexpr uint32_t kStreamRing = 6;              // LDS slots
 constexpr uint32_t kStreamRow = kStreamBlock + 16u;  // + the chain's W spare slots
@@ -1100,7 +1103,10 @@ __device__ bool fold_stream(const double *gran, uint32_t count, uint32_t tag, do
             const uint32_t slot = blk % kStreamRing;
             while (__hip_atomic_load(&ready[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != blk + 1u)
                 __builtin_amdgcn_s_sleep(1);
-            fold_block<kStreamBlock>(reinterpret_cast<const double2 *>(buf + (slot * NC + wave) * kRow), acc);
+            // the alpha pass (NC = 1) runs at 2 waves / SIMD (its LDS): 32-partial register sets; the update pass
+            // keeps 16 (its VGPRs set its occupancy)
+            fold_block<kStreamBlock, NC == 1 ? kAlphaFoldH : 8u>(
+                reinterpret_cast<const double2 *>(buf + (slot * NC + wave) * kRow), acc);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __hip_atomic_store(&consumed[wave], blk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
