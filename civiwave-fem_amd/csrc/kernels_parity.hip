@@ -689,21 +689,22 @@ __global__ __launch_bounds__(kBlock) void k_dot_chunks_generic(const float *__re
 // exact (such a fold is never -0.0), so the tail chunk equals the reference's shorter loop.
 constexpr int kDotChunksPerBlock = 32;
 constexpr int kDotRow = 257;
-template <int NV>
+// (CPB chunks per block; no early return, so a persistent caller can loop over blocks with a barrier in between)
+template <int NV, int CPB = kDotChunksPerBlock>
 __device__ __forceinline__ void dot_chunks256(const float *__restrict__ a, const float *__restrict__ b,
                                               const float *__restrict__ c, uint32_t D, uint32_t chunks,
                                               double *__restrict__ pab, double *__restrict__ pac, uint32_t bx,
                                               const double *gran, uint32_t tag)
 {
-    __shared__ float sa[kDotChunksPerBlock * kDotRow];
-    __shared__ float sb[kDotChunksPerBlock * kDotRow];
-    __shared__ float sc[NV == 2 ? kDotChunksPerBlock * kDotRow : 1];
-    const uint64_t base = (uint64_t)bx * kDotChunksPerBlock * 256u;
+    __shared__ float sa[CPB * kDotRow];
+    __shared__ float sb[CPB * kDotRow];
+    __shared__ float sc[NV == 2 ? CPB * kDotRow : 1];
+    const uint64_t base = (uint64_t)bx * CPB * 256u;
     // 16-B loads (4 DOFs per lane and step) when the operands are 16-B aligned (a caller's device pointer need
     // not be); a block's range starts 32 KB into the vector, the tail past D goes scalar
     const bool al = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
                       reinterpret_cast<uintptr_t>(NV == 2 ? c : a)) & 15u) == 0;
-    for (uint32_t i = 4u * threadIdx.x; i < kDotChunksPerBlock * 256u; i += 1024u)
+    for (uint32_t i = 4u * threadIdx.x; i < CPB * 256u; i += 1024u)
     {
         const uint64_t gi = base + i;
         const uint32_t l = (i >> 8) * kDotRow + (i & 255u);  // 4 consecutive DOFs stay in one row
@@ -730,10 +731,8 @@ __device__ __forceinline__ void dot_chunks256(const float *__restrict__ a, const
             }
     }
     __syncthreads();
-    if (threadIdx.x >= kDotChunksPerBlock)
-        return;
-    const uint32_t k = bx * kDotChunksPerBlock + threadIdx.x;
-    if (k >= chunks)
+    const uint32_t k = bx * CPB + threadIdx.x;
+    if (threadIdx.x >= (uint32_t)CPB || k >= chunks)
         return;
     const float *ra = sa + threadIdx.x * kDotRow, *rb = sb + threadIdx.x * kDotRow;
     const float *rc = sc + (NV == 2 ? threadIdx.x * kDotRow : 0u);
@@ -752,11 +751,13 @@ __device__ __forceinline__ void dot_chunks256(const float *__restrict__ a, const
         gran_store(rs, NV * k, s0, tag);
         if constexpr (NV == 2)
             gran_store(rs, NV * k + 1u, s1, tag);
-        return;
     }
-    pab[k] = s0;
-    if constexpr (NV == 2)
-        pac[k] = s1;
+    else
+    {
+        pab[k] = s0;
+        if constexpr (NV == 2)
+            pac[k] = s1;
+    }
 }
 
 template <int NV>
@@ -1004,7 +1005,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_pcg_beta(Ctl *ctl, const doubl
 #define CWF_ALPHA_FOLD_H 16
 #endif
 constexpr uint32_t kAlphaFoldH = CWF_ALPHA_FOLD_H;  // (a build macro for the same-box A/B of the register sets)
-constexpr uint32_t kStreamBlock = 256;           // chunks per block (C2: 4,020 chunks in 16 blocks)
+constexpr uint32_t kStreamBlock = 256;
+constexpr uint32_t kStreamCPB = 8;         // chunks per block of the streamed p.Ap pass
+// the producing workgroups of the streamed p.Ap / update passes (persistent, in block order). Production, not the
+// chain, bounds both passes (C2, rocprofv3 means, same box: p.Ap + alpha 25.5 / 21.9 / 24.0 us at 128 / 256 / 512;
+// update + beta 31.9 / 28.1 / 29.4 us at 256 / 512 / 768, 29.5 with one workgroup per node block)
+constexpr uint32_t kStreamDotWG = 256;
+constexpr uint32_t kStreamUpdWG = 512;
+// (kStreamBlock: chunks per fold block; C2's 4,020 chunks in 16 blocks)
 constexpr uint32_t kStreamRing = 6;              // LDS slots
 constexpr uint32_t kStreamRow = kStreamBlock + 16u;  // + the chain's W spare slots
 constexpr uint32_t kStreamMaxRounds = 4000000u;  // poll rounds per block before giving up (>= 4 s)
@@ -1143,7 +1151,14 @@ __global__ __launch_bounds__(256) void k_dot_alpha_stream(const float *__restric
             ok ? alpha_decide(ctl, denom) : stream_fail(ctl);
         return;
     }
-    dot_chunks256<1>(p, Ap, nullptr, D, chunks, nullptr, nullptr, blockIdx.x - 1u, gran, tag);
+    // workgroups 1..G walk the blocks in order (block j G + b - 1 in their j-th step), so the partials land roughly in
+    // chunk order while workgroup 0 folds: 8 chunks per block, the first step's land after one round trip
+    const uint32_t nblk = (chunks + kStreamCPB - 1u) / kStreamCPB, G = gridDim.x - 1u;
+    for (uint32_t bx = blockIdx.x - 1u; bx < nblk; bx += G)
+    {
+        dot_chunks256<1, kStreamCPB>(p, Ap, nullptr, D, chunks, nullptr, nullptr, bx, gran, tag);
+        __syncthreads();  // the staging rows are refilled by the next block
+    }
 }
 
 // ---- node-wise vector phases ----
@@ -1245,44 +1260,58 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
                 ok ? beta_decide(ctl, rr, rz, hist) : stream_fail(ctl);
             return;
         }
-    const uint32_t bx = STREAM ? blockIdx.x - 1u : blockIdx.x;
-    const uint32_t n = bx * kBlock + threadIdx.x;
-    float rv[3] = {0.f, 0.f, 0.f}, zv[3] = {0.f, 0.f, 0.f};
-    if (n < s.N)
-    {
-        const double alpha = ctl->alpha;
-        const uint32_t mk = s.mask[n];
+    const auto nodes = [&](uint32_t bx) {
+        const uint32_t n = bx * kBlock + threadIdx.x;
+        float rv[3] = {0.f, 0.f, 0.f}, zv[3] = {0.f, 0.f, 0.f};
+        if (n < s.N)
+        {
+            const double alpha = ctl->alpha;
+            const uint32_t mk = s.mask[n];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+            {
+                const uint32_t d = 3u * n + k;
+                float xv = x[d] + (float)(alpha * (double)p[d]);
+                float rr = r[d] - (float)(alpha * (double)Ap[d]);
+                if (mk & (1u << k))
+                {
+                    xv = rhs[d];
+                    rr = 0.0f;
+                }
+                x[d] = xv;
+                r[d] = rr;
+                rv[k] = rr;
+            }
+            precond_node(inv, n, mk, rv, zv);
+            z[3u * n] = zv[0];
+            z[3u * n + 1] = zv[1];
+            z[3u * n + 2] = zv[2];
+        }
+        if (!prr)  // a reduction chunk other than 256 DOFs: the partials are a separate pass
+            return;
+        const bool own = n < nlim;
 #pragma unroll
         for (int k = 0; k < 3; ++k)
         {
-            const uint32_t d = 3u * n + k;
-            float xv = x[d] + (float)(alpha * (double)p[d]);
-            float rr = r[d] - (float)(alpha * (double)Ap[d]);
-            if (mk & (1u << k))
-            {
-                xv = rhs[d];
-                rr = 0.0f;
-            }
-            x[d] = xv;
-            r[d] = rr;
-            rv[k] = rr;
+            const double r = (double)rv[k];
+            srz[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
         }
-        precond_node(inv, n, mk, rv, zv);
-        z[3u * n] = zv[0];
-        z[3u * n + 1] = zv[1];
-        z[3u * n + 2] = zv[2];
-    }
-    if (!prr)  // a reduction chunk other than 256 DOFs: the partials are a separate pass
-        return;
-    const bool own = n < nlim;
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
+        __syncthreads();
+        wg_chunk_partials<2>(srz, chunks, prr, prz, bx, STREAM ? gran : nullptr, tag);
+    };
+    if constexpr (STREAM)
     {
-        const double r = (double)rv[k];
-        srz[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
+        // workgroups 1..G walk the node blocks in order (block j G + b - 1 in their j-th step), so the partials
+        // land roughly in chunk order while workgroup 0 folds them
+        const uint32_t nblk = (s.N + kBlock - 1u) / kBlock, G = gridDim.x - 1u;
+        for (uint32_t bx = blockIdx.x - 1u; bx < nblk; bx += G)
+        {
+            nodes(bx);
+            __syncthreads();  // srz is restaged by the next block
+        }
     }
-    __syncthreads();
-    wg_chunk_partials<2>(srz, chunks, prr, prz, bx, STREAM ? gran : nullptr, tag);
+    else
+        nodes(blockIdx.x);
 }
 
 // p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
@@ -1523,9 +1552,10 @@ void parity_pcg_iteration(cwf_hip_system *h, const float *rhs, hipStream_t st, h
         if (e1)
             (void)hipEventRecord(e1, st);
         const uint32_t t1 = ++h->fgran_tag, t2 = ++h->fgran_tag;
-        k_dot_alpha_stream<<<1u + grid_for(chunks, kDotChunksPerBlock), 256, 0, st>>>(h->p, h->Ap, 3u * s.N, chunks,
-                                                                                      h->ctl, h->fgran, t1);
-        k_update<true><<<1u + grid_for(s.N, kBlock), kBlock, 0, st>>>(s, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z,
+        const uint32_t gd = std::min(grid_for(chunks, kStreamCPB), kStreamDotWG);
+        const uint32_t gu = std::min(grid_for(s.N, kBlock), kStreamUpdWG);
+        k_dot_alpha_stream<<<1u + gd, 256, 0, st>>>(h->p, h->Ap, 3u * s.N, chunks, h->ctl, h->fgran, t1);
+        k_update<true><<<1u + gu, kBlock, 0, st>>>(s, rhs, h->inv, h->p, h->Ap, h->x, h->r, h->z,
                                                                       h->ctl, h->part0, h->part1, s.N, chunks,
                                                                       h->fgran, t2, h->hist);
         k_p_update<<<grid_for(s.N, kBlock), kBlock, 0, st>>>(s, h->z, h->p, h->ctl);
