@@ -1247,7 +1247,7 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
                                                    double *__restrict__ prz, uint32_t nlim, uint32_t chunks,
                                                    const double *gran, uint32_t tag, double *__restrict__ hist)
 {
-    constexpr uint32_t kSh = STREAM ? std::max<uint32_t>(3u * kChunkRow, fold_stream_lds<2>()) : 3u * kChunkRow;
+    constexpr uint32_t kSh = STREAM ? std::max<uint32_t>(6u * kChunkRow, fold_stream_lds<2>()) : 3u * kChunkRow;
     __shared__ double2 srz[kSh];
     if (!ctl->active)
         return;
@@ -1260,7 +1260,8 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
                 ok ? beta_decide(ctl, rr, rz, hist) : stream_fail(ctl);
             return;
         }
-    const auto nodes = [&](uint32_t bx) {
+    // one node block: x, r, z and (prr) the staged fp64 products of its DOFs in st
+    const auto nodes = [&](uint32_t bx, double2 *st) {
         const uint32_t n = bx * kBlock + threadIdx.x;
         float rv[3] = {0.f, 0.f, 0.f}, zv[3] = {0.f, 0.f, 0.f};
         if (n < s.N)
@@ -1294,24 +1295,33 @@ __global__ __launch_bounds__(kBlock) void k_update(DevSys s, const float *__rest
         for (int k = 0; k < 3; ++k)
         {
             const double r = (double)rv[k];
-            srz[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
+            st[chunk_slot(3u * threadIdx.x + k)] = own ? double2{r * r, r * (double)zv[k]} : double2{0.0, 0.0};
         }
-        __syncthreads();
-        wg_chunk_partials<2>(srz, chunks, prr, prz, bx, STREAM ? gran : nullptr, tag);
     };
     if constexpr (STREAM)
     {
         // workgroups 1..G walk the node blocks in order (block j G + b - 1 in their j-th step), so the partials
-        // land roughly in chunk order while workgroup 0 folds them
+        // land roughly in chunk order while workgroup 0 folds them. The staging rows alternate by step: wave 0's
+        // lanes 0-2 fold block j's chunks while waves 1-3 already load and form block j + G (wave 0 reaches step
+        // j + 1's barrier only after its chains, so block j + 2 G never restages rows still being folded)
         const uint32_t nblk = (s.N + kBlock - 1u) / kBlock, G = gridDim.x - 1u;
-        for (uint32_t bx = blockIdx.x - 1u; bx < nblk; bx += G)
+        uint32_t j = 0;
+        for (uint32_t bx = blockIdx.x - 1u; bx < nblk; bx += G, ++j)
         {
-            nodes(bx);
-            __syncthreads();  // srz is restaged by the next block
+            double2 *st = srz + (j & 1u) * (3u * kChunkRow);
+            nodes(bx, st);
+            __syncthreads();
+            wg_chunk_partials<2>(st, chunks, prr, prz, bx, gran, tag);
         }
     }
     else
-        nodes(blockIdx.x);
+    {
+        nodes(blockIdx.x, srz);
+        if (!prr)
+            return;
+        __syncthreads();
+        wg_chunk_partials<2>(srz, chunks, prr, prz, blockIdx.x);
+    }
 }
 
 // p = f32(double(z) + beta double(p)), constrained -> 0 (pcg.cpp:897-914)
